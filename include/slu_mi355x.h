@@ -1,0 +1,221 @@
+/*
+ * slu_mi355x.h -- C ABI of libslu_mi355x.so, the MI355X-native numeric
+ * factorization engine for SuperLU_DIST.
+ *
+ * Three groups of entry points:
+ *
+ * 1. Drop-in replacements (identical prototypes to the reference):
+ *      pdgstrf  -- SRC/superlu_ddefs.h:530-531, implemented at SRC/pdgstrf.c:242
+ *      psgstrf  -- SRC/superlu_sdefs.h:507,     implemented at SRC/psgstrf.c
+ *      pzgstrf  -- SRC/superlu_zdefs.h:507,     implemented at SRC/pzgstrf.c
+ *      dscatter_l / dscatter_l_1 / dscatter_u   SRC/superlu_ddefs.h:519-528 (+ s/z),
+ *        exported because the reference's pdgstrf.c.o defines them
+ *        (SRC/pdgstrf.c:171 #includes SRC/dscatter.c) and dscatter3d.c.o
+ *        still references them after pdgstrf.c.o is removed.
+ *    pdgstrf reads the MPI communicators in gridinfo_t only to bootstrap RCCL
+ *    (the MPI symbols are resolved from the host process at run time, so this
+ *    library has no link-time MPI dependency).
+ *
+ * 2. Engine API (no MPI): the same factorization driven by a caller that
+ *    bootstraps RCCL itself (bench.py / tests through torch.distributed).
+ *
+ * 3. Front-end helpers used by tests and the benchmark to build LUstructs for
+ *    stencil matrices (geometric nested dissection, supernodal symbolic
+ *    factorization, 2D block-cyclic distribution in the reference layout of
+ *    SRC/pddistribute.c:327-2400).
+ *
+ * All functions are extern "C"; no C++ exception crosses this boundary.
+ */
+#ifndef SLU_MI355X_H
+#define SLU_MI355X_H
+
+#include "slu_abi.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---------------- 1. drop-in entry points ---------------- */
+int_t pdgstrf(superlu_dist_options_t *options, int m, int n, double anorm,
+              dLUstruct_t *LUstruct, gridinfo_t *grid, SuperLUStat_t *stat,
+              int *info);
+int_t psgstrf(superlu_dist_options_t *options, int m, int n, float anorm,
+              sLUstruct_t *LUstruct, gridinfo_t *grid, SuperLUStat_t *stat,
+              int *info);
+int_t pzgstrf(superlu_dist_options_t *options, int m, int n, double anorm,
+              zLUstruct_t *LUstruct, gridinfo_t *grid, SuperLUStat_t *stat,
+              int *info);
+
+void dscatter_l_1(int ib, int ljb, int nsupc, int_t iukp, int_t *xsup,
+                  int klst, int nbrow, int_t lptr, int temp_nbrow,
+                  int_t *usub, int_t *lsub, double *tempv,
+                  int *indirect_thread, int_t **Lrowind_bc_ptr,
+                  double **Lnzval_bc_ptr, gridinfo_t *grid);
+void dscatter_l(int ib, int ljb, int nsupc, int_t iukp, int_t *xsup,
+                int klst, int nbrow, int_t lptr, int temp_nbrow,
+                int_t *usub, int_t *lsub, double *tempv,
+                int *indirect_thread, int *indirect2,
+                int_t **Lrowind_bc_ptr, double **Lnzval_bc_ptr,
+                gridinfo_t *grid);
+void dscatter_u(int ib, int jb, int nsupc, int_t iukp, int_t *xsup,
+                int klst, int nbrow, int_t lptr, int temp_nbrow,
+                int_t *lsub, int_t *usub, double *tempv,
+                int_t **Ufstnz_br_ptr, double **Unzval_br_ptr,
+                gridinfo_t *grid);
+void sscatter_l_1(int ib, int ljb, int nsupc, int_t iukp, int_t *xsup,
+                  int klst, int nbrow, int_t lptr, int temp_nbrow,
+                  int_t *usub, int_t *lsub, float *tempv,
+                  int *indirect_thread, int_t **Lrowind_bc_ptr,
+                  float **Lnzval_bc_ptr, gridinfo_t *grid);
+void sscatter_l(int ib, int ljb, int nsupc, int_t iukp, int_t *xsup,
+                int klst, int nbrow, int_t lptr, int temp_nbrow,
+                int_t *usub, int_t *lsub, float *tempv,
+                int *indirect_thread, int *indirect2,
+                int_t **Lrowind_bc_ptr, float **Lnzval_bc_ptr,
+                gridinfo_t *grid);
+void sscatter_u(int ib, int jb, int nsupc, int_t iukp, int_t *xsup,
+                int klst, int nbrow, int_t lptr, int temp_nbrow,
+                int_t *lsub, int_t *usub, float *tempv,
+                int_t **Ufstnz_br_ptr, float **Unzval_br_ptr,
+                gridinfo_t *grid);
+void zscatter_l_1(int ib, int ljb, int nsupc, int_t iukp, int_t *xsup,
+                  int klst, int nbrow, int_t lptr, int temp_nbrow,
+                  int_t *usub, int_t *lsub, doublecomplex *tempv,
+                  int *indirect_thread, int_t **Lrowind_bc_ptr,
+                  doublecomplex **Lnzval_bc_ptr, gridinfo_t *grid);
+void zscatter_l(int ib, int ljb, int nsupc, int_t iukp, int_t *xsup,
+                int klst, int nbrow, int_t lptr, int temp_nbrow,
+                int_t *usub, int_t *lsub, doublecomplex *tempv,
+                int *indirect_thread, int *indirect2,
+                int_t **Lrowind_bc_ptr, doublecomplex **Lnzval_bc_ptr,
+                gridinfo_t *grid);
+void zscatter_u(int ib, int jb, int nsupc, int_t iukp, int_t *xsup,
+                int klst, int nbrow, int_t lptr, int temp_nbrow,
+                int_t *lsub, int_t *usub, doublecomplex *tempv,
+                int_t **Ufstnz_br_ptr, doublecomplex **Unzval_br_ptr,
+                gridinfo_t *grid);
+
+/* ---------------- 2. engine API ---------------- */
+
+/* value type codes */
+enum { SLU_D = 0, SLU_S = 1, SLU_Z = 2 };
+
+/* One communicator context per 2D grid: RCCL world/row/column communicators
+ * plus the device this rank drives.  uid is an ncclUniqueId (128 bytes)
+ * created by slu_comm_unique_id on world rank 0 and broadcast by the caller.
+ * For a 1x1 grid pass uid = NULL (no RCCL is created). */
+typedef struct slu_comm slu_comm;
+int slu_comm_unique_id(void *uid_out128);
+slu_comm *slu_comm_create(const void *uid128, int nprow, int npcol, int iam,
+                          int device);
+void slu_comm_destroy(slu_comm *c);
+
+/* Engine options (everything the kernels need beyond the LUstruct). */
+typedef struct {
+    int replace_tiny_pivot; /* options->ReplaceTinyPivot */
+    int timing;             /* 1: record per-phase HIP events */
+    int reserved[6];
+} slu_engine_opts;
+
+/* A plan = device-resident factors + every index table the kernels use.
+ * Built from a host LUstruct (any of d/s/z by dtype), once per structure. */
+typedef struct slu_plan slu_plan;
+slu_plan *slu_plan_create(int dtype, void *LUstruct, int n, int nprow,
+                          int npcol, int iam, slu_comm *comm,
+                          const slu_engine_opts *opts, char *err, int errlen);
+/* (Re)load the numeric values of the host LUstruct into HBM. */
+int slu_plan_upload(slu_plan *p);
+/* Numeric factorization on the device (inputs resident in HBM).
+ * anorm is used for the tiny-pivot threshold as in SRC/pdgstrf.c:412-413. */
+int slu_plan_factor(slu_plan *p, double anorm, int *info, int *tiny_pivots);
+/* Copy factors back into the host LUstruct arrays. */
+int slu_plan_download(slu_plan *p);
+void slu_plan_destroy(slu_plan *p);
+
+/* Plan statistics (algorithmic work of one factorization on this rank). */
+typedef struct {
+    int64_t nsupers, nlevels;
+    int64_t n_schur_tiles, n_diag, n_trsm_items;
+    double schur_flops;        /* exact, unpadded: sum 2*nrows*seglen */
+    double schur_flops_padded; /* reference accounting 2*m*ncols*ldu */
+    double panel_flops;        /* diag LU + TRSM + TRSV (SRC/pdgstrf2.c) */
+    double scatter_bytes;      /* 3*sizeof(T)*m*ncols summed */
+    double lu_bytes;           /* device bytes of L and U values */
+    double index_bytes;        /* device bytes of plan index tables */
+    /* timing of the last slu_plan_factor (ms), when opts.timing */
+    double t_total_ms, t_diag_ms, t_trsm_ms, t_schur_ms, t_comm_ms;
+    double t_schur_big_ms;     /* Schur launches of levels with >= 1 big GEMM */
+    double schur_big_flops;
+    int64_t n_schur_launches;
+} slu_plan_stats;
+int slu_plan_get_stats(const slu_plan *p, slu_plan_stats *st);
+
+/* Last error string of this thread (empty when none). */
+const char *slu_last_error(void);
+
+/* ---------------- 3. front-end helpers ---------------- */
+
+/* Sparse matrix in compressed-column form, values of the given dtype
+ * (complex = interleaved re,im doubles). */
+typedef struct {
+    int64_t n, nnz;
+    int64_t *colptr; /* n+1 */
+    int64_t *rowind; /* nnz */
+    void *val;       /* nnz values */
+    int dtype;
+} slu_csc;
+
+/* kind: 0 = 2D 5-point, 1 = 3D 7-point, 2 = 3D 27-point.
+ * Row r = (i*ny + j)*nz + l (lexicographic), diagonal diag (+ i*diag_im for
+ * complex), every off-diagonal neighbour = off. */
+slu_csc *slu_gen_stencil(int kind, int nx, int ny, int nz, double diag,
+                         double diag_im, double off, int dtype);
+slu_csc *slu_csc_create(int64_t n, int64_t nnz, const int64_t *colptr,
+                        const int64_t *rowind, const void *val, int dtype);
+void slu_csc_free(slu_csc *A);
+
+/* Geometric nested dissection of an nx*ny*nz grid (nz=1 for 2D).
+ * perm_c[i] = position of column i in the new order (SuperLU convention). */
+int slu_order_nd_grid(int nx, int ny, int nz, int64_t *perm_c);
+
+/* Symbolic factorization of P(A+A^T)P^T (structure of the LU factors when A
+ * is structurally symmetric; a valid superset otherwise).  perm_c is
+ * composed with an etree postorder.  relax / maxsup as sp_ienv_dist(2/3). */
+typedef struct slu_symb slu_symb;
+slu_symb *slu_symbolic(const slu_csc *A, const int64_t *perm_c, int relax,
+                       int maxsup);
+void slu_symb_free(slu_symb *s);
+int64_t slu_symb_nsupers(const slu_symb *s);
+/* copies: xsup (nsupers+1), supno (n), final perm_c (n) */
+void slu_symb_arrays(const slu_symb *s, int64_t *xsup, int64_t *supno,
+                     int64_t *perm_c);
+/* nnz(L) including the diagonal blocks, nnz(U) excluding them */
+void slu_symb_counts(const slu_symb *s, double *nnzL, double *nnzU);
+
+/* Build this rank's LUstruct (dtype-typed dLUstruct_t/sLUstruct_t/zLUstruct_t
+ * allocated by the library) holding P*A*P^T in the layout of
+ * SRC/pddistribute.c, with ToRecv/ToSendD/ToSendR/bufmax filled as there. */
+void *slu_distribute(const slu_symb *s, const slu_csc *A, int nprow,
+                     int npcol, int myrow, int mycol);
+void slu_lustruct_free(void *LUstruct, int dtype);
+
+/* Permuted-matrix helpers for tests: B = P*A*P^T in CSC. */
+slu_csc *slu_permute(const slu_csc *A, const int64_t *perm_c);
+
+/* Flat view of a library-built LUstruct (contiguous *_dat arrays). */
+typedef struct {
+    int64_t nsupers;
+    int_t *xsup, *supno;
+    int_t *Lidx; int64_t Lidx_cnt; long *Lidx_off; /* Lrowind_bc_dat */
+    void *Lval; int64_t Lval_cnt; long *Lval_off;   /* Lnzval_bc_dat */
+    int_t *Uidx; int64_t Uidx_cnt; long *Uidx_off;  /* Ufstnz_br_dat */
+    void *Uval; int64_t Uval_cnt; long *Uval_off;   /* Unzval_br_dat */
+    int *ToRecv, *ToSendD, **ToSendR;
+    int_t bufmax[5];
+} slu_lu_view;
+int slu_lu_get_view(void *LUstruct, int dtype, slu_lu_view *v);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SLU_MI355X_H */

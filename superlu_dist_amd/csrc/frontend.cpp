@@ -1,0 +1,749 @@
+// Front-end: stencil matrices, geometric nested dissection, supernodal symbolic
+// factorization and 2D block-cyclic distribution into the SuperLU_DIST LU
+// layout.  Host C++.  This is the input side of the numeric factorization
+// (the reference's get_perm_c / symbfact / pddistribute stage, SURVEY §8f
+// rows 1 and 3); it exists so that tests and the benchmark can build the
+// LUstruct that pdgstrf consumes without the reference's front-end.
+//
+// Layout produced (SRC/superlu_defs.h:152-190, SRC/pddistribute.c:689-1340):
+//   L block column ljb (PCOL(jb)==mycol):
+//     index = [nblocks, nsupr, {gb, nrows, rows[nrows]}...]   (blocks sorted
+//     by gb, diagonal block first on the diagonal process row)
+//     nzval = nsupr x nsupc column-major
+//   U block row lb (PROW(gb)==myrow):
+//     index = [nblocks, len(nzval), len(index), {jb, nnz, fstnz[nsupc(jb)]}...,
+//              -1]  (blocks sorted by jb)
+//     nzval = concatenated column segments [fstnz, xsup[gb+1])
+//   ToRecv / ToSendD / ToSendR / bufmax as SRC/pddistribute.c:752-801,2370.
+#include "slu_mi355x.h"
+
+#include <algorithm>
+#include <complex>
+#include <cstdlib>
+#include <cstring>
+#include <numeric>
+#include <vector>
+
+using std::vector;
+
+namespace {
+
+size_t vsize(int dtype) { return dtype == SLU_S ? 4 : dtype == SLU_Z ? 16 : 8; }
+
+// ----------------------------------------------------------------------------
+// Nested dissection of a regular grid.
+struct Box { int x0, x1, y0, y1, z0, z1; };
+
+void nd_box(const Box &b, int ny, int nz, vector<int64_t> &order) {
+    int dx = b.x1 - b.x0, dy = b.y1 - b.y0, dz = b.z1 - b.z0;
+    if (dx <= 0 || dy <= 0 || dz <= 0) return;
+    long vol = (long)dx * dy * dz;
+    int mx = std::max(dx, std::max(dy, dz));
+    if (vol <= 32 || mx <= 2) {
+        for (int i = b.x0; i < b.x1; ++i)
+            for (int j = b.y0; j < b.y1; ++j)
+                for (int l = b.z0; l < b.z1; ++l)
+                    order.push_back(((int64_t)i * ny + j) * nz + l);
+        return;
+    }
+    Box lo = b, hi = b, sep = b;
+    if (dx == mx) {
+        int m = b.x0 + dx / 2;
+        lo.x1 = m; hi.x0 = m + 1; sep.x0 = m; sep.x1 = m + 1;
+    } else if (dy == mx) {
+        int m = b.y0 + dy / 2;
+        lo.y1 = m; hi.y0 = m + 1; sep.y0 = m; sep.y1 = m + 1;
+    } else {
+        int m = b.z0 + dz / 2;
+        lo.z1 = m; hi.z0 = m + 1; sep.z0 = m; sep.z1 = m + 1;
+    }
+    nd_box(lo, ny, nz, order);
+    nd_box(hi, ny, nz, order);
+    for (int i = sep.x0; i < sep.x1; ++i)
+        for (int j = sep.y0; j < sep.y1; ++j)
+            for (int l = sep.z0; l < sep.z1; ++l)
+                order.push_back(((int64_t)i * ny + j) * nz + l);
+}
+
+// Symmetric adjacency (no diagonal), CSC-like, sorted rows.
+struct Graph {
+    int64_t n = 0;
+    vector<int64_t> ptr, idx;
+};
+
+Graph sym_pattern(const slu_csc *A, const vector<int64_t> &perm) {
+    int64_t n = A->n;
+    vector<int64_t> cnt(n + 1, 0);
+    for (int64_t j = 0; j < n; ++j)
+        for (int64_t p = A->colptr[j]; p < A->colptr[j + 1]; ++p) {
+            int64_t i = A->rowind[p];
+            if (i == j) continue;
+            cnt[perm[i] + 1]++;
+            cnt[perm[j] + 1]++;
+        }
+    Graph g;
+    g.n = n;
+    g.ptr.assign(n + 1, 0);
+    for (int64_t j = 0; j < n; ++j) g.ptr[j + 1] = g.ptr[j] + cnt[j + 1];
+    g.idx.resize(g.ptr[n]);
+    vector<int64_t> pos(g.ptr.begin(), g.ptr.end() - 1);
+    for (int64_t j = 0; j < n; ++j)
+        for (int64_t p = A->colptr[j]; p < A->colptr[j + 1]; ++p) {
+            int64_t i = A->rowind[p];
+            if (i == j) continue;
+            int64_t pi = perm[i], pj = perm[j];
+            g.idx[pos[pj]++] = pi;
+            g.idx[pos[pi]++] = pj;
+        }
+    // sort + dedupe each column
+    vector<int64_t> nptr(n + 1, 0);
+    int64_t w = 0;
+    for (int64_t j = 0; j < n; ++j) {
+        int64_t b = g.ptr[j], e = g.ptr[j + 1];
+        std::sort(g.idx.begin() + b, g.idx.begin() + e);
+        nptr[j] = w;
+        int64_t last = -1;
+        for (int64_t p = b; p < e; ++p)
+            if (g.idx[p] != last) { last = g.idx[p]; g.idx[w++] = last; }
+    }
+    nptr[n] = w;
+    g.idx.resize(w);
+    g.ptr.swap(nptr);
+    return g;
+}
+
+vector<int64_t> etree_of(const Graph &g) {
+    int64_t n = g.n;
+    vector<int64_t> parent(n, -1), anc(n, -1);
+    for (int64_t k = 0; k < n; ++k) {
+        for (int64_t p = g.ptr[k]; p < g.ptr[k + 1]; ++p) {
+            int64_t i = g.idx[p];
+            if (i >= k) break; // sorted
+            while (true) {
+                int64_t a = anc[i];
+                if (a == k) break;
+                anc[i] = k;
+                if (a == -1) { parent[i] = k; break; }
+                i = a;
+            }
+        }
+    }
+    return parent;
+}
+
+vector<int64_t> postorder(const vector<int64_t> &parent) {
+    int64_t n = parent.size();
+    vector<int64_t> head(n, -1), next(n, -1);
+    // children in increasing order: insert in reverse
+    for (int64_t j = n - 1; j >= 0; --j) {
+        int64_t p = parent[j];
+        if (p >= 0) { next[j] = head[p]; head[p] = j; }
+    }
+    vector<int64_t> post;
+    post.reserve(n);
+    vector<int64_t> stack;
+    for (int64_t r = 0; r < n; ++r) {
+        if (parent[r] != -1) continue;
+        stack.push_back(r);
+        while (!stack.empty()) {
+            int64_t v = stack.back();
+            int64_t c = head[v];
+            if (c != -1) {
+                head[v] = next[c];
+                stack.push_back(c);
+            } else {
+                stack.pop_back();
+                post.push_back(v);
+            }
+        }
+    }
+    return post; // post[k] = node visited k-th
+}
+
+} // namespace
+
+struct slu_symb {
+    int64_t n = 0, nsupers = 0;
+    vector<int64_t> perm;       // final perm_c
+    vector<int64_t> xsup, supno;
+    vector<int64_t> sptr, srows; // struct(L_s) incl. diagonal rows, sorted
+    vector<int64_t> sparent;     // supernodal etree
+    double nnzL = 0, nnzU = 0;
+};
+
+extern "C" {
+
+slu_csc *slu_csc_create(int64_t n, int64_t nnz, const int64_t *colptr,
+                        const int64_t *rowind, const void *val, int dtype) {
+    slu_csc *A = (slu_csc *)calloc(1, sizeof(slu_csc));
+    A->n = n;
+    A->nnz = nnz;
+    A->dtype = dtype;
+    A->colptr = (int64_t *)malloc((n + 1) * sizeof(int64_t));
+    A->rowind = (int64_t *)malloc(std::max<int64_t>(nnz, 1) * sizeof(int64_t));
+    A->val = malloc(std::max<int64_t>(nnz, 1) * vsize(dtype));
+    memcpy(A->colptr, colptr, (n + 1) * sizeof(int64_t));
+    if (nnz) {
+        memcpy(A->rowind, rowind, nnz * sizeof(int64_t));
+        memcpy(A->val, val, nnz * vsize(dtype));
+    }
+    return A;
+}
+
+void slu_csc_free(slu_csc *A) {
+    if (!A) return;
+    free(A->colptr);
+    free(A->rowind);
+    free(A->val);
+    free(A);
+}
+
+slu_csc *slu_gen_stencil(int kind, int nx, int ny, int nz, double diag,
+                         double diag_im, double off, int dtype) {
+    if (kind == 0) nz = 1;
+    int64_t n = (int64_t)nx * ny * nz;
+    int maxnb = kind == 2 ? 27 : kind == 1 ? 7 : 5;
+    slu_csc *A = (slu_csc *)calloc(1, sizeof(slu_csc));
+    A->n = n;
+    A->dtype = dtype;
+    A->colptr = (int64_t *)malloc((n + 1) * sizeof(int64_t));
+    A->rowind = (int64_t *)malloc(n * maxnb * sizeof(int64_t));
+    A->val = malloc(n * maxnb * vsize(dtype));
+    int64_t w = 0;
+    auto put = [&](int64_t r, bool isdiag) {
+        A->rowind[w] = r;
+        if (dtype == SLU_D) ((double *)A->val)[w] = isdiag ? diag : off;
+        else if (dtype == SLU_S) ((float *)A->val)[w] = (float)(isdiag ? diag : off);
+        else {
+            ((double *)A->val)[2 * w] = isdiag ? diag : off;
+            ((double *)A->val)[2 * w + 1] = isdiag ? diag_im : 0.0;
+        }
+        ++w;
+    };
+    int dmin = -1, dmax = 1;
+    for (int i = 0; i < nx; ++i)
+        for (int j = 0; j < ny; ++j)
+            for (int l = 0; l < nz; ++l) {
+                int64_t c = ((int64_t)i * ny + j) * nz + l;
+                A->colptr[c] = w;
+                // neighbours in lexicographic (sorted) order
+                for (int di = dmin; di <= dmax; ++di)
+                    for (int dj = dmin; dj <= dmax; ++dj)
+                        for (int dl = dmin; dl <= dmax; ++dl) {
+                            int nd = (di != 0) + (dj != 0) + (dl != 0);
+                            if (kind == 0 && (dl != 0 || nd > 1)) continue;
+                            if (kind == 1 && nd > 1) continue;
+                            int ii = i + di, jj = j + dj, ll = l + dl;
+                            if (ii < 0 || ii >= nx || jj < 0 || jj >= ny ||
+                                ll < 0 || ll >= nz)
+                                continue;
+                            int64_t r = ((int64_t)ii * ny + jj) * nz + ll;
+                            put(r, nd == 0);
+                        }
+            }
+    A->colptr[n] = w;
+    A->nnz = w;
+    return A;
+}
+
+int slu_order_nd_grid(int nx, int ny, int nz, int64_t *perm_c) {
+    if (nz < 1) nz = 1;
+    vector<int64_t> order;
+    order.reserve((size_t)nx * ny * nz);
+    nd_box(Box{0, nx, 0, ny, 0, nz}, ny, nz, order);
+    int64_t n = (int64_t)nx * ny * nz;
+    if ((int64_t)order.size() != n) return -1;
+    for (int64_t k = 0; k < n; ++k) perm_c[order[k]] = k;
+    return 0;
+}
+
+slu_symb *slu_symbolic(const slu_csc *A, const int64_t *perm_c_in, int relax,
+                       int maxsup) {
+    int64_t n = A->n;
+    if (maxsup < 1) maxsup = 256;
+    if (relax > maxsup) relax = maxsup;
+    vector<int64_t> perm(n);
+    if (perm_c_in) std::copy(perm_c_in, perm_c_in + n, perm.begin());
+    else std::iota(perm.begin(), perm.end(), 0);
+
+    // etree of P(A+A^T)P^T, then compose perm with its postorder
+    Graph g = sym_pattern(A, perm);
+    vector<int64_t> parent = etree_of(g);
+    vector<int64_t> post = postorder(parent);
+    vector<int64_t> pinv(n);
+    for (int64_t k = 0; k < n; ++k) pinv[post[k]] = k;
+    for (int64_t i = 0; i < n; ++i) perm[i] = pinv[perm[i]];
+    g = sym_pattern(A, perm);
+    parent = etree_of(g);
+
+    // column counts (off-diagonal) by row subtrees: O(nnz(L))
+    vector<int64_t> cc(n, 0), mark(n, -1), nchild(n, 0), size(n, 1);
+    for (int64_t i = 0; i < n; ++i) {
+        mark[i] = i;
+        for (int64_t p = g.ptr[i]; p < g.ptr[i + 1]; ++p) {
+            int64_t k = g.idx[p];
+            if (k >= i) break;
+            while (k != -1 && k < i && mark[k] != i) {
+                mark[k] = i;
+                cc[k]++;
+                k = parent[k];
+            }
+        }
+    }
+    for (int64_t j = 0; j < n; ++j)
+        if (parent[j] >= 0) { nchild[parent[j]]++; size[parent[j]] += size[j]; }
+
+    // supernode partition: relaxed subtrees, then fundamental chains
+    vector<int64_t> xsup;
+    xsup.reserve(n / 4 + 2);
+    int64_t j = 0;
+    while (j < n) {
+        // is j the first node of a relaxed subtree?  (postorder: the subtree
+        // rooted at r occupies [r-size[r]+1, r])
+        int64_t r = j;
+        while (parent[r] != -1 && size[parent[r]] <= relax &&
+               parent[r] - size[parent[r]] + 1 == j)
+            r = parent[r];
+        if (size[r] <= relax && r - size[r] + 1 == j) {
+            for (int64_t s = j; s <= r; s += maxsup) xsup.push_back(s);
+            j = r + 1;
+            continue;
+        }
+        // fundamental supernode starting at j
+        xsup.push_back(j);
+        int64_t len = 1;
+        while (j + 1 < n && len < maxsup && parent[j] == j + 1 &&
+               nchild[j + 1] == 1 && cc[j] == cc[j + 1] + 1 &&
+               size[j + 1] > relax) {
+            ++j;
+            ++len;
+        }
+        ++j;
+    }
+    xsup.push_back(n);
+
+    slu_symb *S = new slu_symb;
+    S->n = n;
+    S->perm = perm;
+    S->nsupers = (int64_t)xsup.size() - 1;
+    S->xsup = xsup;
+    S->supno.resize(n);
+    for (int64_t s = 0; s < S->nsupers; ++s)
+        for (int64_t c = xsup[s]; c < xsup[s + 1]; ++c) S->supno[c] = s;
+
+    // supernodal structures
+    int64_t ns = S->nsupers;
+    S->sparent.assign(ns, -1);
+    vector<vector<int64_t>> kids(ns);
+    S->sptr.assign(ns + 1, 0);
+    S->srows.clear();
+    vector<int64_t> mk(n, -1), below;
+    for (int64_t s = 0; s < ns; ++s) {
+        int64_t f = xsup[s], l = xsup[s + 1] - 1;
+        below.clear();
+        for (int64_t c = f; c <= l; ++c)
+            for (int64_t p = g.ptr[c]; p < g.ptr[c + 1]; ++p) {
+                int64_t i = g.idx[p];
+                if (i > l && mk[i] != s) { mk[i] = s; below.push_back(i); }
+            }
+        for (int64_t c : kids[s]) {
+            for (int64_t p = S->sptr[c]; p < S->sptr[c + 1]; ++p) {
+                int64_t i = S->srows[p];
+                if (i > l && mk[i] != s) { mk[i] = s; below.push_back(i); }
+            }
+        }
+        std::sort(below.begin(), below.end());
+        for (int64_t c = f; c <= l; ++c) S->srows.push_back(c);
+        S->srows.insert(S->srows.end(), below.begin(), below.end());
+        S->sptr[s + 1] = S->srows.size();
+        int64_t w = l - f + 1;
+        S->nnzL += (double)w * (w + 1) / 2 + (double)w * below.size();
+        S->nnzU += (double)w * (w - 1) / 2 + (double)w * below.size();
+        if (!below.empty()) {
+            int64_t ps = S->supno[below[0]];
+            S->sparent[s] = ps;
+            kids[ps].push_back(s);
+        }
+    }
+    return S;
+}
+
+void slu_symb_free(slu_symb *s) { delete s; }
+int64_t slu_symb_nsupers(const slu_symb *s) { return s->nsupers; }
+void slu_symb_arrays(const slu_symb *s, int64_t *xsup, int64_t *supno,
+                     int64_t *perm_c) {
+    if (xsup) std::copy(s->xsup.begin(), s->xsup.end(), xsup);
+    if (supno) std::copy(s->supno.begin(), s->supno.end(), supno);
+    if (perm_c) std::copy(s->perm.begin(), s->perm.end(), perm_c);
+}
+void slu_symb_counts(const slu_symb *s, double *nnzL, double *nnzU) {
+    if (nnzL) *nnzL = s->nnzL;
+    if (nnzU) *nnzU = s->nnzU;
+}
+
+slu_csc *slu_permute(const slu_csc *A, const int64_t *perm) {
+    int64_t n = A->n;
+    size_t vs = vsize(A->dtype);
+    vector<int64_t> iperm(n);
+    for (int64_t i = 0; i < n; ++i) iperm[perm[i]] = i;
+    slu_csc *B = (slu_csc *)calloc(1, sizeof(slu_csc));
+    B->n = n;
+    B->nnz = A->nnz;
+    B->dtype = A->dtype;
+    B->colptr = (int64_t *)malloc((n + 1) * sizeof(int64_t));
+    B->rowind = (int64_t *)malloc(std::max<int64_t>(A->nnz, 1) * sizeof(int64_t));
+    B->val = malloc(std::max<int64_t>(A->nnz, 1) * vs);
+    int64_t w = 0;
+    vector<std::pair<int64_t, int64_t>> col;
+    for (int64_t jn = 0; jn < n; ++jn) {
+        B->colptr[jn] = w;
+        int64_t jo = iperm[jn];
+        col.clear();
+        for (int64_t p = A->colptr[jo]; p < A->colptr[jo + 1]; ++p)
+            col.push_back({perm[A->rowind[p]], p});
+        std::sort(col.begin(), col.end());
+        for (auto &e : col) {
+            B->rowind[w] = e.first;
+            memcpy((char *)B->val + w * vs, (char *)A->val + e.second * vs, vs);
+            ++w;
+        }
+    }
+    B->colptr[n] = w;
+    return B;
+}
+
+} // extern "C"
+
+// ----------------------------------------------------------------------------
+// Distribution.
+namespace {
+
+template <typename T, typename LocalLU, typename LUstruct>
+void *distribute_t(const slu_symb *S, const slu_csc *A, int Pr, int Pc,
+                   int myrow, int mycol) {
+    const int64_t n = S->n, ns = S->nsupers;
+    const vector<int64_t> &xsup = S->xsup, &supno = S->supno;
+    slu_csc *B = slu_permute(A, S->perm.data());
+    const T *bval = (const T *)B->val;
+
+    LUstruct *LU = (LUstruct *)calloc(1, sizeof(LUstruct));
+    LU->Glu_persist = (Glu_persist_t *)calloc(1, sizeof(Glu_persist_t));
+    LU->Glu_persist->xsup = (int_t *)malloc((ns + 1) * sizeof(int_t));
+    LU->Glu_persist->supno = (int_t *)malloc(n * sizeof(int_t));
+    std::copy(xsup.begin(), xsup.end(), LU->Glu_persist->xsup);
+    std::copy(supno.begin(), supno.end(), LU->Glu_persist->supno);
+    LocalLU *Llu = (LocalLU *)calloc(1, sizeof(LocalLU));
+    LU->Llu = Llu;
+    LU->dt = sizeof(T) == 4 ? 's' : sizeof(T) == 8 ? 'd' : 'z';
+
+    auto W = [&](int64_t s) { return xsup[s + 1] - xsup[s]; };
+    const int64_t nlc = (ns + Pc - 1) / Pc; // local block columns
+    const int64_t nlr = (ns + Pr - 1) / Pr; // local block rows
+
+    // ---- global buffer maxima (every rank computes the same numbers) ----
+    int_t bufmax[SLU_NBUFFERS] = {0, 0, 0, 0, 0};
+    {
+        vector<int64_t> rowsin(Pr), blksin(Pr);
+        for (int64_t s = 0; s < ns; ++s) {
+            std::fill(rowsin.begin(), rowsin.end(), 0);
+            std::fill(blksin.begin(), blksin.end(), 0);
+            int64_t last = -1;
+            for (int64_t p = S->sptr[s]; p < S->sptr[s + 1]; ++p) {
+                int64_t gb = supno[S->srows[p]];
+                rowsin[gb % Pr]++;
+                if (gb != last) { blksin[gb % Pr]++; last = gb; }
+            }
+            for (int pr = 0; pr < Pr; ++pr)
+                if (rowsin[pr]) {
+                    int64_t len = rowsin[pr];
+                    int64_t len1 = len + SLU_BC_HEADER + blksin[pr] * SLU_LB_DESCRIPTOR;
+                    bufmax[0] = std::max<int64_t>(bufmax[0], len1);
+                    bufmax[1] = std::max<int64_t>(bufmax[1], len * W(s));
+                    bufmax[4] = std::max<int64_t>(bufmax[4], len);
+                }
+            // U block row s: blocks jb (struct rows below diag), per column
+            // process: nnz and index length
+            vector<int64_t> ulen(Pc, 0), uidx(Pc, 0), ublk(Pc, 0);
+            int64_t w = W(s);
+            last = -1;
+            for (int64_t p = S->sptr[s] + w; p < S->sptr[s + 1]; ++p) {
+                int64_t jb = supno[S->srows[p]];
+                ulen[jb % Pc] += w;
+                if (jb != last) { ublk[jb % Pc]++; uidx[jb % Pc] += W(jb); last = jb; }
+            }
+            for (int pc = 0; pc < Pc; ++pc)
+                if (ulen[pc]) {
+                    int64_t len1 = uidx[pc] + SLU_BR_HEADER + ublk[pc] * SLU_UB_DESCRIPTOR;
+                    bufmax[2] = std::max<int64_t>(bufmax[2], len1);
+                    bufmax[3] = std::max<int64_t>(bufmax[3], ulen[pc]);
+                }
+        }
+    }
+    for (int i = 0; i < SLU_NBUFFERS; ++i) Llu->bufmax[i] = bufmax[i];
+
+    // ---- L block columns ----
+    Llu->Lrowind_bc_ptr = (int_t **)calloc(nlc, sizeof(int_t *));
+    Llu->Lnzval_bc_ptr = (T **)calloc(nlc, sizeof(T *));
+    Llu->Lrowind_bc_offset = (long *)malloc(nlc * sizeof(long));
+    Llu->Lnzval_bc_offset = (long *)malloc(nlc * sizeof(long));
+    // sizes first
+    vector<int64_t> lidx_len(nlc, 0), lval_len(nlc, 0);
+    int64_t lidx_tot = 0, lval_tot = 0;
+    for (int64_t jb = mycol; jb < ns; jb += Pc) {
+        int64_t ljb = jb / Pc, len = 0, nb = 0, last = -1;
+        for (int64_t p = S->sptr[jb]; p < S->sptr[jb + 1]; ++p) {
+            int64_t gb = supno[S->srows[p]];
+            if (gb % Pr != myrow) continue;
+            ++len;
+            if (gb != last) { ++nb; last = gb; }
+        }
+        if (len) {
+            lidx_len[ljb] = len + SLU_BC_HEADER + nb * SLU_LB_DESCRIPTOR;
+            lval_len[ljb] = len * W(jb);
+        }
+    }
+    for (int64_t ljb = 0; ljb < nlc; ++ljb) {
+        if (lidx_len[ljb]) {
+            Llu->Lrowind_bc_offset[ljb] = lidx_tot;
+            Llu->Lnzval_bc_offset[ljb] = lval_tot;
+            lidx_tot += lidx_len[ljb];
+            lval_tot += lval_len[ljb];
+        } else {
+            Llu->Lrowind_bc_offset[ljb] = -1;
+            Llu->Lnzval_bc_offset[ljb] = -1;
+        }
+    }
+    Llu->Lrowind_bc_dat = (int_t *)malloc((lidx_tot + 1) * sizeof(int_t));
+    Llu->Lnzval_bc_dat = (T *)calloc(lval_tot + 1, sizeof(T));
+    Llu->Lrowind_bc_cnt = lidx_tot + 1;
+    Llu->Lnzval_bc_cnt = lval_tot + 1;
+
+    vector<int64_t> rowpos(n, -1);
+    for (int64_t jb = mycol; jb < ns; jb += Pc) {
+        int64_t ljb = jb / Pc;
+        if (!lidx_len[ljb]) continue;
+        int_t *index = Llu->Lrowind_bc_dat + Llu->Lrowind_bc_offset[ljb];
+        T *lusup = Llu->Lnzval_bc_dat + Llu->Lnzval_bc_offset[ljb];
+        Llu->Lrowind_bc_ptr[ljb] = index;
+        Llu->Lnzval_bc_ptr[ljb] = lusup;
+        int64_t nsupr = lval_len[ljb] / W(jb);
+        index[0] = 0;
+        index[1] = nsupr;
+        int64_t w = SLU_BC_HEADER, r = 0, last = -1, desc = -1;
+        for (int64_t p = S->sptr[jb]; p < S->sptr[jb + 1]; ++p) {
+            int64_t gr = S->srows[p], gb = supno[gr];
+            if (gb % Pr != myrow) continue;
+            if (gb != last) {
+                index[0]++;
+                desc = w;
+                index[w++] = gb;
+                index[w++] = 0;
+                last = gb;
+            }
+            index[desc + 1]++;
+            index[w++] = gr;
+            rowpos[gr] = r++;
+        }
+        // values of B in the block column
+        for (int64_t c = xsup[jb]; c < xsup[jb + 1]; ++c) {
+            int64_t cc = c - xsup[jb];
+            for (int64_t p = B->colptr[c]; p < B->colptr[c + 1]; ++p) {
+                int64_t gr = B->rowind[p];
+                if (gr < xsup[jb]) continue;       // U part
+                if (supno[gr] % Pr != myrow) continue;
+                lusup[rowpos[gr] + cc * nsupr] = bval[p];
+            }
+        }
+        for (int64_t p = S->sptr[jb]; p < S->sptr[jb + 1]; ++p) rowpos[S->srows[p]] = -1;
+    }
+
+    // ---- U block rows ----
+    Llu->Ufstnz_br_ptr = (int_t **)calloc(nlr, sizeof(int_t *));
+    Llu->Unzval_br_ptr = (T **)calloc(nlr, sizeof(T *));
+    Llu->Ufstnz_br_offset = (long *)malloc(nlr * sizeof(long));
+    Llu->Unzval_br_offset = (long *)malloc(nlr * sizeof(long));
+    vector<int64_t> uidx_len(nlr, 0), uval_len(nlr, 0);
+    int64_t uidx_tot = 0, uval_tot = 0;
+    for (int64_t gb = myrow; gb < ns; gb += Pr) {
+        int64_t lb = gb / Pr, w = W(gb), len = 0, idx = 0, nb = 0, last = -1;
+        for (int64_t p = S->sptr[gb] + w; p < S->sptr[gb + 1]; ++p) {
+            int64_t jb = supno[S->srows[p]];
+            if (jb % Pc != mycol) continue;
+            len += w;
+            if (jb != last) { ++nb; idx += W(jb); last = jb; }
+        }
+        if (len) {
+            uidx_len[lb] = idx + SLU_BR_HEADER + nb * SLU_UB_DESCRIPTOR + 1;
+            uval_len[lb] = len;
+        }
+    }
+    for (int64_t lb = 0; lb < nlr; ++lb) {
+        if (uidx_len[lb]) {
+            Llu->Ufstnz_br_offset[lb] = uidx_tot;
+            Llu->Unzval_br_offset[lb] = uval_tot;
+            uidx_tot += uidx_len[lb];
+            uval_tot += uval_len[lb];
+        } else {
+            Llu->Ufstnz_br_offset[lb] = -1;
+            Llu->Unzval_br_offset[lb] = -1;
+        }
+    }
+    Llu->Ufstnz_br_dat = (int_t *)malloc((uidx_tot + 1) * sizeof(int_t));
+    Llu->Unzval_br_dat = (T *)calloc(uval_tot + 1, sizeof(T));
+    Llu->Ufstnz_br_cnt = uidx_tot + 1;
+    Llu->Unzval_br_cnt = uval_tot + 1;
+    // per U block row: value offset of column gc's segment (full segments)
+    vector<int64_t> ucoloff(n, -1);
+    for (int64_t gb = myrow; gb < ns; gb += Pr) {
+        int64_t lb = gb / Pr, w = W(gb);
+        if (!uidx_len[lb]) continue;
+        int_t *index = Llu->Ufstnz_br_dat + Llu->Ufstnz_br_offset[lb];
+        T *uval = Llu->Unzval_br_dat + Llu->Unzval_br_offset[lb];
+        Llu->Ufstnz_br_ptr[lb] = index;
+        Llu->Unzval_br_ptr[lb] = uval;
+        int64_t len1 = uidx_len[lb] - 1;
+        index[0] = 0;
+        index[1] = uval_len[lb];
+        index[2] = len1;
+        index[len1] = -1;
+        int64_t iw = SLU_BR_HEADER, voff = 0, last = -1, desc = -1;
+        for (int64_t p = S->sptr[gb] + w; p < S->sptr[gb + 1]; ++p) {
+            int64_t gc = S->srows[p], jb = supno[gc];
+            if (jb % Pc != mycol) continue;
+            if (jb != last) {
+                index[0]++;
+                desc = iw;
+                index[iw++] = jb;
+                index[iw++] = 0;
+                for (int64_t c = 0; c < W(jb); ++c) index[iw + c] = xsup[gb + 1];
+                iw += W(jb);
+                last = jb;
+            }
+            index[desc + 1] += w;
+            index[desc + 2 + (gc - xsup[jb])] = xsup[gb];
+            ucoloff[gc] = voff;
+            voff += w;
+        }
+        // values: U(gb, gc) for gc in my process column
+        for (int64_t p = S->sptr[gb] + w; p < S->sptr[gb + 1]; ++p) {
+            int64_t gc = S->srows[p];
+            if (supno[gc] % Pc != mycol) continue;
+            for (int64_t q = B->colptr[gc]; q < B->colptr[gc + 1]; ++q) {
+                int64_t gr = B->rowind[q];
+                if (gr < xsup[gb] || gr >= xsup[gb + 1]) continue;
+                uval[ucoloff[gc] + gr - xsup[gb]] = bval[q];
+            }
+        }
+        for (int64_t p = S->sptr[gb] + w; p < S->sptr[gb + 1]; ++p) ucoloff[S->srows[p]] = -1;
+    }
+
+    // ---- communication schedule (SRC/pddistribute.c:752-801) ----
+    Llu->ToRecv = (int *)calloc(ns, sizeof(int));
+    Llu->ToSendD = (int *)calloc(nlr, sizeof(int));
+    Llu->ToSendR = (int **)malloc(nlc * sizeof(int *));
+    int *tsr = (int *)malloc(std::max<int64_t>(nlc * Pc, 1) * sizeof(int));
+    for (int64_t i = 0; i < nlc * Pc; ++i) tsr[i] = SLU_EMPTY;
+    for (int64_t i = 0; i < nlc; ++i) Llu->ToSendR[i] = tsr + i * Pc;
+    for (int64_t gb = 0; gb < ns; ++gb) {
+        int64_t w = W(gb);
+        int kcol = gb % Pc;
+        for (int64_t p = S->sptr[gb] + w; p < S->sptr[gb + 1]; ++p) {
+            int64_t jb = supno[S->srows[p]];
+            int pc = jb % Pc;
+            if (mycol == kcol && mycol != pc) Llu->ToSendR[gb / Pc][pc] = 1;
+            if (mycol == pc) {
+                if (myrow == gb % Pr) {
+                    Llu->ToSendD[gb / Pr] = 1;
+                    Llu->ToRecv[gb] = 1;
+                } else
+                    Llu->ToRecv[gb] = 2;
+            }
+        }
+    }
+    slu_csc_free(B);
+    return LU;
+}
+
+template <typename LocalLU, typename LUstruct>
+void free_t(void *p) {
+    LUstruct *LU = (LUstruct *)p;
+    if (!LU) return;
+    LocalLU *Llu = LU->Llu;
+    if (Llu) {
+        free(Llu->Lrowind_bc_ptr);
+        free(Llu->Lnzval_bc_ptr);
+        free(Llu->Lrowind_bc_offset);
+        free(Llu->Lnzval_bc_offset);
+        free(Llu->Lrowind_bc_dat);
+        free(Llu->Lnzval_bc_dat);
+        free(Llu->Ufstnz_br_ptr);
+        free(Llu->Unzval_br_ptr);
+        free(Llu->Ufstnz_br_offset);
+        free(Llu->Unzval_br_offset);
+        free(Llu->Ufstnz_br_dat);
+        free(Llu->Unzval_br_dat);
+        free(Llu->ToRecv);
+        free(Llu->ToSendD);
+        if (Llu->ToSendR) free(Llu->ToSendR[0]);
+        free(Llu->ToSendR);
+        free(Llu);
+    }
+    if (LU->Glu_persist) {
+        free(LU->Glu_persist->xsup);
+        free(LU->Glu_persist->supno);
+        free(LU->Glu_persist);
+    }
+    free(LU);
+}
+
+} // namespace
+
+namespace {
+template <typename LocalLU, typename LUstruct>
+int view_t(void *p, slu_lu_view *v) {
+    LUstruct *LU = (LUstruct *)p;
+    LocalLU *L = LU->Llu;
+    memset(v, 0, sizeof(*v));
+    v->xsup = LU->Glu_persist->xsup;
+    v->supno = LU->Glu_persist->supno;
+    v->Lidx = L->Lrowind_bc_dat; v->Lidx_cnt = L->Lrowind_bc_cnt; v->Lidx_off = L->Lrowind_bc_offset;
+    v->Lval = L->Lnzval_bc_dat; v->Lval_cnt = L->Lnzval_bc_cnt; v->Lval_off = L->Lnzval_bc_offset;
+    v->Uidx = L->Ufstnz_br_dat; v->Uidx_cnt = L->Ufstnz_br_cnt; v->Uidx_off = L->Ufstnz_br_offset;
+    v->Uval = L->Unzval_br_dat; v->Uval_cnt = L->Unzval_br_cnt; v->Uval_off = L->Unzval_br_offset;
+    v->ToRecv = L->ToRecv; v->ToSendD = L->ToSendD; v->ToSendR = L->ToSendR;
+    for (int i = 0; i < SLU_NBUFFERS; ++i) v->bufmax[i] = L->bufmax[i];
+    return 0;
+}
+
+} // namespace
+
+extern "C" {
+
+void *slu_distribute(const slu_symb *s, const slu_csc *A, int nprow,
+                     int npcol, int myrow, int mycol) {
+    switch (A->dtype) {
+    case SLU_D: return distribute_t<double, dLocalLU_t, dLUstruct_t>(s, A, nprow, npcol, myrow, mycol);
+    case SLU_S: return distribute_t<float, sLocalLU_t, sLUstruct_t>(s, A, nprow, npcol, myrow, mycol);
+    case SLU_Z: return distribute_t<doublecomplex, zLocalLU_t, zLUstruct_t>(s, A, nprow, npcol, myrow, mycol);
+    }
+    return nullptr;
+}
+
+int slu_lu_get_view(void *LU, int dtype, slu_lu_view *v) {
+    switch (dtype) {
+    case SLU_D: return view_t<dLocalLU_t, dLUstruct_t>(LU, v);
+    case SLU_S: return view_t<sLocalLU_t, sLUstruct_t>(LU, v);
+    case SLU_Z: return view_t<zLocalLU_t, zLUstruct_t>(LU, v);
+    }
+    return -1;
+}
+
+void slu_lustruct_free(void *LU, int dtype) {
+    switch (dtype) {
+    case SLU_D: free_t<dLocalLU_t, dLUstruct_t>(LU); break;
+    case SLU_S: free_t<sLocalLU_t, sLUstruct_t>(LU); break;
+    case SLU_Z: free_t<zLocalLU_t, zLUstruct_t>(LU); break;
+    }
+}
+
+} // extern "C"

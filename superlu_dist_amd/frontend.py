@@ -1,0 +1,144 @@
+"""Python side of the front-end helpers (matrix generation, ordering,
+symbolic factorization, distribution).  Thin wrappers over the C++ code in
+``csrc/frontend.cpp``; they build LUstructs in the reference layout
+(SRC/pddistribute.c) for the tests and the benchmark."""
+import ctypes as C
+
+import numpy as np
+
+from .lib import (DTYPES, SLU_D, SLU_S, SLU_Z, SluLuView, as_i64p, c_i64p, lib)
+
+STENCIL_2D5, STENCIL_3D7, STENCIL_3D27 = 0, 1, 2
+
+
+class Csc:
+    """Owning handle of a library slu_csc."""
+
+    def __init__(self, ptr):
+        self.ptr = ptr
+
+    @classmethod
+    def stencil(cls, kind, nx, ny, nz=1, diag=None, diag_im=0.0, off=-1.0, dtype=SLU_D):
+        if diag is None:
+            diag = {STENCIL_2D5: 4.0, STENCIL_3D7: 6.0, STENCIL_3D27: 26.0}[kind]
+        return cls(lib().slu_gen_stencil(kind, nx, ny, nz, diag, diag_im, off, dtype))
+
+    @classmethod
+    def from_arrays(cls, n, colptr, rowind, val, dtype):
+        colptr = np.ascontiguousarray(colptr, dtype=np.int64)
+        rowind = np.ascontiguousarray(rowind, dtype=np.int64)
+        val = np.ascontiguousarray(val, dtype=DTYPES[dtype])
+        return cls(lib().slu_csc_create(n, len(rowind), as_i64p(colptr), as_i64p(rowind),
+                                        val.ctypes.data_as(C.c_void_p), dtype))
+
+    @property
+    def n(self):
+        return self.ptr.contents.n
+
+    @property
+    def dtype(self):
+        return self.ptr.contents.dtype
+
+    def arrays(self):
+        s = self.ptr.contents
+        colptr = np.ctypeslib.as_array(s.colptr, shape=(s.n + 1,)).copy()
+        rowind = np.ctypeslib.as_array(s.rowind, shape=(s.nnz,)).copy()
+        npt = DTYPES[s.dtype]
+        buf = (C.c_char * (s.nnz * np.dtype(npt).itemsize)).from_address(s.val)
+        val = np.frombuffer(buf, dtype=npt).copy()
+        return colptr, rowind, val
+
+    def to_dense(self):
+        colptr, rowind, val = self.arrays()
+        n = self.n
+        A = np.zeros((n, n), dtype=val.dtype)
+        for j in range(n):
+            A[rowind[colptr[j]:colptr[j + 1]], j] = val[colptr[j]:colptr[j + 1]]
+        return A
+
+    def permuted(self, perm):
+        perm = np.ascontiguousarray(perm, dtype=np.int64)
+        return Csc(lib().slu_permute(self.ptr, as_i64p(perm)))
+
+    def __del__(self):
+        if getattr(self, "ptr", None):
+            lib().slu_csc_free(self.ptr)
+            self.ptr = None
+
+
+def nd_order(nx, ny, nz=1):
+    perm = np.empty(nx * ny * nz, dtype=np.int64)
+    if lib().slu_order_nd_grid(nx, ny, nz, as_i64p(perm)) != 0:
+        raise RuntimeError("nested dissection failed")
+    return perm
+
+
+class Symbolic:
+    def __init__(self, A, perm_c=None, relax=60, maxsup=256):
+        self.A = A
+        pc = None
+        if perm_c is not None:
+            self._perm_in = np.ascontiguousarray(perm_c, dtype=np.int64)
+            pc = as_i64p(self._perm_in)
+        self.ptr = lib().slu_symbolic(A.ptr, pc, relax, maxsup)
+        self.n = A.n
+        self.nsupers = lib().slu_symb_nsupers(self.ptr)
+        self.xsup = np.empty(self.nsupers + 1, dtype=np.int64)
+        self.supno = np.empty(self.n, dtype=np.int64)
+        self.perm_c = np.empty(self.n, dtype=np.int64)
+        lib().slu_symb_arrays(self.ptr, as_i64p(self.xsup), as_i64p(self.supno),
+                              as_i64p(self.perm_c))
+        a, b = C.c_double(), C.c_double()
+        lib().slu_symb_counts(self.ptr, C.byref(a), C.byref(b))
+        self.nnzL, self.nnzU = a.value, b.value
+
+    def distribute(self, nprow=1, npcol=1, myrow=0, mycol=0):
+        return LUStruct(self, nprow, npcol, myrow, mycol)
+
+    def __del__(self):
+        if getattr(self, "ptr", None):
+            lib().slu_symb_free(self.ptr)
+            self.ptr = None
+
+
+class LUStruct:
+    """One rank's LUstruct (dLUstruct_t / sLUstruct_t / zLUstruct_t) built by
+    the library; exposes its flat arrays as numpy views."""
+
+    def __init__(self, symb, nprow, npcol, myrow, mycol):
+        self.symb = symb
+        self.dtype = symb.A.dtype
+        self.nprow, self.npcol, self.myrow, self.mycol = nprow, npcol, myrow, mycol
+        self.ptr = lib().slu_distribute(symb.ptr, symb.A.ptr, nprow, npcol, myrow, mycol)
+        if not self.ptr:
+            raise RuntimeError("slu_distribute failed")
+        v = SluLuView()
+        lib().slu_lu_get_view(self.ptr, self.dtype, C.byref(v))
+        self.view = v
+        npt = DTYPES[self.dtype]
+        isz = np.dtype(npt).itemsize
+        self.Lidx = np.ctypeslib.as_array(v.Lidx, shape=(v.Lidx_cnt,))
+        self.Uidx = np.ctypeslib.as_array(v.Uidx, shape=(v.Uidx_cnt,))
+        self.Lval = np.frombuffer((C.c_char * (v.Lval_cnt * isz)).from_address(v.Lval), dtype=npt)
+        self.Uval = np.frombuffer((C.c_char * (v.Uval_cnt * isz)).from_address(v.Uval), dtype=npt)
+        ns = symb.nsupers
+        self.nlc = (ns + npcol - 1) // npcol
+        self.nlr = (ns + nprow - 1) // nprow
+        self.Loff = np.ctypeslib.as_array(v.Lidx_off, shape=(self.nlc,))
+        self.Lvoff = np.ctypeslib.as_array(v.Lval_off, shape=(self.nlc,))
+        self.Uoff = np.ctypeslib.as_array(v.Uidx_off, shape=(self.nlr,))
+        self.Uvoff = np.ctypeslib.as_array(v.Uval_off, shape=(self.nlr,))
+        self.ToRecv = np.ctypeslib.as_array(v.ToRecv, shape=(ns,))
+        self.ToSendD = np.ctypeslib.as_array(v.ToSendD, shape=(self.nlr,))
+        self.bufmax = np.array(list(v.bufmax), dtype=np.int64)
+
+    def to_sendr(self):
+        out = np.empty((self.nlc, self.npcol), dtype=np.int32)
+        for i in range(self.nlc):
+            out[i] = np.ctypeslib.as_array(self.view.ToSendR[i], shape=(self.npcol,))
+        return out
+
+    def __del__(self):
+        if getattr(self, "ptr", None):
+            lib().slu_lustruct_free(self.ptr, self.dtype)
+            self.ptr = None

@@ -1,0 +1,112 @@
+"""ctypes binding of libslu_mi355x.so (include/slu_mi355x.h).
+
+The shared library is built in-tree by ``make -C superlu_dist_amd/csrc``
+(``__graft_entry__.build()``).  Nothing here falls back to Python or the CPU:
+a missing library raises immediately.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libslu_mi355x.so")
+
+SLU_D, SLU_S, SLU_Z = 0, 1, 2
+DTYPES = {SLU_D: np.float64, SLU_S: np.float32, SLU_Z: np.complex128}
+DTYPE_CODE = {"d": SLU_D, "s": SLU_S, "z": SLU_Z}
+
+c_i64p = C.POINTER(C.c_int64)
+c_intp = C.POINTER(C.c_int)
+
+
+class SluCsc(C.Structure):
+    _fields_ = [("n", C.c_int64), ("nnz", C.c_int64), ("colptr", c_i64p),
+                ("rowind", c_i64p), ("val", C.c_void_p), ("dtype", C.c_int)]
+
+
+class SluLuView(C.Structure):
+    _fields_ = [("nsupers", C.c_int64), ("xsup", c_i64p), ("supno", c_i64p),
+                ("Lidx", c_i64p), ("Lidx_cnt", C.c_int64), ("Lidx_off", C.POINTER(C.c_long)),
+                ("Lval", C.c_void_p), ("Lval_cnt", C.c_int64), ("Lval_off", C.POINTER(C.c_long)),
+                ("Uidx", c_i64p), ("Uidx_cnt", C.c_int64), ("Uidx_off", C.POINTER(C.c_long)),
+                ("Uval", C.c_void_p), ("Uval_cnt", C.c_int64), ("Uval_off", C.POINTER(C.c_long)),
+                ("ToRecv", c_intp), ("ToSendD", c_intp), ("ToSendR", C.POINTER(c_intp)),
+                ("bufmax", C.c_int64 * 5)]
+
+
+class EngineOpts(C.Structure):
+    _fields_ = [("replace_tiny_pivot", C.c_int), ("timing", C.c_int),
+                ("reserved", C.c_int * 6)]
+
+
+class PlanStats(C.Structure):
+    _fields_ = [("nsupers", C.c_int64), ("nlevels", C.c_int64),
+                ("n_schur_tiles", C.c_int64), ("n_diag", C.c_int64),
+                ("n_trsm_items", C.c_int64),
+                ("schur_flops", C.c_double), ("schur_flops_padded", C.c_double),
+                ("panel_flops", C.c_double), ("scatter_bytes", C.c_double),
+                ("lu_bytes", C.c_double), ("index_bytes", C.c_double),
+                ("t_total_ms", C.c_double), ("t_diag_ms", C.c_double),
+                ("t_trsm_ms", C.c_double), ("t_schur_ms", C.c_double),
+                ("t_comm_ms", C.c_double), ("t_schur_big_ms", C.c_double),
+                ("schur_big_flops", C.c_double), ("n_schur_launches", C.c_int64)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+_lib = None
+
+
+def lib():
+    """Load the in-tree shared library (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(
+            f"{LIB_PATH} missing: run `python -c 'import __graft_entry__ as g; g.build()'`")
+    L = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+    P = C.c_void_p
+    sig = {
+        "slu_gen_stencil": (C.POINTER(SluCsc), [C.c_int, C.c_int, C.c_int, C.c_int,
+                                                C.c_double, C.c_double, C.c_double, C.c_int]),
+        "slu_csc_create": (C.POINTER(SluCsc), [C.c_int64, C.c_int64, c_i64p, c_i64p, P, C.c_int]),
+        "slu_csc_free": (None, [C.POINTER(SluCsc)]),
+        "slu_order_nd_grid": (C.c_int, [C.c_int, C.c_int, C.c_int, c_i64p]),
+        "slu_symbolic": (P, [C.POINTER(SluCsc), c_i64p, C.c_int, C.c_int]),
+        "slu_symb_free": (None, [P]),
+        "slu_symb_nsupers": (C.c_int64, [P]),
+        "slu_symb_arrays": (None, [P, c_i64p, c_i64p, c_i64p]),
+        "slu_symb_counts": (None, [P, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
+        "slu_distribute": (P, [P, C.POINTER(SluCsc), C.c_int, C.c_int, C.c_int, C.c_int]),
+        "slu_lustruct_free": (None, [P, C.c_int]),
+        "slu_permute": (C.POINTER(SluCsc), [C.POINTER(SluCsc), c_i64p]),
+        "slu_lu_get_view": (C.c_int, [P, C.c_int, C.POINTER(SluLuView)]),
+        "slu_comm_unique_id": (C.c_int, [P]),
+        "slu_comm_create": (P, [P, C.c_int, C.c_int, C.c_int, C.c_int]),
+        "slu_comm_destroy": (None, [P]),
+        "slu_plan_create": (P, [C.c_int, P, C.c_int, C.c_int, C.c_int, C.c_int, P,
+                                C.POINTER(EngineOpts), C.c_char_p, C.c_int]),
+        "slu_plan_upload": (C.c_int, [P]),
+        "slu_plan_factor": (C.c_int, [P, C.c_double, c_intp, c_intp]),
+        "slu_plan_download": (C.c_int, [P]),
+        "slu_plan_destroy": (None, [P]),
+        "slu_plan_get_stats": (C.c_int, [P, C.POINTER(PlanStats)]),
+        "slu_last_error": (C.c_char_p, []),
+    }
+    for name, (res, args) in sig.items():
+        if not hasattr(L, name):
+            if os.environ.get("SLU_PARTIAL_LIB"):
+                continue
+            raise RuntimeError(f"{LIB_PATH} does not export {name}: rebuild it")
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def as_i64p(a):
+    return a.ctypes.data_as(c_i64p)
