@@ -191,6 +191,8 @@ void slu_symb_arrays(const slu_symb *s, int64_t *xsup, int64_t *supno,
                      int64_t *perm_c);
 /* nnz(L) including the diagonal blocks, nnz(U) excluding them */
 void slu_symb_counts(const slu_symb *s, double *nnzL, double *nnzU);
+/* |struct(L_s)| (rows incl. the diagonal block) per supernode */
+void slu_symb_struct_sizes(const slu_symb *s, int64_t *sizes);
 
 /* Build this rank's LUstruct (dtype-typed dLUstruct_t/sLUstruct_t/zLUstruct_t
  * allocated by the library) holding P*A*P^T in the layout of

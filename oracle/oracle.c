@@ -27,6 +27,10 @@
 #include "slu_abi.h"
 
 /* ---------------- double ---------------- */
+#define F_SCALE(x) (x)
+#define F_RANK1 2.0
+#define F_TRSM 1.0
+#define F_SCHUR 2.0
 #define VT double
 #define LUS dLUstruct_t
 #define OR_NAME(x) d_##x
@@ -104,6 +108,14 @@ static inline doublecomplex zc_recip(doublecomplex b) {
     doublecomplex one = {1.0, 0.0}; return zc_div(one, b); }
 static inline double zc_abs1(doublecomplex a) { return fabs(a.r) + fabs(a.i); }
 static const doublecomplex zc_zero = {0.0, 0.0};
+#undef F_SCALE
+#undef F_RANK1
+#undef F_TRSM
+#undef F_SCHUR
+#define F_SCALE(x) (6.0 * (x) + 10.0)
+#define F_RANK1 8.0
+#define F_TRSM 4.0
+#define F_SCHUR 8.0
 #define VT doublecomplex
 #define LUS zLUstruct_t
 #define OR_NAME(x) z_##x

@@ -15,7 +15,10 @@
  *
  * Expects: VT (value type), OR_NAME(x) (name mangling), LUS (LUstruct type),
  * and the scalar macros V_ZERO, V_SUB(a,b), V_MUL(a,b), V_DIV(a,b), V_ABS(a),
- * V_ISZERO(a), V_SET_RE(a,re) (keep sign), V_RECIP(a).
+ * V_ISZERO(a), V_SET_THRESH(a,t) (keep sign), V_RECIP(a), and the flop
+ * weights of the reference's stat->ops[FACT] accounting: F_SCALE(x), F_RANK1,
+ * F_TRSM, F_SCHUR (SRC/pdgstrf2.c:252,262,318,355; SRC/pzgstrf2.c:253,263,319,356;
+ * SRC/zlook_ahead_update.c:160).
  */
 
 /* pdgstrf2_trsm, SRC/pdgstrf2.c:213-269 (diagonal block) and :302-355 (TRSM). */
@@ -42,7 +45,7 @@ static void OR_NAME(panel_l)(LUS **LU, int Pr, int Pc, int_t k, int_t *xsup,
             VT temp = V_RECIP(*piv);
             for (int_t i = j + 1; i < nsupc; ++i)
                 lusup[i + j * nsupr] = V_MUL(lusup[i + j * nsupr], temp);
-            *flops += (double)(nsupc - j - 1);
+            *flops += F_SCALE((double)(nsupc - j - 1));
         }
         /* rank-1 update inside the diagonal block, :256-263 (dger) */
         for (int_t l = j + 1; l < nsupc; ++l) {
@@ -51,7 +54,7 @@ static void OR_NAME(panel_l)(LUS **LU, int Pr, int Pc, int_t k, int_t *xsup,
                 lusup[i + l * nsupr] = V_SUB(lusup[i + l * nsupr],
                                              V_MUL(lusup[i + j * nsupr], u));
         }
-        *flops += 2.0 * (double)(nsupc - j - 1) * (double)(nsupc - j - 1);
+        *flops += F_RANK1 * (double)(nsupc - j - 1) * (double)(nsupc - j - 1);
     }
     /* --- L(:,k) := L(:,k) * U_kk^{-1} on every rank of process column kcol
      *     (dtrsm "R","U","N","N", :311 diag rank rows below the block,
@@ -71,7 +74,7 @@ static void OR_NAME(panel_l)(LUS **LU, int Pr, int Pc, int_t k, int_t *xsup,
                 X[i + j * ld] = V_DIV(s, lusup[j + j * nsupr]);
             }
         }
-        *flops += (double)nsupc * (nsupc + 1) * (double)(ld - r0);
+        *flops += F_TRSM * (double)nsupc * (nsupc + 1) * (double)(ld - r0);
     }
 }
 
@@ -171,7 +174,7 @@ static void OR_NAME(schur)(LUS **LU, int Pr, int Pc, int_t k, int_t *xsup,
                                     nzval[d + jj * ldv] = V_SUB(nzval[d + jj * ldv], s);
                                 }
                                 ruk += seg;
-                                *flops += 2.0 * nbrow * seg;
+                                *flops += F_SCHUR * nbrow * seg;
                             }
                         } else {
                             /* dscatter_u: locate U(ib,jb) in block row ib
@@ -201,7 +204,7 @@ static void OR_NAME(schur)(LUS **LU, int Pr, int Pc, int_t k, int_t *xsup,
                                         ucol[rel] = V_SUB(ucol[rel], s);
                                     }
                                     ruk += seg;
-                                    *flops += 2.0 * nbrow * seg;
+                                    *flops += F_SCHUR * nbrow * seg;
                                 }
                                 ruip += ilst - dfnz;
                             }

@@ -90,7 +90,7 @@ def run_reference(A, perm_c, nprow, npcol, relax=60, maxsup=256, lookahead=10,
         env = dict(os.environ)
         env.update({"MPICH_CC": "gcc", "OMP_NUM_THREADS": str(omp_threads),
                     "MKL_NUM_THREADS": "1", "MKL_THREADING_LAYER": "SEQUENTIAL",
-                    "LD_LIBRARY_PATH": CONDA + "/lib:" + env.get("LD_LIBRARY_PATH", "")})
+                    "LD_LIBRARY_PATH": "/usr/lib/x86_64-linux-gnu:/opt/rocm/lib:" + CONDA + "/lib:" + env.get("LD_LIBRARY_PATH", "")})
         cmd = [os.path.join(CONDA, "bin", "mpiexec"), "-n", str(nprow * npcol), REF_BIN,
                "-lib", LIB_PATH, "-f", mfile, "-r", str(nprow), "-c", str(npcol),
                "-x", str(relax), "-m", str(maxsup), "-l", str(lookahead),

@@ -1,0 +1,251 @@
+// Drop-in C ABI: pdgstrf / psgstrf / pzgstrf and the scatter helpers the
+// reference's pdgstrf.c.o exports.
+//
+// pxgstrf(options, m, n, anorm, LUstruct, grid, stat, info) keeps the
+// reference contract (SRC/pdgstrf.c:242-402, 1927-1931):
+//   * m < 0 -> info = -2, n < 0 -> info = -3, message as pxerr_dist, return -1;
+//   * m == 0 || n == 0 -> return 0;
+//   * factors are written back in place into LUstruct->Llu's host arrays;
+//   * stat->ops[FACT] = algorithmic flops, stat->TinyPivots += replacements,
+//     stat->num_look_aheads = clamp(options->num_lookaheads, 0, 49);
+//   * *info = MIN over ranks of the rank's zero-pivot column (0 if none).
+// It must be called by every rank of grid->comm.  MPI is used only to
+// bootstrap RCCL for multi-rank grids; its symbols are looked up in the host
+// process at run time (this library has no link-time MPI dependency).
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <vector>
+
+#include "common.h"
+#include "slu_mi355x.h"
+
+namespace {
+
+typedef int (*mpi_bcast_t)(void *, int, MPI_Datatype, int, MPI_Comm);
+typedef int (*mpi_allreduce_t)(const void *, void *, int, MPI_Datatype, MPI_Op, MPI_Comm);
+
+template <typename F> F mpi_sym(const char *name) {
+    void *p = dlsym(RTLD_DEFAULT, name);
+    if (!p) throw slu::Error(slu::fmt("MPI symbol %s not found in the process", name));
+    return (F)p;
+}
+
+int pick_device(int iam) {
+    const char *e = getenv("SUPERLU_DEVICE");
+    if (e) return atoi(e);
+    int nd = 0;
+    if (hipGetDeviceCount(&nd) != hipSuccess || nd <= 0)
+        throw slu::Error("no HIP device visible: the MI355X engine needs a GPU");
+    const char *lr = getenv("MPI_LOCALRANKID");
+    if (!lr) lr = getenv("OMPI_COMM_WORLD_LOCAL_RANK");
+    if (!lr) lr = getenv("LOCAL_RANK");
+    int r = lr ? atoi(lr) : iam;
+    return r % nd;
+}
+
+std::mutex g_mu;
+std::map<long, slu_comm *> g_comms; // keyed by the grid's MPI communicator
+
+slu_comm *comm_for_grid(gridinfo_t *grid) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    long key = (long)(intptr_t)grid->comm;
+    auto it = g_comms.find(key);
+    if (it != g_comms.end()) return it->second;
+    int nprow = (int)grid->nprow, npcol = (int)grid->npcol;
+    unsigned char uid[128] = {0};
+    if (nprow * npcol > 1) {
+        if (grid->iam == 0 && slu_comm_unique_id(uid) != 0)
+            throw slu::Error(slu_last_error());
+        auto bcast = mpi_sym<mpi_bcast_t>("MPI_Bcast");
+        bcast(uid, 128, MPI_BYTE, 0, grid->comm);
+    }
+    slu_comm *c = slu_comm_create(nprow * npcol > 1 ? uid : nullptr, nprow, npcol, grid->iam,
+                                  pick_device(grid->iam));
+    if (!c) throw slu::Error(slu_last_error());
+    g_comms[key] = c;
+    return c;
+}
+
+template <typename LUS>
+int_t pxgstrf(int dtype, const char *name, superlu_dist_options_t *options, int m, int n,
+              double anorm, LUS *LUstruct, gridinfo_t *grid, SuperLUStat_t *stat, int *info) {
+    *info = 0;
+    if (m < 0) *info = -2;
+    else if (n < 0) *info = -3;
+    if (*info) {
+        printf("{%lld,%lld}: On entry to %6s, parameter number %lld had an illegal value\n",
+               (long long)(grid->iam / grid->npcol), (long long)(grid->iam % grid->npcol), name,
+               (long long)-*info);
+        return -1;
+    }
+    if (m == 0 || n == 0) return 0;
+    stat->ops[SLU_PHASE_FACT] = 0.0f;
+    stat->current_buffer = stat->peak_buffer = stat->gpu_buffer = 0.0f;
+    stat->num_look_aheads = std::max(0, std::min(options->num_lookaheads, SLU_MAX_LOOKAHEADS - 1));
+    slu_plan *plan = nullptr;
+    try {
+        slu_comm *c = comm_for_grid(grid);
+        slu_engine_opts eo{};
+        eo.replace_tiny_pivot = options->ReplaceTinyPivot == SLU_YES;
+        char err[512] = {0};
+        plan = slu_plan_create(dtype, LUstruct, n, (int)grid->nprow, (int)grid->npcol, grid->iam,
+                               c, &eo, err, sizeof err);
+        if (!plan) throw slu::Error(err);
+        int myinfo = 0, tiny = 0;
+        if (slu_plan_upload(plan) || slu_plan_factor(plan, anorm, &myinfo, &tiny) ||
+            slu_plan_download(plan))
+            throw slu::Error(slu_last_error());
+        slu_plan_stats st;
+        slu_plan_get_stats(plan, &st);
+        stat->ops[SLU_PHASE_FACT] = (float)(st.schur_flops + st.panel_flops);
+        stat->TinyPivots += tiny;
+        stat->gpu_buffer = (float)(st.lu_bytes + st.index_bytes);
+        slu_plan_destroy(plan);
+        plan = nullptr;
+        int gi = myinfo ? myinfo : n + 1;
+        if (grid->nprow * grid->npcol > 1) {
+            auto allreduce = mpi_sym<mpi_allreduce_t>("MPI_Allreduce");
+            int in = gi;
+            allreduce(&in, &gi, 1, MPI_INT, MPI_MIN, grid->comm);
+        }
+        *info = gi == n + 1 ? 0 : gi;
+        return 0;
+    } catch (const std::exception &e) {
+        if (plan) slu_plan_destroy(plan);
+        fprintf(stderr, "%s (MI355X engine): %s\n", name, e.what());
+        fflush(stderr);
+        abort(); // the reference ABORTs on internal failures (SRC/util_dist.h ABORT)
+    }
+}
+
+// ------------------------------------------------------------------ scatter
+// Host implementations with the reference prototypes and semantics of
+// SRC/dscatter.c:28-277 (s/z are type substitutions).
+template <typename T> inline void vsub(T &a, const T &b) { a -= b; }
+inline void vsub(doublecomplex &a, const doublecomplex &b) { a.r -= b.r; a.i -= b.i; }
+
+template <typename T>
+void scatter_l_1(int ib, int ljb, int nsupc, int_t iukp, int_t *xsup, int klst, int nbrow,
+                 int_t lptr, int temp_nbrow, int_t *usub, int_t *lsub, T *tempv,
+                 int *indirect_thread, int_t **Lrowind_bc_ptr, T **Lnzval_bc_ptr) {
+    int_t *index = Lrowind_bc_ptr[ljb];
+    int_t ldv = index[1], lptrj = SLU_BC_HEADER, luptrj = 0;
+    while (index[lptrj] != ib) {
+        luptrj += index[lptrj + 1];
+        lptrj += SLU_LB_DESCRIPTOR + index[lptrj + 1];
+    }
+    int_t fnz = xsup[ib], dest_nbrow = index[lptrj + 1];
+    lptrj += SLU_LB_DESCRIPTOR;
+    for (int_t i = 0; i < dest_nbrow; ++i) indirect_thread[index[lptrj + i] - fnz] = (int)i;
+    T *nzval = Lnzval_bc_ptr[ljb] + luptrj;
+    for (int jj = 0; jj < nsupc; ++jj) {
+        int_t segsize = klst - usub[iukp + jj];
+        if (segsize) {
+            for (int i = 0; i < temp_nbrow; ++i)
+                vsub(nzval[indirect_thread[lsub[lptr + i] - fnz]], tempv[i]);
+            tempv += nbrow;
+        }
+        nzval += ldv;
+    }
+}
+
+template <typename T>
+void scatter_l(int ib, int ljb, int nsupc, int_t iukp, int_t *xsup, int klst, int nbrow,
+               int_t lptr, int temp_nbrow, int_t *usub, int_t *lsub, T *tempv,
+               int *indirect_thread, int *indirect2, int_t **Lrowind_bc_ptr, T **Lnzval_bc_ptr) {
+    int_t *index = Lrowind_bc_ptr[ljb];
+    int_t ldv = index[1], lptrj = SLU_BC_HEADER, luptrj = 0;
+    while (index[lptrj] != ib) {
+        luptrj += index[lptrj + 1];
+        lptrj += SLU_LB_DESCRIPTOR + index[lptrj + 1];
+    }
+    int_t fnz = xsup[ib], dest_nbrow = index[lptrj + 1];
+    lptrj += SLU_LB_DESCRIPTOR;
+    for (int_t i = 0; i < dest_nbrow; ++i) indirect_thread[index[lptrj + i] - fnz] = (int)i;
+    for (int i = 0; i < temp_nbrow; ++i) indirect2[i] = indirect_thread[lsub[lptr + i] - fnz];
+    T *nzval = Lnzval_bc_ptr[ljb] + luptrj;
+    for (int jj = 0; jj < nsupc; ++jj) {
+        int_t segsize = klst - usub[iukp + jj];
+        if (segsize) {
+            for (int i = 0; i < temp_nbrow; ++i) vsub(nzval[indirect2[i]], tempv[i]);
+            tempv += nbrow;
+        }
+        nzval += ldv;
+    }
+}
+
+template <typename T>
+void scatter_u(int ib, int jb, int nsupc, int_t iukp, int_t *xsup, int klst, int nbrow,
+               int_t lptr, int temp_nbrow, int_t *lsub, int_t *usub, T *tempv,
+               int_t **Ufstnz_br_ptr, T **Unzval_br_ptr, gridinfo_t *grid) {
+    int_t ilst = xsup[ib + 1], lib = ib / grid->nprow;
+    int_t *index = Ufstnz_br_ptr[lib];
+    int_t iuip = SLU_BR_HEADER, ruip = 0;
+    while (index[iuip] < jb) {
+        ruip += index[iuip + 1];
+        iuip += SLU_UB_DESCRIPTOR + (xsup[index[iuip] + 1] - xsup[index[iuip]]);
+    }
+    iuip += SLU_UB_DESCRIPTOR;
+    for (int jj = 0; jj < nsupc; ++jj) {
+        int_t segsize = klst - usub[iukp + jj];
+        int_t fnz = index[iuip++];
+        if (segsize) {
+            T *ucol = &Unzval_br_ptr[lib][ruip];
+            for (int i = 0; i < temp_nbrow; ++i) vsub(ucol[lsub[lptr + i] - fnz], tempv[i]);
+            tempv += nbrow;
+        }
+        ruip += ilst - fnz;
+    }
+}
+
+} // namespace
+
+extern "C" {
+
+int_t pdgstrf(superlu_dist_options_t *options, int m, int n, double anorm,
+              dLUstruct_t *LUstruct, gridinfo_t *grid, SuperLUStat_t *stat, int *info) {
+    return pxgstrf(SLU_D, "PDGSTRF", options, m, n, anorm, LUstruct, grid, stat, info);
+}
+int_t psgstrf(superlu_dist_options_t *options, int m, int n, float anorm,
+              sLUstruct_t *LUstruct, gridinfo_t *grid, SuperLUStat_t *stat, int *info) {
+    return pxgstrf(SLU_S, "PSGSTRF", options, m, n, (double)anorm, LUstruct, grid, stat, info);
+}
+int_t pzgstrf(superlu_dist_options_t *options, int m, int n, double anorm,
+              zLUstruct_t *LUstruct, gridinfo_t *grid, SuperLUStat_t *stat, int *info) {
+    return pxgstrf(SLU_Z, "PZGSTRF", options, m, n, anorm, LUstruct, grid, stat, info);
+}
+
+#define SLU_SCATTER_EXPORTS(P, T)                                                              \
+    void P##scatter_l_1(int ib, int ljb, int nsupc, int_t iukp, int_t *xsup, int klst,          \
+                        int nbrow, int_t lptr, int temp_nbrow, int_t *usub, int_t *lsub,        \
+                        T *tempv, int *indirect_thread, int_t **Lrowind_bc_ptr,                 \
+                        T **Lnzval_bc_ptr, gridinfo_t *) {                                      \
+        scatter_l_1<T>(ib, ljb, nsupc, iukp, xsup, klst, nbrow, lptr, temp_nbrow, usub, lsub,   \
+                       tempv, indirect_thread, Lrowind_bc_ptr, Lnzval_bc_ptr);                  \
+    }                                                                                          \
+    void P##scatter_l(int ib, int ljb, int nsupc, int_t iukp, int_t *xsup, int klst,            \
+                      int nbrow, int_t lptr, int temp_nbrow, int_t *usub, int_t *lsub,          \
+                      T *tempv, int *indirect_thread, int *indirect2,                           \
+                      int_t **Lrowind_bc_ptr, T **Lnzval_bc_ptr, gridinfo_t *) {                \
+        scatter_l<T>(ib, ljb, nsupc, iukp, xsup, klst, nbrow, lptr, temp_nbrow, usub, lsub,     \
+                     tempv, indirect_thread, indirect2, Lrowind_bc_ptr, Lnzval_bc_ptr);         \
+    }                                                                                          \
+    void P##scatter_u(int ib, int jb, int nsupc, int_t iukp, int_t *xsup, int klst, int nbrow,  \
+                      int_t lptr, int temp_nbrow, int_t *lsub, int_t *usub, T *tempv,           \
+                      int_t **Ufstnz_br_ptr, T **Unzval_br_ptr, gridinfo_t *grid) {             \
+        scatter_u<T>(ib, jb, nsupc, iukp, xsup, klst, nbrow, lptr, temp_nbrow, lsub, usub,      \
+                     tempv, Ufstnz_br_ptr, Unzval_br_ptr, grid);                                \
+    }
+
+SLU_SCATTER_EXPORTS(d, double)
+SLU_SCATTER_EXPORTS(s, float)
+SLU_SCATTER_EXPORTS(z, doublecomplex)
+
+} // extern "C"

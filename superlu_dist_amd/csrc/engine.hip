@@ -1,0 +1,831 @@
+// MI355X numeric factorization engine: plan construction (host), level-
+// synchronous execution of the batched kernels in kernels.h, RCCL panel
+// exchange for 2D grids, and the engine C API of include/slu_mi355x.h.
+//
+// Algorithm (what replaces the k-loop of SRC/pdgstrf.c:1108-1756):
+//   The supernodal dependency DAG (k -> ib for every block L(ib,k), k -> jb
+//   for every block U(k,jb)) is levelled once at plan time.  Supernodes of one
+//   level are independent, so for each level the engine launches
+//     1. k_diag_lu  on all diagonal blocks of the level owned by this rank,
+//     2. (grids) broadcast of the factored diagonal blocks along process rows
+//        and columns,
+//     3. k_trsm_l / k_trsm_u on every local L / U panel block of the level,
+//     4. (grids) broadcast of L panels along process rows and U panels along
+//        process columns (RCCL grouped broadcasts),
+//     5. k_schur over every (L row tile x U column tile) of every supernode of
+//        the level, scattering straight into the destination blocks.
+//   The set of updates and the per-element arithmetic are those of the
+//   reference; only the order in which independent updates are applied
+//   differs (the reference orders them by its static schedule,
+//   SRC/dstatic_schedule.c:39).  Two supernodes of one level that update the
+//   same destination block use atomic fp adds for those blocks.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <memory>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "common.h"
+#include "kernels.h"
+#include "slu_mi355x.h"
+
+using std::vector;
+
+namespace slu {
+
+static thread_local std::string g_last_error;
+void set_last_error(const std::string &s) { g_last_error = s; }
+
+template <typename T> struct DevBuf {
+    T *p = nullptr;
+    size_t n = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf &) = delete;
+    DevBuf &operator=(const DevBuf &) = delete;
+    ~DevBuf() { release(); }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+    void alloc(size_t cnt) {
+        release();
+        n = cnt;
+        if (cnt) HIPCHK(hipMalloc(&p, cnt * sizeof(T)));
+    }
+    void upload(const vector<T> &v) {
+        alloc(v.size());
+        if (!v.empty()) HIPCHK(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+    }
+    size_t bytes() const { return n * sizeof(T); }
+};
+
+} // namespace slu
+
+// ------------------------------------------------------------------ comm
+struct slu_comm {
+    int nprow = 1, npcol = 1, iam = 0, myrow = 0, mycol = 0, device = 0;
+    ncclComm_t world = nullptr, row = nullptr, col = nullptr;
+};
+
+namespace slu {
+
+using i64 = int64_t;
+
+struct LevelRange {
+    int diag_off = 0, diag_n = 0;
+    int tl_off = 0, tl_n = 0;
+    int tu_off = 0, tu_n = 0;
+    int k_off = 0, k_n = 0;
+    int tile_off = 0, tile_n = 0;
+    double schur_flops = 0;
+    bool big = false;
+};
+
+struct PlanBase {
+    virtual ~PlanBase() = default;
+    virtual void upload() = 0;
+    virtual void factor(double anorm, int *info, int *tiny) = 0;
+    virtual void download() = 0;
+    slu_plan_stats stats{};
+};
+
+// One rank's plan for value type T (double / float / zc) over the host
+// LUstruct layout LocalLU / LUS.
+template <typename T, typename HT, typename LocalLU, typename LUS>
+struct Plan : PlanBase {
+    // ---- problem
+    int n = 0, nsupers = 0, Pr = 1, Pc = 1, iam = 0, myrow = 0, mycol = 0;
+    slu_comm *comm = nullptr;
+    slu_engine_opts opts{};
+    LUS *LU = nullptr;
+    vector<i64> xsup;
+    int nlc = 0, nlr = 0;
+    hipStream_t stream = nullptr;
+
+    // ---- local storage layout
+    vector<i64> lval_off, uval_off; // per local column / row, -1 if empty
+    vector<int> lval_ld;            // nsupr per local column
+    i64 lval_total = 0, uval_total = 0;
+    bool l_contig = false, u_contig = false;
+    // L blocks (column-major order of columns, storage order within)
+    vector<LBlk> lblk;
+    vector<int> lblk_ib, lblk_rowstart, lblk_nrows;
+    vector<int> lcol_first, lcol_nblk; // per local column
+    vector<int> lmap;
+    // U blocks
+    vector<UBlk> ublk;
+    vector<int> ublk_jb;
+    vector<int> urow_first, urow_nblk;
+    vector<i64> ucol_voff;
+    vector<int> ucol_fst;
+
+    // ---- schedule
+    vector<int> level_of;
+    vector<LevelRange> levels;
+    vector<DiagItem<T>> diag_items;
+    vector<TrsmLItem<T>> tl_items;
+    vector<TrsmUItem<T>> tu_items;
+    vector<KInfo<T>> kinfos;
+    vector<TileItem> tiles;
+    // per-k panel arrays (device copies referenced by KInfo / TrsmUItem)
+    vector<int> h_rg, h_ra, h_cg, h_cb, h_pair, h_ct0;
+    vector<i64> h_cvoff;
+
+    // ---- device
+    DevBuf<T> d_L, d_U;
+    DevBuf<LBlk> d_lblk;
+    DevBuf<int> d_lmap;
+    DevBuf<UBlk> d_ublk;
+    DevBuf<i64> d_ucol_voff;
+    DevBuf<int> d_ucol_fst;
+    DevBuf<DiagItem<T>> d_diag;
+    DevBuf<TrsmLItem<T>> d_tl;
+    DevBuf<TrsmUItem<T>> d_tu;
+    DevBuf<KInfo<T>> d_kinfo;
+    DevBuf<TileItem> d_tiles;
+    DevBuf<int> d_rg, d_ra, d_cg, d_cb, d_pair, d_ct0;
+    DevBuf<i64> d_cvoff;
+    DevBuf<int> d_counters; // [0] tiny pivots, [1..] unused
+    DevBuf<int> d_zpiv;     // per supernode: max zero-pivot column + 1
+
+    int W(i64 k) const { return (int)(xsup[k + 1] - xsup[k]); }
+
+    Plan(LUS *lu, int n_, int nprow, int npcol, int iam_, slu_comm *c,
+         const slu_engine_opts *o) {
+        LU = lu;
+        n = n_;
+        Pr = nprow;
+        Pc = npcol;
+        iam = iam_;
+        myrow = iam / Pc;
+        mycol = iam % Pc;
+        comm = c;
+        if (o) opts = *o;
+        SLU_REQUIRE(Pr * Pc == 1 || (comm && comm->world),
+                    "a %dx%d grid needs an RCCL communicator", Pr, Pc);
+        if (comm) HIPCHK(hipSetDevice(comm->device));
+        HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+        int_t *hx = LU->Glu_persist->xsup;
+        nsupers = (int)(LU->Glu_persist->supno[n - 1] + 1);
+        xsup.assign(hx, hx + nsupers + 1);
+        nlc = (nsupers + Pc - 1) / Pc;
+        nlr = (nsupers + Pr - 1) / Pr;
+        for (int k = 0; k < nsupers; ++k)
+            SLU_REQUIRE(W(k) <= 512, "supernode %d has %d columns (> MAX_SUPER_SIZE 512)", k, W(k));
+        SLU_REQUIRE(Pr * Pc == 1, "multi-rank grids: see build_exchange (not yet enabled)");
+        build_local();
+        build_schedule();
+        build_device();
+    }
+
+    ~Plan() override {
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+
+    // ------------------------------------------------------- local layout
+    void build_local() {
+        LocalLU *Llu = LU->Llu;
+        lval_off.assign(nlc, -1);
+        lval_ld.assign(nlc, 0);
+        lcol_first.assign(nlc, 0);
+        lcol_nblk.assign(nlc, 0);
+        i64 off = 0;
+        l_contig = Llu->Lnzval_bc_dat != nullptr;
+        for (int ljb = 0; ljb < nlc; ++ljb) {
+            int jb = ljb * Pc + mycol;
+            int_t *index = Llu->Lrowind_bc_ptr[ljb];
+            lcol_first[ljb] = (int)lblk.size();
+            if (!index) continue;
+            int nb = (int)index[0], nsupr = (int)index[1];
+            lval_off[ljb] = off;
+            lval_ld[ljb] = nsupr;
+            if (Llu->Lnzval_bc_dat && (HT *)Llu->Lnzval_bc_ptr[ljb] != (HT *)Llu->Lnzval_bc_dat + off)
+                l_contig = false;
+            i64 p = SLU_BC_HEADER;
+            int rs = 0;
+            for (int b = 0; b < nb; ++b) {
+                int gb = (int)index[p], nr = (int)index[p + 1];
+                LBlk L{};
+                L.colvoff = off;
+                L.mapoff = (i64)lmap.size();
+                L.ld = nsupr;
+                L.fcol = (int)xsup[jb];
+                L.frow = (int)xsup[gb];
+                lmap.resize(lmap.size() + W(gb), -1);
+                for (int i = 0; i < nr; ++i) {
+                    i64 gr = index[p + 2 + i];
+                    lmap[L.mapoff + gr - xsup[gb]] = rs + i;
+                }
+                lblk.push_back(L);
+                lblk_ib.push_back(gb);
+                lblk_rowstart.push_back(rs);
+                lblk_nrows.push_back(nr);
+                rs += nr;
+                p += SLU_LB_DESCRIPTOR + nr;
+            }
+            SLU_REQUIRE(rs == nsupr, "L column %d: block rows %d != nsupr %d", jb, rs, nsupr);
+            lcol_nblk[ljb] = nb;
+            off += (i64)nsupr * W(jb);
+        }
+        lval_total = off;
+
+        uval_off.assign(nlr, -1);
+        urow_first.assign(nlr, 0);
+        urow_nblk.assign(nlr, 0);
+        off = 0;
+        u_contig = Llu->Unzval_br_dat != nullptr;
+        for (int lb = 0; lb < nlr; ++lb) {
+            int gb = lb * Pr + myrow;
+            int_t *index = Llu->Ufstnz_br_ptr[lb];
+            urow_first[lb] = (int)ublk.size();
+            if (!index) continue;
+            int nb = (int)index[0];
+            i64 len = index[1];
+            uval_off[lb] = off;
+            if (Llu->Unzval_br_dat && (HT *)Llu->Unzval_br_ptr[lb] != (HT *)Llu->Unzval_br_dat + off)
+                u_contig = false;
+            i64 p = SLU_BR_HEADER, run = 0;
+            i64 klst = xsup[gb + 1];
+            for (int b = 0; b < nb; ++b) {
+                int jb = (int)index[p];
+                UBlk U{};
+                U.coloff = (i64)ucol_voff.size();
+                U.fcol = (int)xsup[jb];
+                for (int c = 0; c < W(jb); ++c) {
+                    i64 fst = index[p + SLU_UB_DESCRIPTOR + c];
+                    ucol_voff.push_back(off + run);
+                    ucol_fst.push_back((int)fst);
+                    run += klst - fst;
+                }
+                ublk.push_back(U);
+                ublk_jb.push_back(jb);
+                p += SLU_UB_DESCRIPTOR + W(jb);
+            }
+            SLU_REQUIRE(run == len, "U row %d: segment lengths %lld != %lld", gb, (long long)run, (long long)len);
+            urow_nblk[lb] = nb;
+            off += len;
+        }
+        uval_total = off;
+    }
+
+    int find_lblk(int ib, int jb) const { // local column jb, block ib
+        int ljb = jb / Pc, f = lcol_first[ljb], nb = lcol_nblk[ljb];
+        auto b = lblk_ib.begin() + f, e = b + nb;
+        auto it = std::lower_bound(b, e, ib);
+        SLU_REQUIRE(it != e && *it == ib, "missing L block (%d,%d)", ib, jb);
+        return (int)(it - lblk_ib.begin());
+    }
+    int find_ublk(int ib, int jb) const { // local row ib, block jb
+        int lb = ib / Pr, f = urow_first[lb], nb = urow_nblk[lb];
+        auto b = ublk_jb.begin() + f, e = b + nb;
+        auto it = std::lower_bound(b, e, jb);
+        SLU_REQUIRE(it != e && *it == jb, "missing U block (%d,%d)", ib, jb);
+        return (int)(it - ublk_jb.begin());
+    }
+
+    // ------------------------------------------------------- schedule
+    void build_schedule() {
+        // dependency levels (1x1: the whole DAG is local)
+        level_of.assign(nsupers, 0);
+        int maxlev = 0;
+        for (int k = 0; k < nsupers; ++k) {
+            int lk = level_of[k];
+            maxlev = std::max(maxlev, lk);
+            int ljb = k / Pc;
+            for (int b = 0; b < lcol_nblk[ljb]; ++b) {
+                int ib = lblk_ib[lcol_first[ljb] + b];
+                if (ib != k) level_of[ib] = std::max(level_of[ib], lk + 1);
+            }
+            int lb = k / Pr;
+            for (int b = 0; b < urow_nblk[lb]; ++b) {
+                int jb = ublk_jb[urow_first[lb] + b];
+                level_of[jb] = std::max(level_of[jb], lk + 1);
+            }
+        }
+        vector<vector<int>> bylev(maxlev + 1);
+        for (int k = 0; k < nsupers; ++k) bylev[level_of[k]].push_back(k);
+        levels.resize(maxlev + 1);
+        stats.nsupers = nsupers;
+        stats.nlevels = maxlev + 1;
+
+        vector<int> owner(lblk.size() + ublk.size(), -1), touched;
+        for (int L = 0; L <= maxlev; ++L) {
+            LevelRange &R = levels[L];
+            R.diag_off = (int)diag_items.size();
+            R.tl_off = (int)tl_items.size();
+            R.tu_off = (int)tu_items.size();
+            R.k_off = (int)kinfos.size();
+            R.tile_off = (int)tiles.size();
+            for (int k : bylev[L]) add_supernode(k, R);
+            R.diag_n = (int)diag_items.size() - R.diag_off;
+            R.tl_n = (int)tl_items.size() - R.tl_off;
+            R.tu_n = (int)tu_items.size() - R.tu_off;
+            R.k_n = (int)kinfos.size() - R.k_off;
+            R.tile_n = (int)tiles.size() - R.tile_off;
+            // conflicting destinations inside the level -> atomics
+            touched.clear();
+            for (int s = R.k_off; s < R.k_off + R.k_n; ++s) {
+                KInfoHost &kh = khost[s];
+                for (int h : kh.dests) {
+                    int key = h >= 0 ? h : (int)lblk.size() + ~h;
+                    if (owner[key] == -1) {
+                        owner[key] = s;
+                        touched.push_back(key);
+                    } else if (owner[key] != s) {
+                        kinfos[owner[key]].atomic = 1;
+                        kinfos[s].atomic = 1;
+                    }
+                }
+            }
+            for (int key : touched) owner[key] = -1;
+        }
+        khost.clear();
+    }
+
+    struct KInfoHost {
+        vector<int> dests;
+    };
+    vector<KInfoHost> khost;
+
+    void add_supernode(int k, LevelRange &R) {
+        LocalLU *Llu = LU->Llu;
+        const int w = W(k);
+        const int ljb = k / Pc, lb = k / Pr;
+        const bool lcol_local = (k % Pc) == mycol && Llu->Lrowind_bc_ptr[ljb];
+        const bool diag_here = lcol_local && (k % Pr) == myrow;
+        // ---- diagonal block
+        i64 diag_off = -1;
+        int diag_ld = 0;
+        if (diag_here) {
+            diag_off = lval_off[ljb];
+            diag_ld = lval_ld[ljb];
+            SLU_REQUIRE(lblk_ib[lcol_first[ljb]] == k, "diagonal block of %d is not first", k);
+            DiagItem<T> d{};
+            d.a = (T *)(intptr_t)diag_off; // relocated in build_device
+            d.ld = diag_ld;
+            d.w = w;
+            d.k = k;
+            d.fcol = (int)xsup[k];
+            diag_items.push_back(d);
+            stats.n_diag++;
+            double wd = w;
+            stats.panel_flops += wd * (wd - 1) / 2 + 2 * (wd - 1) * wd * (2 * wd - 1) / 6;
+        }
+        // ---- L panel (rows of column k below the diagonal block)
+        int r0 = 0, m = 0;
+        vector<int> lbs; // L block ids of the panel (excluding the diagonal block)
+        if (lcol_local) {
+            int f = lcol_first[ljb], nb = lcol_nblk[ljb];
+            for (int b = 0; b < nb; ++b) {
+                if (lblk_ib[f + b] == k) { r0 += lblk_nrows[f + b]; continue; }
+                lbs.push_back(f + b);
+                m += lblk_nrows[f + b];
+            }
+            if (m > 0) {
+                for (int c0 = 0; c0 < m; c0 += TRSM_THREADS) {
+                    TrsmLItem<T> t{};
+                    t.x = (T *)(intptr_t)(lval_off[ljb] + r0 + c0);
+                    t.u = (const T *)(intptr_t)diag_off;
+                    t.ldx = lval_ld[ljb];
+                    t.ldu = diag_ld;
+                    t.w = w;
+                    t.nrows = std::min(TRSM_THREADS, m - c0);
+                    tl_items.push_back(t);
+                    stats.n_trsm_items++;
+                }
+                stats.panel_flops += (double)w * (w + 1) * m;
+            }
+        }
+        // ---- U panel (nonempty columns of block row k)
+        vector<int> ubs; // U block ids
+        int ncols = 0, kmin = w;
+        const int cols_off = (int)h_cg.size();
+        if ((k % Pr) == myrow && Llu->Ufstnz_br_ptr[lb]) {
+            int f = urow_first[lb], nb = urow_nblk[lb];
+            i64 klst = xsup[k + 1];
+            for (int b = 0; b < nb; ++b) {
+                int ub = f + b, jb = ublk_jb[ub];
+                int bidx = (int)ubs.size();
+                bool any = false;
+                for (int c = 0; c < W(jb); ++c) {
+                    i64 e = ublk[ub].coloff + c;
+                    int fst = ucol_fst[e];
+                    if (fst >= klst) continue;
+                    any = true;
+                    h_cg.push_back((int)xsup[jb] + c);
+                    h_cb.push_back(bidx);
+                    h_cvoff.push_back(ucol_voff[e]);
+                    int t0 = (int)(fst - xsup[k]);
+                    h_ct0.push_back(t0);
+                    kmin = std::min(kmin, t0);
+                    ++ncols;
+                    double seg = (double)(klst - fst);
+                    stats.panel_flops += seg * (seg + 1);
+                }
+                if (any) ubs.push_back(ub);
+            }
+            for (int c0 = 0; c0 < ncols; c0 += TRSM_THREADS) {
+                TrsmUItem<T> t{};
+                t.l = (const T *)(intptr_t)diag_off;
+                t.ldl = diag_ld;
+                t.w = w;
+                t.ncols = std::min(TRSM_THREADS, ncols - c0);
+                t.voff = (const i64 *)(intptr_t)(cols_off + c0); // relocated
+                t.t0 = (const int *)(intptr_t)(cols_off + c0);
+                int km = w;
+                for (int c = 0; c < t.ncols; ++c) km = std::min(km, h_ct0[cols_off + c0 + c]);
+                t.kmin = km;
+                tu_items.push_back(t);
+                stats.n_trsm_items++;
+            }
+        }
+        if (m == 0 || ncols == 0) return; // nothing to update from k here
+        // ---- Schur update of k
+        KInfo<T> ki{};
+        ki.a = (const T *)(intptr_t)(lval_off[ljb] + r0);
+        ki.lda = lval_ld[ljb];
+        ki.m = m;
+        ki.n = ncols;
+        ki.kmin = kmin;
+        ki.kw = w - kmin;
+        ki.nub = (int)ubs.size();
+        ki.cvoff = (const i64 *)(intptr_t)cols_off;
+        ki.ct0 = (const int *)(intptr_t)cols_off;
+        ki.cg = (const int *)(intptr_t)cols_off;
+        ki.cb = (const int *)(intptr_t)cols_off;
+        ki.ubase = nullptr; // Uval
+        const int rows_off = (int)h_rg.size();
+        for (size_t a = 0; a < lbs.size(); ++a)
+            for (int i = 0; i < lblk_nrows[lbs[a]]; ++i) {
+                h_rg.push_back(0); // filled from the index array below
+                h_ra.push_back((int)a);
+            }
+        // fill global rows from the index array of column k
+        {
+            int_t *index = Llu->Lrowind_bc_ptr[ljb];
+            i64 p = SLU_BC_HEADER;
+            int w_ = rows_off;
+            for (int b = 0; b < (int)index[0]; ++b) {
+                int gb = (int)index[p], nr = (int)index[p + 1];
+                if (gb != k)
+                    for (int i = 0; i < nr; ++i) h_rg[w_++] = (int)index[p + 2 + i];
+                p += SLU_LB_DESCRIPTOR + nr;
+            }
+        }
+        ki.rg = (const int *)(intptr_t)rows_off;
+        ki.ra = (const int *)(intptr_t)rows_off;
+        const int pair_off = (int)h_pair.size();
+        KInfoHost kh;
+        for (size_t a = 0; a < lbs.size(); ++a) {
+            int ib = lblk_ib[lbs[a]];
+            for (size_t b = 0; b < ubs.size(); ++b) {
+                int jb = ublk_jb[ubs[b]];
+                int h = ib >= jb ? find_lblk(ib, jb) : ~find_ublk(ib, jb);
+                h_pair.push_back(h);
+                kh.dests.push_back(h);
+            }
+        }
+        ki.pair = (const int *)(intptr_t)pair_off;
+        ki.atomic = 0;
+        kinfos.push_back(ki);
+        khost.push_back(std::move(kh));
+        const int slot = (int)kinfos.size() - 1 - R.k_off;
+        const int tm = (m + SC_BM - 1) / SC_BM, tn = (ncols + SC_BN - 1) / SC_BN;
+        for (int i = 0; i < tm; ++i)
+            for (int j = 0; j < tn; ++j) tiles.push_back(TileItem{slot, i, j});
+        // algorithmic work: exact unpadded flops and padded flops
+        double fl = 0;
+        for (int c = 0; c < ncols; ++c) fl += 2.0 * m * (w - h_ct0[cols_off + c]);
+        double mult = sizeof(T) == 16 ? 4.0 : 1.0; // complex: 8 real flops per multiply-add
+        stats.schur_flops += fl * mult;
+        stats.schur_flops_padded += 2.0 * m * ncols * (double)(w - kmin) * mult;
+        stats.scatter_bytes += 3.0 * sizeof(T) * (double)m * ncols;
+        stats.n_schur_tiles += (i64)tm * tn;
+        R.schur_flops += fl * mult;
+        if (w >= 64 && m >= 256 && ncols >= 256) R.big = true;
+    }
+
+    // ------------------------------------------------------- device
+    void build_device() {
+        d_L.alloc(std::max<i64>(lval_total, 1));
+        d_U.alloc(std::max<i64>(uval_total, 1));
+        T *L = d_L.p, *U = d_U.p;
+        d_rg.upload(h_rg);
+        d_ra.upload(h_ra);
+        d_cg.upload(h_cg);
+        d_cb.upload(h_cb);
+        d_pair.upload(h_pair);
+        d_ct0.upload(h_ct0);
+        d_cvoff.upload(h_cvoff);
+        for (auto &d : diag_items) d.a = L + (intptr_t)d.a;
+        for (auto &t : tl_items) {
+            t.x = L + (intptr_t)t.x;
+            t.u = L + (intptr_t)t.u;
+        }
+        for (auto &t : tu_items) {
+            t.l = L + (intptr_t)t.l;
+            t.ubase = U;
+            intptr_t co = (intptr_t)t.voff;
+            t.voff = d_cvoff.p + co;
+            t.t0 = d_ct0.p + co;
+        }
+        for (auto &k : kinfos) {
+            k.a = L + (intptr_t)k.a;
+            k.ubase = U;
+            intptr_t co = (intptr_t)k.cvoff, ro = (intptr_t)k.rg, po = (intptr_t)k.pair;
+            k.cvoff = d_cvoff.p + co;
+            k.ct0 = d_ct0.p + co;
+            k.cg = d_cg.p + co;
+            k.cb = d_cb.p + co;
+            k.rg = d_rg.p + ro;
+            k.ra = d_ra.p + ro;
+            k.pair = d_pair.p + po;
+        }
+        d_diag.upload(diag_items);
+        d_tl.upload(tl_items);
+        d_tu.upload(tu_items);
+        d_kinfo.upload(kinfos);
+        d_tiles.upload(tiles);
+        d_lblk.upload(lblk);
+        d_lmap.upload(lmap);
+        d_ublk.upload(ublk);
+        d_ucol_voff.upload(ucol_voff);
+        d_ucol_fst.upload(ucol_fst);
+        d_counters.alloc(4);
+        d_zpiv.alloc(nsupers);
+        stats.lu_bytes = (double)(lval_total + uval_total) * sizeof(T);
+        stats.index_bytes = (double)(d_lblk.bytes() + d_lmap.bytes() + d_ublk.bytes() +
+                                     d_ucol_voff.bytes() + d_ucol_fst.bytes() + d_diag.bytes() +
+                                     d_tl.bytes() + d_tu.bytes() + d_kinfo.bytes() +
+                                     d_tiles.bytes() + d_rg.bytes() + d_ra.bytes() +
+                                     d_cg.bytes() + d_cb.bytes() + d_pair.bytes() +
+                                     d_ct0.bytes() + d_cvoff.bytes());
+    }
+
+    // ------------------------------------------------------- values
+    void upload() override {
+        LocalLU *Llu = LU->Llu;
+        if (l_contig && lval_total) {
+            HIPCHK(hipMemcpy(d_L.p, Llu->Lnzval_bc_dat, lval_total * sizeof(T), hipMemcpyHostToDevice));
+        } else {
+            for (int ljb = 0; ljb < nlc; ++ljb)
+                if (lval_off[ljb] >= 0)
+                    HIPCHK(hipMemcpy(d_L.p + lval_off[ljb], Llu->Lnzval_bc_ptr[ljb],
+                                     (size_t)lval_ld[ljb] * W(ljb * Pc + mycol) * sizeof(T),
+                                     hipMemcpyHostToDevice));
+        }
+        if (u_contig && uval_total) {
+            HIPCHK(hipMemcpy(d_U.p, Llu->Unzval_br_dat, uval_total * sizeof(T), hipMemcpyHostToDevice));
+        } else {
+            for (int lb = 0; lb < nlr; ++lb)
+                if (uval_off[lb] >= 0)
+                    HIPCHK(hipMemcpy(d_U.p + uval_off[lb], Llu->Unzval_br_ptr[lb],
+                                     (size_t)Llu->Ufstnz_br_ptr[lb][1] * sizeof(T),
+                                     hipMemcpyHostToDevice));
+        }
+    }
+
+    void download() override {
+        LocalLU *Llu = LU->Llu;
+        HIPCHK(hipStreamSynchronize(stream));
+        if (l_contig && lval_total) {
+            HIPCHK(hipMemcpy(Llu->Lnzval_bc_dat, d_L.p, lval_total * sizeof(T), hipMemcpyDeviceToHost));
+        } else {
+            for (int ljb = 0; ljb < nlc; ++ljb)
+                if (lval_off[ljb] >= 0)
+                    HIPCHK(hipMemcpy(Llu->Lnzval_bc_ptr[ljb], d_L.p + lval_off[ljb],
+                                     (size_t)lval_ld[ljb] * W(ljb * Pc + mycol) * sizeof(T),
+                                     hipMemcpyDeviceToHost));
+        }
+        if (u_contig && uval_total) {
+            HIPCHK(hipMemcpy(Llu->Unzval_br_dat, d_U.p, uval_total * sizeof(T), hipMemcpyDeviceToHost));
+        } else {
+            for (int lb = 0; lb < nlr; ++lb)
+                if (uval_off[lb] >= 0)
+                    HIPCHK(hipMemcpy(Llu->Unzval_br_ptr[lb], d_U.p + uval_off[lb],
+                                     (size_t)Llu->Ufstnz_br_ptr[lb][1] * sizeof(T),
+                                     hipMemcpyDeviceToHost));
+        }
+    }
+
+    // ------------------------------------------------------- factor
+    void factor(double anorm, int *info, int *tiny) override {
+        // thresh = smach_dist("Epsilon") * anorm (SRC/pdgstrf.c:412-413); in
+        // psgstrf thresh is a float product.
+        const float s_eps = 5.9604644775390625e-08f; // FLT_EPSILON * 0.5
+        double thresh = sizeof(T) == 4 ? (double)(float)(s_eps * (float)anorm) : (double)s_eps * anorm;
+        HIPCHK(hipMemsetAsync(d_counters.p, 0, d_counters.bytes(), stream));
+        HIPCHK(hipMemsetAsync(d_zpiv.p, 0, d_zpiv.bytes(), stream));
+        const bool timing = opts.timing != 0;
+        vector<hipEvent_t> ev;
+        auto mark = [&]() -> int {
+            hipEvent_t e;
+            HIPCHK(hipEventCreate(&e));
+            HIPCHK(hipEventRecord(e, stream));
+            ev.push_back(e);
+            return (int)ev.size() - 1;
+        };
+        struct Span { int a, b, kind; bool big; };
+        vector<Span> spans;
+        int e_start = timing ? mark() : -1;
+        stats.n_schur_launches = 0;
+        for (size_t L = 0; L < levels.size(); ++L) {
+            const LevelRange &R = levels[L];
+            if (R.diag_n) {
+                int a = timing ? mark() : -1;
+                hipLaunchKernelGGL(k_diag_lu<T>, dim3(R.diag_n), dim3(DIAG_THREADS), 0, stream,
+                                   d_diag.p + R.diag_off, thresh, opts.replace_tiny_pivot,
+                                   d_counters.p, d_zpiv.p);
+                if (timing) spans.push_back({a, mark(), 0, false});
+            }
+            if (R.tl_n || R.tu_n) {
+                int a = timing ? mark() : -1;
+                if (R.tl_n)
+                    hipLaunchKernelGGL(k_trsm_l<T>, dim3(R.tl_n), dim3(TRSM_THREADS), 0, stream,
+                                       d_tl.p + R.tl_off);
+                if (R.tu_n)
+                    hipLaunchKernelGGL(k_trsm_u<T>, dim3(R.tu_n), dim3(TRSM_THREADS), 0, stream,
+                                       d_tu.p + R.tu_off);
+                if (timing) spans.push_back({a, mark(), 1, false});
+            }
+            if (R.tile_n) {
+                int a = timing ? mark() : -1;
+                hipLaunchKernelGGL(k_schur<T>, dim3(R.tile_n), dim3(SC_THREADS), 0, stream,
+                                   d_tiles.p + R.tile_off, d_kinfo.p + R.k_off, d_L.p, d_U.p,
+                                   d_lblk.p, d_lmap.p, d_ublk.p, d_ucol_voff.p, d_ucol_fst.p);
+                stats.n_schur_launches++;
+                if (timing) spans.push_back({a, mark(), 2, R.big});
+            }
+        }
+        HIPCHK(hipGetLastError());
+        int e_end = timing ? mark() : -1;
+        HIPCHK(hipStreamSynchronize(stream));
+        int hc[4];
+        HIPCHK(hipMemcpy(hc, d_counters.p, sizeof hc, hipMemcpyDeviceToHost));
+        vector<int> zp(nsupers);
+        HIPCHK(hipMemcpy(zp.data(), d_zpiv.p, nsupers * sizeof(int), hipMemcpyDeviceToHost));
+        // per-rank info: the zero pivot of the last supernode (in elimination
+        // order) that had one (SRC/pdgstrf2.c:246-247 overwrites *info)
+        int my_info = 0;
+        for (int k = 0; k < nsupers; ++k)
+            if (zp[k]) my_info = zp[k];
+        *info = my_info;
+        *tiny = hc[0];
+        if (timing) {
+            float ms;
+            HIPCHK(hipEventElapsedTime(&ms, ev[e_start], ev[e_end]));
+            stats.t_total_ms = ms;
+            stats.t_diag_ms = stats.t_trsm_ms = stats.t_schur_ms = stats.t_schur_big_ms = 0;
+            stats.schur_big_flops = 0;
+            for (auto &s : spans) {
+                HIPCHK(hipEventElapsedTime(&ms, ev[s.a], ev[s.b]));
+                if (s.kind == 0) stats.t_diag_ms += ms;
+                else if (s.kind == 1) stats.t_trsm_ms += ms;
+                else {
+                    stats.t_schur_ms += ms;
+                    if (s.big) stats.t_schur_big_ms += ms;
+                }
+            }
+            for (auto &R : levels)
+                if (R.big) stats.schur_big_flops += R.schur_flops;
+            for (auto e : ev) (void)hipEventDestroy(e);
+        }
+    }
+};
+
+template <typename P> PlanBase *make_plan(void *LU, int n, int pr, int pc, int iam, slu_comm *c,
+                                          const slu_engine_opts *o) {
+    return new P((decltype(std::declval<P>().LU))LU, n, pr, pc, iam, c, o);
+}
+
+} // namespace slu
+
+struct slu_plan {
+    int dtype = 0;
+    std::unique_ptr<slu::PlanBase> impl;
+};
+
+using namespace slu;
+
+extern "C" {
+
+const char *slu_last_error(void) { return g_last_error.c_str(); }
+
+int slu_comm_unique_id(void *uid) {
+    try {
+        ncclUniqueId id;
+        NCCLCHK(ncclGetUniqueId(&id));
+        memcpy(uid, &id, sizeof id);
+        return 0;
+    } catch (const std::exception &e) {
+        set_last_error(e.what());
+        return -1;
+    }
+}
+
+slu_comm *slu_comm_create(const void *uid, int nprow, int npcol, int iam, int device) {
+    try {
+        auto *c = new slu_comm;
+        c->nprow = nprow;
+        c->npcol = npcol;
+        c->iam = iam;
+        c->myrow = iam / npcol;
+        c->mycol = iam % npcol;
+        c->device = device;
+        HIPCHK(hipSetDevice(device));
+        if (nprow * npcol > 1) {
+            SLU_REQUIRE(uid != nullptr, "uid required for a %dx%d grid", nprow, npcol);
+            ncclUniqueId id;
+            memcpy(&id, uid, sizeof id);
+            NCCLCHK(ncclCommInitRank(&c->world, nprow * npcol, id, iam));
+            NCCLCHK(ncclCommSplit(c->world, c->myrow, c->mycol, &c->row, nullptr));
+            NCCLCHK(ncclCommSplit(c->world, c->mycol, c->myrow, &c->col, nullptr));
+        }
+        return c;
+    } catch (const std::exception &e) {
+        set_last_error(e.what());
+        return nullptr;
+    }
+}
+
+void slu_comm_destroy(slu_comm *c) {
+    if (!c) return;
+    if (c->row) ncclCommDestroy(c->row);
+    if (c->col) ncclCommDestroy(c->col);
+    if (c->world) ncclCommDestroy(c->world);
+    delete c;
+}
+
+slu_plan *slu_plan_create(int dtype, void *LU, int n, int nprow, int npcol, int iam,
+                          slu_comm *comm, const slu_engine_opts *opts, char *err, int errlen) {
+    try {
+        auto *p = new slu_plan;
+        p->dtype = dtype;
+        switch (dtype) {
+        case SLU_D:
+            p->impl.reset(make_plan<Plan<double, double, dLocalLU_t, dLUstruct_t>>(LU, n, nprow, npcol, iam, comm, opts));
+            break;
+        case SLU_S:
+            p->impl.reset(make_plan<Plan<float, float, sLocalLU_t, sLUstruct_t>>(LU, n, nprow, npcol, iam, comm, opts));
+            break;
+        case SLU_Z:
+            p->impl.reset(make_plan<Plan<zc, doublecomplex, zLocalLU_t, zLUstruct_t>>(LU, n, nprow, npcol, iam, comm, opts));
+            break;
+        default:
+            throw Error(fmt("bad dtype %d", dtype));
+        }
+        return p;
+    } catch (const std::exception &e) {
+        set_last_error(e.what());
+        if (err && errlen > 0) snprintf(err, errlen, "%s", e.what());
+        return nullptr;
+    }
+}
+
+int slu_plan_upload(slu_plan *p) {
+    try {
+        p->impl->upload();
+        return 0;
+    } catch (const std::exception &e) {
+        set_last_error(e.what());
+        return -1;
+    }
+}
+
+int slu_plan_factor(slu_plan *p, double anorm, int *info, int *tiny) {
+    try {
+        int i = 0, t = 0;
+        p->impl->factor(anorm, &i, &t);
+        if (info) *info = i;
+        if (tiny) *tiny = t;
+        return 0;
+    } catch (const std::exception &e) {
+        set_last_error(e.what());
+        return -1;
+    }
+}
+
+int slu_plan_download(slu_plan *p) {
+    try {
+        p->impl->download();
+        return 0;
+    } catch (const std::exception &e) {
+        set_last_error(e.what());
+        return -1;
+    }
+}
+
+void slu_plan_destroy(slu_plan *p) { delete p; }
+
+int slu_plan_get_stats(const slu_plan *p, slu_plan_stats *st) {
+    *st = p->impl->stats;
+    return 0;
+}
+
+} // extern "C"

@@ -309,15 +309,29 @@ slu_symb *slu_symbolic(const slu_csc *A, const int64_t *perm_c_in, int relax,
             j = r + 1;
             continue;
         }
-        // fundamental supernode starting at j
+        // Chain supernode starting at j.  A fundamental supernode needs
+        // cc[c] == cc[c+1]+1 along the chain; separator planes of a nested
+        // dissection break that at every border column, so (as in relaxed
+        // amalgamation) a chain is extended while the explicit zeros it
+        // introduces stay below AMALG_ZERO_FRAC of the stored entries.  Along
+        // a chain struct(L_c)\{c} is contained in struct(L_{c+1}), so the
+        // supernode's structure is [f..l] u struct(L_l): exact bookkeeping.
+        const double AMALG_ZERO_FRAC = 0.10;
         xsup.push_back(j);
-        int64_t len = 1;
+        int64_t f = j, len = 1;
+        double sumcc = (double)cc[j];
         while (j + 1 < n && len < maxsup && parent[j] == j + 1 &&
-               nchild[j + 1] == 1 && cc[j] == cc[j + 1] + 1 &&
-               size[j + 1] > relax) {
+               nchild[j + 1] == 1 && size[j + 1] > relax) {
+            double w = (double)(len + 1), c1 = (double)cc[j + 1];
+            double zeros = w * (w - 1) / 2 + w * c1 - (sumcc + c1);
+            double stored = w * (w + 1) / 2 + w * c1;
+            bool fundamental = cc[j] == cc[j + 1] + 1;
+            if (!fundamental && zeros > AMALG_ZERO_FRAC * stored) break;
             ++j;
             ++len;
+            sumcc += c1;
         }
+        (void)f;
         ++j;
     }
     xsup.push_back(n);
@@ -375,6 +389,9 @@ void slu_symb_arrays(const slu_symb *s, int64_t *xsup, int64_t *supno,
     if (xsup) std::copy(s->xsup.begin(), s->xsup.end(), xsup);
     if (supno) std::copy(s->supno.begin(), s->supno.end(), supno);
     if (perm_c) std::copy(s->perm.begin(), s->perm.end(), perm_c);
+}
+void slu_symb_struct_sizes(const slu_symb *s, int64_t *sizes) {
+    for (int64_t k = 0; k < s->nsupers; ++k) sizes[k] = s->sptr[k + 1] - s->sptr[k];
 }
 void slu_symb_counts(const slu_symb *s, double *nnzL, double *nnzU) {
     if (nnzL) *nnzL = s->nnzL;
@@ -513,7 +530,7 @@ void *distribute_t(const slu_symb *S, const slu_csc *A, int Pr, int Pc,
             Llu->Lnzval_bc_offset[ljb] = -1;
         }
     }
-    Llu->Lrowind_bc_dat = (int_t *)malloc((lidx_tot + 1) * sizeof(int_t));
+    Llu->Lrowind_bc_dat = (int_t *)calloc(lidx_tot + 1, sizeof(int_t));
     Llu->Lnzval_bc_dat = (T *)calloc(lval_tot + 1, sizeof(T));
     Llu->Lrowind_bc_cnt = lidx_tot + 1;
     Llu->Lnzval_bc_cnt = lval_tot + 1;
@@ -588,7 +605,7 @@ void *distribute_t(const slu_symb *S, const slu_csc *A, int Pr, int Pc,
             Llu->Unzval_br_offset[lb] = -1;
         }
     }
-    Llu->Ufstnz_br_dat = (int_t *)malloc((uidx_tot + 1) * sizeof(int_t));
+    Llu->Ufstnz_br_dat = (int_t *)calloc(uidx_tot + 1, sizeof(int_t));
     Llu->Unzval_br_dat = (T *)calloc(uval_tot + 1, sizeof(T));
     Llu->Ufstnz_br_cnt = uidx_tot + 1;
     Llu->Unzval_br_cnt = uval_tot + 1;

@@ -1,0 +1,90 @@
+"""Python driver of the MI355X engine (csrc/engine.hip) through its C ABI.
+
+A ``Plan`` is built once per LU structure: it copies the factor storage of a
+host LUstruct into HBM, levels the supernodal dependency DAG and uploads every
+index table the kernels need.  ``factor()`` then runs the numeric
+factorization entirely on the device; ``download()`` writes the factors back
+into the host LUstruct (the in-place contract of SRC/pdgstrf.c).
+"""
+import ctypes as C
+
+from .lib import EngineOpts, PlanStats, lib
+
+SMACH_EPS = 5.9604644775390625e-08  # smach_dist("Epsilon"), SRC/smach_dist.c:64
+
+
+class Comm:
+    """RCCL communicators of one 2D grid (one rank per GPU)."""
+
+    def __init__(self, nprow, npcol, iam, device=0, uid=None):
+        self.nprow, self.npcol, self.iam = nprow, npcol, iam
+        buf = None
+        if nprow * npcol > 1:
+            if uid is None:
+                raise ValueError("multi-rank grids need the RCCL unique id")
+            buf = C.create_string_buffer(bytes(uid), 128)
+        self.ptr = lib().slu_comm_create(buf, nprow, npcol, iam, device)
+        if not self.ptr:
+            raise RuntimeError(lib().slu_last_error().decode())
+
+    @staticmethod
+    def unique_id():
+        buf = C.create_string_buffer(128)
+        if lib().slu_comm_unique_id(buf) != 0:
+            raise RuntimeError(lib().slu_last_error().decode())
+        return buf.raw
+
+    def __del__(self):
+        if getattr(self, "ptr", None):
+            lib().slu_comm_destroy(self.ptr)
+            self.ptr = None
+
+
+class Plan:
+    def __init__(self, lu, comm=None, replace_tiny=False, timing=False):
+        self.lu = lu
+        o = EngineOpts()
+        o.replace_tiny_pivot = int(bool(replace_tiny))
+        o.timing = int(bool(timing))
+        err = C.create_string_buffer(1024)
+        iam = lu.myrow * lu.npcol + lu.mycol
+        self.comm = comm
+        self.ptr = lib().slu_plan_create(lu.dtype, lu.ptr, lu.symb.n, lu.nprow, lu.npcol, iam,
+                                         comm.ptr if comm is not None else None, C.byref(o),
+                                         err, len(err))
+        if not self.ptr:
+            raise RuntimeError("slu_plan_create: " + err.value.decode())
+
+    def _chk(self, rc):
+        if rc != 0:
+            raise RuntimeError(lib().slu_last_error().decode())
+
+    def upload(self):
+        self._chk(lib().slu_plan_upload(self.ptr))
+
+    def factor(self, anorm=1.0):
+        info, tiny = C.c_int(), C.c_int()
+        self._chk(lib().slu_plan_factor(self.ptr, anorm, C.byref(info), C.byref(tiny)))
+        return info.value, tiny.value
+
+    def download(self):
+        self._chk(lib().slu_plan_download(self.ptr))
+
+    def stats(self):
+        st = PlanStats()
+        lib().slu_plan_get_stats(self.ptr, C.byref(st))
+        return st.as_dict()
+
+    def __del__(self):
+        if getattr(self, "ptr", None):
+            lib().slu_plan_destroy(self.ptr)
+            self.ptr = None
+
+
+def factor_lustruct(lu, anorm=1.0, comm=None, replace_tiny=False):
+    """Factor one rank's LUstruct in place on the GPU; returns (info, tiny, stats)."""
+    p = Plan(lu, comm=comm, replace_tiny=replace_tiny)
+    p.upload()
+    info, tiny = p.factor(anorm)
+    p.download()
+    return info, tiny, p.stats()

@@ -91,6 +91,22 @@ class Symbolic:
         a, b = C.c_double(), C.c_double()
         lib().slu_symb_counts(self.ptr, C.byref(a), C.byref(b))
         self.nnzL, self.nnzU = a.value, b.value
+        self.struct_sizes = np.empty(self.nsupers, dtype=np.int64)
+        lib().slu_symb_struct_sizes(self.ptr, as_i64p(self.struct_sizes))
+
+    def flops(self):
+        """Algorithmic flops of the factorization with full U segments
+        (SURVEY §8d): diag LU + L TRSM + U TRSV + Schur, fp64 counting."""
+        w = np.diff(self.xsup).astype(np.float64)
+        b = self.struct_sizes - w
+        j = None
+        diag = np.array([sum((wi - jj - 1) + 2.0 * (wi - jj - 1) ** 2 for jj in range(int(wi)))
+                         for wi in w]) if len(w) < 0 else (w * (w - 1) / 2 + 2 * (w - 1) * w * (2 * w - 1) / 6)
+        trsm = w * (w + 1) * b
+        trsv = b * w * (w + 1)
+        schur = 2.0 * b * b * w
+        return {"schur": schur.sum(), "panel": (diag + trsm + trsv).sum(),
+                "total": (schur + diag + trsm + trsv).sum()}
 
     def distribute(self, nprow=1, npcol=1, myrow=0, mycol=0):
         return LUStruct(self, nprow, npcol, myrow, mycol)

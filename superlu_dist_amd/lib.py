@@ -80,6 +80,7 @@ def lib():
         "slu_symb_nsupers": (C.c_int64, [P]),
         "slu_symb_arrays": (None, [P, c_i64p, c_i64p, c_i64p]),
         "slu_symb_counts": (None, [P, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
+        "slu_symb_struct_sizes": (None, [P, c_i64p]),
         "slu_distribute": (P, [P, C.POINTER(SluCsc), C.c_int, C.c_int, C.c_int, C.c_int]),
         "slu_lustruct_free": (None, [P, C.c_int]),
         "slu_permute": (C.POINTER(SluCsc), [C.POINTER(SluCsc), c_i64p]),
@@ -98,8 +99,6 @@ def lib():
     }
     for name, (res, args) in sig.items():
         if not hasattr(L, name):
-            if os.environ.get("SLU_PARTIAL_LIB"):
-                continue
             raise RuntimeError(f"{LIB_PATH} does not export {name}: rebuild it")
         f = getattr(L, name)
         f.restype = res

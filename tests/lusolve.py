@@ -1,0 +1,64 @@
+"""Host-side supernodal triangular solves on a factored 1x1 LUstruct (test
+helper for backward-error checks; the reference's pdgstrs is out of scope)."""
+import numpy as np
+from scipy.linalg import solve_triangular
+
+
+def solve_1x1(lu, b):
+    """Solve (P A P^T) x = b with the factors held in lu (1x1 grid)."""
+    S = lu.symb
+    xs = S.xsup
+    x = np.array(b, dtype=np.result_type(lu.Lval.dtype, np.float64 if lu.Lval.dtype != np.complex128 else np.complex128)).copy()
+    ns = S.nsupers
+    cols = []
+    for k in range(ns):
+        w = xs[k + 1] - xs[k]
+        idx = lu.Lidx[lu.Loff[k]:]
+        ld = idx[1]
+        blk = lu.Lval[lu.Lvoff[k]:lu.Lvoff[k] + ld * w].reshape(w, ld).T
+        rows, p = [], 2
+        for _ in range(idx[0]):
+            nr = idx[p + 1]
+            rows.extend(idx[p + 2:p + 2 + nr])
+            p += 2 + nr
+        cols.append((blk, np.array(rows)))
+    for k in range(ns):  # forward: L y = b
+        f, l = xs[k], xs[k + 1]
+        blk, rows = cols[k]
+        w = l - f
+        x[f:l] = solve_triangular(blk[:w], x[f:l], lower=True, unit_diagonal=True)
+        if len(rows) > w:
+            x[rows[w:]] -= blk[w:] @ x[f:l]
+    for k in range(ns - 1, -1, -1):  # backward: U x = y
+        f, l = xs[k], xs[k + 1]
+        blk, rows = cols[k]
+        w = l - f
+        if lu.Uoff[k] >= 0:
+            idx = lu.Uidx[lu.Uoff[k]:]
+            v = lu.Uval[lu.Uvoff[k]:]
+            p, q = 3, 0
+            for _ in range(idx[0]):
+                jb = idx[p]
+                for c in range(xs[jb + 1] - xs[jb]):
+                    fst = idx[p + 2 + c]
+                    seg = l - fst
+                    if seg:
+                        x[fst:l] -= v[q:q + seg] * x[xs[jb] + c]
+                    q += seg
+                p += 2 + xs[jb + 1] - xs[jb]
+        x[f:l] = solve_triangular(blk[:w], x[f:l], lower=False)
+    return x
+
+
+def backward_error(A, perm, x_perm, b_perm):
+    """||B x - b|| / (||B|| ||x||) (inf norms) for B = P A P^T."""
+    B = A.permuted(perm)
+    cp, ri, v = B.arrays()
+    n = B.n
+    r = -np.asarray(b_perm, dtype=np.result_type(v, x_perm)).copy()
+    absrow = np.zeros(n)
+    for j in range(n):
+        sl = slice(cp[j], cp[j + 1])
+        r[ri[sl]] += v[sl] * x_perm[j]
+        absrow[ri[sl]] += np.abs(v[sl])
+    return float(np.abs(r).max() / (absrow.max() * np.abs(x_perm).max()))

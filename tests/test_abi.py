@@ -1,0 +1,57 @@
+"""The drop-in boundary: the mirror header reproduces the reference layouts
+byte for byte (tests/golden/abi_layout.json, measured from the reference
+headers by oracle/gen/make_abi_layout.sh), and libslu_mi355x.so exports every
+function include/*.h declares.  CPU only: no compute calls."""
+import ctypes as C
+import json
+import os
+import re
+import shutil
+import subprocess
+import tempfile
+
+import pytest
+
+from conftest import ROOT
+
+
+def _declared_functions():
+    names = []
+    for h in ("slu_mi355x.h",):
+        txt = open(os.path.join(ROOT, "include", h)).read()
+        txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+        for m in re.finditer(r"\b([A-Za-z_][A-Za-z0-9_]*)\s*\(", txt):
+            nm = m.group(1)
+            pre = txt[max(0, m.start() - 40):m.start()]
+            if nm in ("sizeof", "if", "defined") or "typedef" in pre.split(";")[-1]:
+                continue
+            if re.search(r"(int_t|int|void|slu_\w+|char|const char)\s*\**\s*$", pre):
+                names.append(nm)
+    return sorted(set(names))
+
+
+def test_library_exports_every_declared_symbol():
+    lib = C.CDLL(os.path.join(ROOT, "superlu_dist_amd", "lib", "libslu_mi355x.so"))
+    names = _declared_functions()
+    assert {"pdgstrf", "psgstrf", "pzgstrf", "dscatter_l", "dscatter_l_1", "dscatter_u",
+            "zscatter_u", "sscatter_l", "slu_plan_create", "slu_plan_factor"} <= set(names)
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+
+
+@pytest.mark.skipif(shutil.which("gcc") is None or not os.path.exists("/opt/conda/include/mpi.h"),
+                    reason="needs gcc and the MPI header")
+def test_mirror_layout_matches_reference():
+    golden = json.load(open(os.path.join(ROOT, "tests", "golden", "abi_layout.json")))
+    tmp = tempfile.mkdtemp()
+    try:
+        exe = os.path.join(tmp, "probe")
+        subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), "-I",
+                        os.path.join(ROOT, "oracle", "gen"), "-I", "/opt/conda/include",
+                        os.path.join(ROOT, "oracle", "gen", "abi_probe.c"), "-o", exe],
+                       check=True)
+        mine = json.loads(subprocess.run([exe], check=True, capture_output=True,
+                                         text=True).stdout)
+    finally:
+        shutil.rmtree(tmp)
+    assert mine == golden

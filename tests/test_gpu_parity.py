@@ -1,0 +1,98 @@
+"""Parity of the MI355X engine (libslu_mi355x.so, through its C ABI) with the
+reference pdgstrf / psgstrf / pzgstrf.
+
+* every 1x1 golden case: factors vs the REFERENCE's factors
+  (tests/golden/ref_*.npz), info and TinyPivots exact;
+* larger seeded stencils: factors vs the oracle (C restatement);
+* full-size-style property: backward error of the solve with the GPU factors.
+Tolerances (north star): normwise-max relative 1e-12 fp64 / complex, 1e-5 fp32.
+"""
+import numpy as np
+import pytest
+
+import cases
+import pyoracle
+from lusolve import backward_error, solve_1x1
+from superlu_dist_amd.engine import Plan, factor_lustruct
+from superlu_dist_amd.frontend import STENCIL_2D5, STENCIL_3D7, STENCIL_3D27, Csc, Symbolic, nd_order
+from test_oracle import TOL, load_golden
+
+pytestmark = pytest.mark.gpu
+
+ONE_BY_ONE = sorted(n for n, c in cases.CASES.items() if c[2] == (1, 1))
+
+
+@pytest.mark.parametrize("name", ONE_BY_ONE)
+def test_gpu_matches_reference_fixture(name):
+    meta, ref = load_golden(name)
+    A, S, lus = cases.distribute(name)
+    assert cases.structure_digest(lus) == meta["digest"]
+    info, tiny, st = factor_lustruct(lus[0], anorm=meta["anorm"], replace_tiny=meta["replace_tiny"])
+    assert info == meta["ref_info"]
+    assert tiny == meta["ref_tiny"]
+    if info == 0:
+        err = cases.factor_error(lus, ref)
+        assert err < TOL[meta["dtype"]], err
+
+
+@pytest.mark.parametrize("kind,dims,dtype,relax,maxsup", [
+    (STENCIL_3D7, (20, 20, 20), 0, 60, 256),
+    (STENCIL_3D7, (16, 16, 16), 0, 4, 24),
+    (STENCIL_2D5, (60, 60, 1), 0, 60, 256),
+    (STENCIL_3D27, (12, 12, 12), 1, 60, 256),
+    (STENCIL_3D7, (12, 12, 12), 2, 60, 256),
+])
+def test_gpu_matches_oracle_stencil(kind, dims, dtype, relax, maxsup):
+    kw = {}
+    if dtype == 2:
+        kw = dict(diag=6 - 0.25, diag_im=-0.0025)
+    A = Csc.stencil(kind, *dims, dtype=dtype, **kw)
+    S = Symbolic(A, nd_order(*dims), relax, maxsup)
+    gpu, ref = S.distribute(), S.distribute()
+    an = cases.anorm(A)
+    info, tiny, st = factor_lustruct(gpu, anorm=an)
+    o = pyoracle.oracle_factor([ref], 1, 1, A.n, False, an)
+    assert info == o["info"] == 0
+    err = cases.factor_error([gpu], [(ref.Lval, ref.Uval)])
+    assert err < TOL[dtype], err
+    # the plan's algorithmic flop count equals the oracle's accounting
+    assert abs(st["schur_flops"] + st["panel_flops"] - o["flops"]) <= 1e-9 * o["flops"] + 10
+
+
+def test_gpu_backward_error_3d():
+    """Size-independent property at a size the oracle would be slow on."""
+    A = Csc.stencil(STENCIL_3D7, 32, 32, 32)
+    S = Symbolic(A, nd_order(32, 32, 32), 60, 256)
+    lu = S.distribute()
+    info, tiny, st = factor_lustruct(lu, anorm=12.0)
+    assert info == 0
+    rng = np.random.default_rng(1)
+    xt = rng.standard_normal(A.n)
+    B = A.permuted(S.perm_c)
+    cp, ri, v = B.arrays()
+    b = np.zeros(A.n)
+    for j in range(A.n):
+        b[ri[cp[j]:cp[j + 1]]] += v[cp[j]:cp[j + 1]] * xt[j]
+    x = solve_1x1(lu, b)
+    berr = backward_error(A, S.perm_c, x, b)
+    assert berr < 1e-14, berr
+    assert np.abs(x - xt).max() / np.abs(xt).max() < 1e-10
+
+
+def test_gpu_refactor_same_plan_is_reproducible_without_atomics():
+    """A plan can be re-uploaded and re-factored (SamePattern reuse)."""
+    A = Csc.stencil(STENCIL_3D7, 10, 10, 10)
+    S = Symbolic(A, nd_order(10, 10, 10), 60, 256)
+    lu = S.distribute()
+    L0, U0 = lu.Lval.copy(), lu.Uval.copy()
+    p = Plan(lu)
+    outs = []
+    for _ in range(2):
+        lu.Lval[:] = L0
+        lu.Uval[:] = U0
+        p.upload()
+        assert p.factor(12.0) == (0, 0)
+        p.download()
+        outs.append((lu.Lval.copy(), lu.Uval.copy()))
+    assert np.allclose(outs[0][0], outs[1][0], rtol=0, atol=1e-13)
+    assert np.allclose(outs[0][1], outs[1][1], rtol=0, atol=1e-13)
