@@ -128,6 +128,12 @@ int slu_plan_upload(slu_plan *p);
 /* Numeric factorization on the device (inputs resident in HBM).
  * anorm is used for the tiny-pivot threshold as in SRC/pdgstrf.c:412-413. */
 int slu_plan_factor(slu_plan *p, double anorm, int *info, int *tiny_pivots);
+/* Keep a pristine device copy of the uploaded values (snapshot) and restore
+ * the working factor storage from it (benchmark repetitions; device-to-device). */
+int slu_plan_snapshot(slu_plan *p);
+int slu_plan_restore(slu_plan *p);
+/* Wait for all work of the plan's stream. */
+int slu_plan_sync(slu_plan *p);
 /* Copy factors back into the host LUstruct arrays. */
 int slu_plan_download(slu_plan *p);
 void slu_plan_destroy(slu_plan *p);

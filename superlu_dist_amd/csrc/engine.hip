@@ -92,6 +92,9 @@ struct PlanBase {
     virtual void upload() = 0;
     virtual void factor(double anorm, int *info, int *tiny) = 0;
     virtual void download() = 0;
+    virtual void snapshot() = 0;
+    virtual void restore() = 0;
+    virtual void sync() = 0;
     slu_plan_stats stats{};
 };
 
@@ -353,6 +356,8 @@ struct Plan : PlanBase {
     };
     vector<KInfoHost> khost;
 
+    static constexpr bool cplx = sizeof(T) == 16;
+
     void add_supernode(int k, LevelRange &R) {
         LocalLU *Llu = LU->Llu;
         const int w = W(k);
@@ -374,8 +379,9 @@ struct Plan : PlanBase {
             d.fcol = (int)xsup[k];
             diag_items.push_back(d);
             stats.n_diag++;
-            double wd = w;
-            stats.panel_flops += wd * (wd - 1) / 2 + 2 * (wd - 1) * wd * (2 * wd - 1) / 6;
+            // SRC/pdgstrf2.c:252,262 (complex weights SRC/pzgstrf2.c:253,263)
+            double wd = w, s1 = wd * (wd - 1) / 2, s2 = (wd - 1) * wd * (2 * wd - 1) / 6;
+            stats.panel_flops += cplx ? 6 * s1 + 10 * wd + 8 * s2 : s1 + 2 * s2;
         }
         // ---- L panel (rows of column k below the diagonal block)
         int r0 = 0, m = 0;
@@ -399,7 +405,7 @@ struct Plan : PlanBase {
                     tl_items.push_back(t);
                     stats.n_trsm_items++;
                 }
-                stats.panel_flops += (double)w * (w + 1) * m;
+                stats.panel_flops += (cplx ? 4.0 : 1.0) * (double)w * (w + 1) * m;
             }
         }
         // ---- U panel (nonempty columns of block row k)
@@ -590,6 +596,21 @@ struct Plan : PlanBase {
                                      hipMemcpyHostToDevice));
         }
     }
+
+    DevBuf<T> d_L0, d_U0; // pristine copies (snapshot)
+    void snapshot() override {
+        d_L0.alloc(d_L.n);
+        d_U0.alloc(d_U.n);
+        HIPCHK(hipMemcpyAsync(d_L0.p, d_L.p, d_L.bytes(), hipMemcpyDeviceToDevice, stream));
+        HIPCHK(hipMemcpyAsync(d_U0.p, d_U.p, d_U.bytes(), hipMemcpyDeviceToDevice, stream));
+        HIPCHK(hipStreamSynchronize(stream));
+    }
+    void restore() override {
+        SLU_REQUIRE(d_L0.p && d_U0.p, "restore without snapshot");
+        HIPCHK(hipMemcpyAsync(d_L.p, d_L0.p, d_L.bytes(), hipMemcpyDeviceToDevice, stream));
+        HIPCHK(hipMemcpyAsync(d_U.p, d_U0.p, d_U.bytes(), hipMemcpyDeviceToDevice, stream));
+    }
+    void sync() override { HIPCHK(hipStreamSynchronize(stream)); }
 
     void download() override {
         LocalLU *Llu = LU->Llu;
@@ -814,6 +835,36 @@ int slu_plan_factor(slu_plan *p, double anorm, int *info, int *tiny) {
 int slu_plan_download(slu_plan *p) {
     try {
         p->impl->download();
+        return 0;
+    } catch (const std::exception &e) {
+        set_last_error(e.what());
+        return -1;
+    }
+}
+
+int slu_plan_snapshot(slu_plan *p) {
+    try {
+        p->impl->snapshot();
+        return 0;
+    } catch (const std::exception &e) {
+        set_last_error(e.what());
+        return -1;
+    }
+}
+
+int slu_plan_restore(slu_plan *p) {
+    try {
+        p->impl->restore();
+        return 0;
+    } catch (const std::exception &e) {
+        set_last_error(e.what());
+        return -1;
+    }
+}
+
+int slu_plan_sync(slu_plan *p) {
+    try {
+        p->impl->sync();
         return 0;
     } catch (const std::exception &e) {
         set_last_error(e.what());

@@ -67,6 +67,17 @@ class Plan:
         self._chk(lib().slu_plan_factor(self.ptr, anorm, C.byref(info), C.byref(tiny)))
         return info.value, tiny.value
 
+    def snapshot(self):
+        """Keep a pristine device copy of the uploaded values."""
+        self._chk(lib().slu_plan_snapshot(self.ptr))
+
+    def restore(self):
+        """Restore the working factor storage from the snapshot (device to device)."""
+        self._chk(lib().slu_plan_restore(self.ptr))
+
+    def sync(self):
+        self._chk(lib().slu_plan_sync(self.ptr))
+
     def download(self):
         self._chk(lib().slu_plan_download(self.ptr))
 

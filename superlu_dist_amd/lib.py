@@ -93,6 +93,9 @@ def lib():
         "slu_plan_upload": (C.c_int, [P]),
         "slu_plan_factor": (C.c_int, [P, C.c_double, c_intp, c_intp]),
         "slu_plan_download": (C.c_int, [P]),
+        "slu_plan_snapshot": (C.c_int, [P]),
+        "slu_plan_restore": (C.c_int, [P]),
+        "slu_plan_sync": (C.c_int, [P]),
         "slu_plan_destroy": (None, [P]),
         "slu_plan_get_stats": (C.c_int, [P, C.POINTER(PlanStats)]),
         "slu_last_error": (C.c_char_p, []),
