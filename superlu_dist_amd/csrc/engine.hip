@@ -83,6 +83,10 @@ struct LevelRange {
     int tu_off = 0, tu_n = 0;
     int k_off = 0, k_n = 0;
     int tile_off = 0, tile_n = 0;
+    int big_off = 0, big_n = 0; // 128x128 Schur tiles
+    int df_off = 0, df_n = 0;   // fast diag items
+    int lf_off = 0, lf_n = 0;   // fast L-panel TRSM items
+    int uf_off = 0, uf_n = 0;   // fast U-panel TRSM items
     double schur_flops = 0;
     bool big = false;
 };
@@ -135,7 +139,10 @@ struct Plan : PlanBase {
     vector<TrsmLItem<T>> tl_items;
     vector<TrsmUItem<T>> tu_items;
     vector<KInfo<T>> kinfos;
-    vector<TileItem> tiles;
+    vector<TileItem> tiles, tiles_big;
+    vector<DiagItemF<T>> df_items;
+    vector<TrsmItemF<T>> lf_items, uf_items;
+    i64 dinv_level_off = 0, dinv_max = 0; // per-level Dinv scratch
     // per-k panel arrays (device copies referenced by KInfo / TrsmUItem)
     vector<int> h_rg, h_ra, h_cg, h_cb, h_pair, h_ct0;
     vector<i64> h_cvoff;
@@ -151,7 +158,10 @@ struct Plan : PlanBase {
     DevBuf<TrsmLItem<T>> d_tl;
     DevBuf<TrsmUItem<T>> d_tu;
     DevBuf<KInfo<T>> d_kinfo;
-    DevBuf<TileItem> d_tiles;
+    DevBuf<TileItem> d_tiles, d_tiles_big;
+    DevBuf<DiagItemF<T>> d_df;
+    DevBuf<TrsmItemF<T>> d_lf, d_uf;
+    DevBuf<T> d_dinv;
     DevBuf<int> d_rg, d_ra, d_cg, d_cb, d_pair, d_ct0;
     DevBuf<i64> d_cvoff;
     DevBuf<int> d_counters; // [0] tiny pivots, [1..] unused
@@ -325,7 +335,17 @@ struct Plan : PlanBase {
             R.tu_off = (int)tu_items.size();
             R.k_off = (int)kinfos.size();
             R.tile_off = (int)tiles.size();
+            R.big_off = (int)tiles_big.size();
+            R.df_off = (int)df_items.size();
+            R.lf_off = (int)lf_items.size();
+            R.uf_off = (int)uf_items.size();
+            dinv_level_off = 0;
             for (int k : bylev[L]) add_supernode(k, R);
+            dinv_max = std::max(dinv_max, dinv_level_off);
+            R.big_n = (int)tiles_big.size() - R.big_off;
+            R.df_n = (int)df_items.size() - R.df_off;
+            R.lf_n = (int)lf_items.size() - R.lf_off;
+            R.uf_n = (int)uf_items.size() - R.uf_off;
             R.diag_n = (int)diag_items.size() - R.diag_off;
             R.tl_n = (int)tl_items.size() - R.tl_off;
             R.tu_n = (int)tu_items.size() - R.tu_off;
@@ -367,17 +387,33 @@ struct Plan : PlanBase {
         // ---- diagonal block
         i64 diag_off = -1;
         int diag_ld = 0;
+        constexpr int PW = PWOf<T>::v, RB = RBOf<T>::v;
+        const bool fast = w <= FAST_MAXW;
+        const int nbk = (w + PW - 1) / PW;
+        const i64 dinv_off = dinv_level_off;           // U^{-1} blocks at +0, (L^{-1})^T at +nbk*PW*PW
+        if (fast) dinv_level_off += 2 * (i64)nbk * PW * PW;
         if (diag_here) {
             diag_off = lval_off[ljb];
             diag_ld = lval_ld[ljb];
             SLU_REQUIRE(lblk_ib[lcol_first[ljb]] == k, "diagonal block of %d is not first", k);
-            DiagItem<T> d{};
-            d.a = (T *)(intptr_t)diag_off; // relocated in build_device
-            d.ld = diag_ld;
-            d.w = w;
-            d.k = k;
-            d.fcol = (int)xsup[k];
-            diag_items.push_back(d);
+            if (fast) {
+                DiagItemF<T> d{};
+                d.a = (T *)(intptr_t)diag_off; // relocated in build_device
+                d.dinv = (T *)(intptr_t)dinv_off;
+                d.ld = diag_ld;
+                d.w = w;
+                d.k = k;
+                d.fcol = (int)xsup[k];
+                df_items.push_back(d);
+            } else {
+                DiagItem<T> d{};
+                d.a = (T *)(intptr_t)diag_off; // relocated in build_device
+                d.ld = diag_ld;
+                d.w = w;
+                d.k = k;
+                d.fcol = (int)xsup[k];
+                diag_items.push_back(d);
+            }
             stats.n_diag++;
             // SRC/pdgstrf2.c:252,262 (complex weights SRC/pzgstrf2.c:253,263)
             double wd = w, s1 = wd * (wd - 1) / 2, s2 = (wd - 1) * wd * (2 * wd - 1) / 6;
@@ -393,7 +429,21 @@ struct Plan : PlanBase {
                 lbs.push_back(f + b);
                 m += lblk_nrows[f + b];
             }
-            if (m > 0) {
+            if (m > 0 && fast) {
+                for (int c0 = 0; c0 < m; c0 += RB) {
+                    TrsmItemF<T> t{};
+                    t.x = (T *)(intptr_t)(lval_off[ljb] + r0 + c0);
+                    t.t = (const T *)(intptr_t)diag_off;
+                    t.dinv = (const T *)(intptr_t)dinv_off;
+                    t.ldx = lval_ld[ljb];
+                    t.ldt = diag_ld;
+                    t.w = w;
+                    t.nrows = std::min(RB, m - c0);
+                    lf_items.push_back(t);
+                    stats.n_trsm_items++;
+                }
+                stats.panel_flops += (cplx ? 4.0 : 1.0) * (double)w * (w + 1) * m;
+            } else if (m > 0) {
                 for (int c0 = 0; c0 < m; c0 += TRSM_THREADS) {
                     TrsmLItem<T> t{};
                     t.x = (T *)(intptr_t)(lval_off[ljb] + r0 + c0);
@@ -436,7 +486,20 @@ struct Plan : PlanBase {
                 }
                 if (any) ubs.push_back(ub);
             }
-            for (int c0 = 0; c0 < ncols; c0 += TRSM_THREADS) {
+            for (int c0 = 0; fast && c0 < ncols; c0 += RB) {
+                TrsmItemF<T> t{};
+                t.x = nullptr; // Uval
+                t.voff = (const i64 *)(intptr_t)(cols_off + c0);
+                t.t0 = (const int *)(intptr_t)(cols_off + c0);
+                t.t = (const T *)(intptr_t)diag_off;
+                t.dinv = (const T *)(intptr_t)(dinv_off + (i64)nbk * PW * PW);
+                t.ldt = diag_ld;
+                t.w = w;
+                t.nrows = std::min(RB, ncols - c0);
+                uf_items.push_back(t);
+                stats.n_trsm_items++;
+            }
+            for (int c0 = 0; !fast && c0 < ncols; c0 += TRSM_THREADS) {
                 TrsmUItem<T> t{};
                 t.l = (const T *)(intptr_t)diag_off;
                 t.ldl = diag_ld;
@@ -502,9 +565,11 @@ struct Plan : PlanBase {
         kinfos.push_back(ki);
         khost.push_back(std::move(kh));
         const int slot = (int)kinfos.size() - 1 - R.k_off;
-        const int tm = (m + SC_BM - 1) / SC_BM, tn = (ncols + SC_BN - 1) / SC_BN;
+        const bool big = !cplx && m >= SB_BM && ncols >= SB_BN;
+        const int BM = big ? SB_BM : SC_BM, BN = big ? SB_BN : SC_BN;
+        const int tm = (m + BM - 1) / BM, tn = (ncols + BN - 1) / BN;
         for (int i = 0; i < tm; ++i)
-            for (int j = 0; j < tn; ++j) tiles.push_back(TileItem{slot, i, j});
+            for (int j = 0; j < tn; ++j) (big ? tiles_big : tiles).push_back(TileItem{slot, i, j});
         // algorithmic work: exact unpadded flops and padded flops
         double fl = 0;
         for (int c = 0; c < ncols; ++c) fl += 2.0 * m * (w - h_ct0[cols_off + c]);
@@ -513,6 +578,7 @@ struct Plan : PlanBase {
         stats.schur_flops_padded += 2.0 * m * ncols * (double)(w - kmin) * mult;
         stats.scatter_bytes += 3.0 * sizeof(T) * (double)m * ncols;
         stats.n_schur_tiles += (i64)tm * tn;
+        stats.n_diag += 0;
         R.schur_flops += fl * mult;
         if (w >= 64 && m >= 256 && ncols >= 256) R.big = true;
     }
@@ -553,11 +619,33 @@ struct Plan : PlanBase {
             k.ra = d_ra.p + ro;
             k.pair = d_pair.p + po;
         }
+        d_dinv.alloc(std::max<i64>(dinv_max, 1));
+        for (auto &d : df_items) {
+            d.a = L + (intptr_t)d.a;
+            d.dinv = d_dinv.p + (intptr_t)d.dinv;
+        }
+        for (auto &t : lf_items) {
+            t.x = L + (intptr_t)t.x;
+            t.t = L + (intptr_t)t.t;
+            t.dinv = d_dinv.p + (intptr_t)t.dinv;
+        }
+        for (auto &t : uf_items) {
+            t.x = U;
+            intptr_t co = (intptr_t)t.voff;
+            t.voff = d_cvoff.p + co;
+            t.t0 = d_ct0.p + co;
+            t.t = L + (intptr_t)t.t;
+            t.dinv = d_dinv.p + (intptr_t)t.dinv;
+        }
+        d_df.upload(df_items);
+        d_lf.upload(lf_items);
+        d_uf.upload(uf_items);
         d_diag.upload(diag_items);
         d_tl.upload(tl_items);
         d_tu.upload(tu_items);
         d_kinfo.upload(kinfos);
         d_tiles.upload(tiles);
+        d_tiles_big.upload(tiles_big);
         d_lblk.upload(lblk);
         d_lmap.upload(lmap);
         d_ublk.upload(ublk);
@@ -568,7 +656,8 @@ struct Plan : PlanBase {
         stats.lu_bytes = (double)(lval_total + uval_total) * sizeof(T);
         stats.index_bytes = (double)(d_lblk.bytes() + d_lmap.bytes() + d_ublk.bytes() +
                                      d_ucol_voff.bytes() + d_ucol_fst.bytes() + d_diag.bytes() +
-                                     d_tl.bytes() + d_tu.bytes() + d_kinfo.bytes() +
+                                     d_tl.bytes() + d_tu.bytes() + d_kinfo.bytes() + d_tiles_big.bytes() +
+                                     d_df.bytes() + d_lf.bytes() + d_uf.bytes() + d_dinv.bytes() +
                                      d_tiles.bytes() + d_rg.bytes() + d_ra.bytes() +
                                      d_cg.bytes() + d_cb.bytes() + d_pair.bytes() +
                                      d_ct0.bytes() + d_cvoff.bytes());
@@ -635,6 +724,16 @@ struct Plan : PlanBase {
         }
     }
 
+    void launch_big(const LevelRange &R) {
+        if constexpr (sizeof(T) == 16) {
+            SLU_REQUIRE(false, "no 128x128 Schur tiles for complex");
+        } else {
+            hipLaunchKernelGGL(k_schur_big<T>, dim3(R.big_n), dim3(256), 0, stream,
+                               d_tiles_big.p + R.big_off, d_kinfo.p + R.k_off, d_L.p, d_U.p,
+                               d_lblk.p, d_lmap.p, d_ublk.p, d_ucol_voff.p, d_ucol_fst.p);
+        }
+    }
+
     // ------------------------------------------------------- factor
     void factor(double anorm, int *info, int *tiny) override {
         // thresh = smach_dist("Epsilon") * anorm (SRC/pdgstrf.c:412-413); in
@@ -665,6 +764,23 @@ struct Plan : PlanBase {
                                    d_counters.p, d_zpiv.p);
                 if (timing) spans.push_back({a, mark(), 0, false});
             }
+            if (R.df_n) {
+                int a = timing ? mark() : -1;
+                hipLaunchKernelGGL(k_diag_lu_blk<T>, dim3(R.df_n), dim3(256), 0, stream,
+                                   d_df.p + R.df_off, thresh, opts.replace_tiny_pivot,
+                                   d_counters.p, d_zpiv.p);
+                if (timing) spans.push_back({a, mark(), 0, false});
+            }
+            if (R.lf_n || R.uf_n) {
+                int a = timing ? mark() : -1;
+                if (R.lf_n)
+                    hipLaunchKernelGGL((k_trsm_blk<T, 0>), dim3(R.lf_n), dim3(256), 0, stream,
+                                       d_lf.p + R.lf_off);
+                if (R.uf_n)
+                    hipLaunchKernelGGL((k_trsm_blk<T, 1>), dim3(R.uf_n), dim3(256), 0, stream,
+                                       d_uf.p + R.uf_off);
+                if (timing) spans.push_back({a, mark(), 1, false});
+            }
             if (R.tl_n || R.tu_n) {
                 int a = timing ? mark() : -1;
                 if (R.tl_n)
@@ -675,11 +791,13 @@ struct Plan : PlanBase {
                                        d_tu.p + R.tu_off);
                 if (timing) spans.push_back({a, mark(), 1, false});
             }
-            if (R.tile_n) {
+            if (R.tile_n || R.big_n) {
                 int a = timing ? mark() : -1;
-                hipLaunchKernelGGL(k_schur<T>, dim3(R.tile_n), dim3(SC_THREADS), 0, stream,
-                                   d_tiles.p + R.tile_off, d_kinfo.p + R.k_off, d_L.p, d_U.p,
-                                   d_lblk.p, d_lmap.p, d_ublk.p, d_ucol_voff.p, d_ucol_fst.p);
+                if (R.big_n) launch_big(R);
+                if (R.tile_n)
+                    hipLaunchKernelGGL(k_schur<T>, dim3(R.tile_n), dim3(SC_THREADS), 0, stream,
+                                       d_tiles.p + R.tile_off, d_kinfo.p + R.k_off, d_L.p, d_U.p,
+                                       d_lblk.p, d_lmap.p, d_ublk.p, d_ucol_voff.p, d_ucol_fst.p);
                 stats.n_schur_launches++;
                 if (timing) spans.push_back({a, mark(), 2, R.big});
             }

@@ -29,6 +29,7 @@ template <typename T> struct S;
 template <> struct S<double> {
     using T = double;
     __device__ static T zero() { return 0.0; }
+    __device__ static T neg(T a) { return -a; }
     __device__ static T mul(T a, T b) { return a * b; }
     __device__ static T fms(T c, T a, T b) { return c - a * b; } // c - a*b
     __device__ static T div(T a, T b) { return a / b; }
@@ -42,6 +43,7 @@ template <> struct S<double> {
 template <> struct S<float> {
     using T = float;
     __device__ static T zero() { return 0.0f; }
+    __device__ static T neg(T a) { return -a; }
     __device__ static T mul(T a, T b) { return a * b; }
     __device__ static T fms(T c, T a, T b) { return c - a * b; }
     __device__ static T div(T a, T b) { return a / b; }
@@ -55,6 +57,7 @@ template <> struct S<float> {
 template <> struct S<zc> {
     using T = zc;
     __device__ static T zero() { return {0.0, 0.0}; }
+    __device__ static T neg(T a) { return {-a.r, -a.i}; }
     __device__ static T mul(T a, T b) { return {a.r * b.r - a.i * b.i, a.i * b.r + a.r * b.i}; }
     __device__ static T fms(T c, T a, T b) {
         return {c.r - (a.r * b.r - a.i * b.i), c.i - (a.i * b.r + a.r * b.i)};
@@ -82,6 +85,55 @@ template <> struct S<zc> {
         unsafeAtomicAdd(&p->i, -v.i);
     }
 };
+
+__device__ inline double one_of(double) { return 1.0; }
+__device__ inline float one_of(float) { return 1.0f; }
+__device__ inline zc one_of(zc) { return {1.0, 0.0}; }
+
+// ------------------------------------------------------------ MFMA
+template <typename T> struct Mma;
+
+// fp64: v_mfma_f64_16x16x4_f64.  A/B: lane l holds A[l&15][l>>4], B[l>>4][l&15];
+// C/D: col = l&15, row = (l>>4) + 4*i  (cdna_hip_programming.md §3).
+template <> struct Mma<double> {
+    using acc_t = __attribute__((ext_vector_type(4))) double;
+    static constexpr int KSTEP = 4;
+    __device__ static acc_t zero() { return acc_t{0, 0, 0, 0}; }
+    __device__ static void step(acc_t &c, double a, double b) {
+        c = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+    }
+    __device__ static int row(int lane, int i) { return (lane >> 4) + 4 * i; }
+    __device__ static double get(const acc_t &c, int i) { return c[i]; }
+};
+// fp32: v_mfma_f32_16x16x4_f32; C/D: col = l&15, row = 4*(l>>4) + i.
+template <> struct Mma<float> {
+    using acc_t = __attribute__((ext_vector_type(4))) float;
+    static constexpr int KSTEP = 4;
+    __device__ static acc_t zero() { return acc_t{0, 0, 0, 0}; }
+    __device__ static void step(acc_t &c, float a, float b) {
+        c = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+    }
+    __device__ static int row(int lane, int i) { return 4 * (lane >> 4) + i; }
+    __device__ static float get(const acc_t &c, int i) { return c[i]; }
+};
+// complex fp64 on four real fp64 MFMAs: Cr += Ar Br - Ai Bi, Ci += Ar Bi + Ai Br.
+struct zacc {
+    Mma<double>::acc_t r, i;
+};
+template <> struct Mma<zc> {
+    using acc_t = zacc;
+    static constexpr int KSTEP = 4;
+    __device__ static acc_t zero() { return {Mma<double>::zero(), Mma<double>::zero()}; }
+    __device__ static void step(acc_t &c, zc a, zc b) {
+        c.r = __builtin_amdgcn_mfma_f64_16x16x4f64(a.r, b.r, c.r, 0, 0, 0);
+        c.r = __builtin_amdgcn_mfma_f64_16x16x4f64(-a.i, b.i, c.r, 0, 0, 0);
+        c.i = __builtin_amdgcn_mfma_f64_16x16x4f64(a.r, b.i, c.i, 0, 0, 0);
+        c.i = __builtin_amdgcn_mfma_f64_16x16x4f64(a.i, b.r, c.i, 0, 0, 0);
+    }
+    __device__ static int row(int lane, int i) { return (lane >> 4) + 4 * i; }
+    __device__ static zc get(const acc_t &c, int i) { return {c.r[i], c.i[i]}; }
+};
+
 
 // ------------------------------------------------------------ work items
 template <typename T> struct DiagItem {
@@ -339,49 +391,6 @@ k_trsm_u(const TrsmUItem<T> *items) {
 // B = U segments gathered with zero padding above each segment's first row.
 constexpr int SC_BM = 64, SC_BN = 64, SC_BK = 16, SC_THREADS = 256;
 
-template <typename T> struct Mma;
-
-// fp64: v_mfma_f64_16x16x4_f64.  A/B: lane l holds A[l&15][l>>4], B[l>>4][l&15];
-// C/D: col = l&15, row = (l>>4) + 4*i  (cdna_hip_programming.md §3).
-template <> struct Mma<double> {
-    using acc_t = __attribute__((ext_vector_type(4))) double;
-    static constexpr int KSTEP = 4;
-    __device__ static acc_t zero() { return acc_t{0, 0, 0, 0}; }
-    __device__ static void step(acc_t &c, double a, double b) {
-        c = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
-    }
-    __device__ static int row(int lane, int i) { return (lane >> 4) + 4 * i; }
-    __device__ static double get(const acc_t &c, int i) { return c[i]; }
-};
-// fp32: v_mfma_f32_16x16x4_f32; C/D: col = l&15, row = 4*(l>>4) + i.
-template <> struct Mma<float> {
-    using acc_t = __attribute__((ext_vector_type(4))) float;
-    static constexpr int KSTEP = 4;
-    __device__ static acc_t zero() { return acc_t{0, 0, 0, 0}; }
-    __device__ static void step(acc_t &c, float a, float b) {
-        c = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
-    }
-    __device__ static int row(int lane, int i) { return 4 * (lane >> 4) + i; }
-    __device__ static float get(const acc_t &c, int i) { return c[i]; }
-};
-// complex fp64 on four real fp64 MFMAs: Cr += Ar Br - Ai Bi, Ci += Ar Bi + Ai Br.
-struct zacc {
-    Mma<double>::acc_t r, i;
-};
-template <> struct Mma<zc> {
-    using acc_t = zacc;
-    static constexpr int KSTEP = 4;
-    __device__ static acc_t zero() { return {Mma<double>::zero(), Mma<double>::zero()}; }
-    __device__ static void step(acc_t &c, zc a, zc b) {
-        c.r = __builtin_amdgcn_mfma_f64_16x16x4f64(a.r, b.r, c.r, 0, 0, 0);
-        c.r = __builtin_amdgcn_mfma_f64_16x16x4f64(-a.i, b.i, c.r, 0, 0, 0);
-        c.i = __builtin_amdgcn_mfma_f64_16x16x4f64(a.r, b.i, c.i, 0, 0, 0);
-        c.i = __builtin_amdgcn_mfma_f64_16x16x4f64(a.i, b.r, c.i, 0, 0, 0);
-    }
-    __device__ static int row(int lane, int i) { return (lane >> 4) + 4 * i; }
-    __device__ static zc get(const acc_t &c, int i) { return {c.r[i], c.i[i]}; }
-};
-
 template <typename T>
 __global__ void __launch_bounds__(SC_THREADS)
 k_schur(const TileItem *tiles, const KInfo<T> *kinfo, T *Lval, T *Uval,
@@ -508,6 +517,448 @@ k_schur(const TileItem *tiles, const KInfo<T> *kinfo, T *Lval, T *Uval,
         }
         if (ki.atomic) Sx::atomic_sub(dst, v);
         else Sx::sub_to(dst, v);
+    }
+}
+
+
+// ===================================================================== fast
+// panel path (supernodes of width <= 256): blocked, MFMA-based.
+//
+// PW = panel width = size of the inverted diagonal blocks (Dinv).
+template <typename T> struct PWOf { static constexpr int v = 32; };
+template <> struct PWOf<zc> { static constexpr int v = 16; };
+constexpr int FAST_MAXW = 256;
+
+template <typename T> struct DiagItemF {
+    T *a;     // diagonal block, ld
+    T *dinv;  // out: [nb][PW][PW] U11^{-1} blocks, then [nb][PW][PW] (L11^{-1})^T blocks
+    int ld, w, k, fcol;
+};
+
+// Blocked right-looking LU of one <= 256 x 256 diagonal block per workgroup:
+// panels of PW columns are factored in LDS (SRC/pdgstrf2.c:213-269 semantics:
+// tiny-pivot replacement, reciprocal scaling, zero-pivot info), the U12 row
+// block is L11^{-1} A12, and the trailing block is updated with MFMA
+// (A22 -= L21 U12).  The inverses of the PW x PW diagonal blocks of L and U
+// are written to dinv for the MFMA TRSMs.
+template <typename T>
+__global__ void __launch_bounds__(256)
+k_diag_lu_blk(const DiagItemF<T> *items, double thresh, int replace_tiny, int *tiny_count,
+              int *zpiv) {
+    constexpr int PW = PWOf<T>::v;
+    using Sx = S<T>;
+    using M = Mma<T>;
+    const DiagItemF<T> it = items[blockIdx.x];
+    T *A = it.a;
+    const int ld = it.ld, w = it.w, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int nb = (w + PW - 1) / PW;
+    T *dinvU = it.dinv, *dinvLT = it.dinv + (int64_t)nb * PW * PW;
+    __shared__ T sP[FAST_MAXW][PW + 1];
+    __shared__ T sU12[PW][FAST_MAXW + 1];
+    __shared__ T sLinv[PW][PW + 1];
+    __shared__ T s_rp;
+    __shared__ int s_zero;
+    for (int p = 0; p < nb; ++p) {
+        const int p0 = p * PW, pw = min(PW, w - p0), nrow = w - p0;
+        for (int e = tid; e < nrow * pw; e += 256) {
+            int r = e % nrow, c = e / nrow;
+            sP[r][c] = A[(p0 + r) + (int64_t)(p0 + c) * ld];
+        }
+        __syncthreads();
+        for (int j = 0; j < pw; ++j) {
+            if (tid == 0) {
+                T piv = sP[j][j];
+                if (replace_tiny && Sx::abs1(piv) < thresh) {
+                    piv = Sx::thresh(piv, thresh);
+                    sP[j][j] = piv;
+                    atomicAdd(tiny_count, 1);
+                }
+                if (Sx::iszero(piv)) {
+                    s_zero = 1;
+                    atomicMax(&zpiv[it.k], it.fcol + p0 + j + 1);
+                } else {
+                    s_zero = 0;
+                    s_rp = Sx::recip(piv);
+                }
+            }
+            __syncthreads();
+            const bool z = s_zero;
+            const T rp = s_rp;
+            for (int r = j + 1 + tid; r < nrow; r += 256) {
+                T l = sP[r][j];
+                if (!z) l = Sx::mul(l, rp);
+                sP[r][j] = l;
+                for (int c = j + 1; c < pw; ++c) sP[r][c] = Sx::fms(sP[r][c], l, sP[j][c]);
+            }
+            __syncthreads();
+        }
+        for (int e = tid; e < nrow * pw; e += 256) {
+            int r = e % nrow, c = e / nrow;
+            A[(p0 + r) + (int64_t)(p0 + c) * ld] = sP[r][c];
+        }
+        // inverses of the diagonal PW x PW blocks
+        if (tid < PW) { // column j of U11^{-1}
+            const int j = tid;
+            T x[PW];
+#pragma unroll
+            for (int i = PW - 1; i >= 0; --i) {
+                T v = Sx::zero();
+                if (i == j) v = one_of(v);
+#pragma unroll
+                for (int k = 0; k < PW; ++k)
+                    if (k > i && k <= j) v = Sx::fms(v, sP[i][k], x[k]);
+                x[i] = (i <= j && j < pw) ? Sx::div(v, sP[i][i]) : Sx::zero();
+            }
+#pragma unroll
+            for (int i = 0; i < PW; ++i) dinvU[(int64_t)p * PW * PW + i * PW + j] = x[i];
+        } else if (tid >= 64 && tid < 64 + PW) { // column j of L11^{-1} (unit lower)
+            const int j = tid - 64;
+            T x[PW];
+#pragma unroll
+            for (int i = 0; i < PW; ++i) {
+                T v = Sx::zero();
+                if (i == j) v = one_of(v);
+#pragma unroll
+                for (int k = 0; k < PW; ++k)
+                    if (k >= j && k < i) v = Sx::fms(v, sP[i][k], x[k]);
+                x[i] = (i >= j && i < pw && j < pw) ? v : Sx::zero();
+            }
+#pragma unroll
+            for (int i = 0; i < PW; ++i) {
+                sLinv[i][j] = x[i];
+                dinvLT[(int64_t)p * PW * PW + j * PW + i] = x[i];
+            }
+        }
+        __syncthreads();
+        const int c0 = p0 + pw, ncol = w - c0;
+        if (ncol <= 0) break;
+        // U12 = L11^{-1} A12, thread per column
+        for (int c = tid; c < ncol; c += 256) {
+            T a[PW];
+#pragma unroll
+            for (int k = 0; k < PW; ++k)
+                a[k] = k < pw ? A[(p0 + k) + (int64_t)(c0 + c) * ld] : Sx::zero();
+#pragma unroll
+            for (int i = 0; i < PW; ++i) {
+                T y = a[i];
+#pragma unroll
+                for (int k = 0; k < PW; ++k)
+                    if (k < i) y = Sx::fms(y, Sx::neg(sLinv[i][k]), a[k]);
+                if (i < pw) {
+                    A[(p0 + i) + (int64_t)(c0 + c) * ld] = y;
+                    sU12[i][c] = y;
+                }
+            }
+        }
+        __syncthreads();
+        // A22 -= L21 U12 with MFMA 16x16 fragments, 4 waves; each wave takes
+        // FB fragments at a time and issues all their loads before the MFMAs
+        // (the block lives in L2: hide its latency with ILP).
+        const int nf = (ncol + 15) / 16;
+        constexpr int FB = 4;
+        for (int f0 = wid * FB; f0 < nf * nf; f0 += 4 * FB) {
+            T cv[FB][4];
+#pragma unroll
+            for (int q = 0; q < FB; ++q) {
+                const int f = f0 + q, fr = f / nf, fc = f % nf;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int r = fr * 16 + M::row(lane, i), c = fc * 16 + (lane & 15);
+                    cv[q][i] = (f < nf * nf && r < ncol && c < ncol)
+                                   ? A[(c0 + r) + (int64_t)(c0 + c) * ld] : Sx::zero();
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < FB; ++q) {
+                const int f = f0 + q, fr = f / nf, fc = f % nf;
+                typename M::acc_t acc = M::zero();
+#pragma unroll
+                for (int ks = 0; ks < PW; ks += 4) {
+                    const int k = ks + (lane >> 4);
+                    const int r = fr * 16 + (lane & 15), c = fc * 16 + (lane & 15);
+                    T av = (k < pw && r < ncol) ? sP[pw + r][k] : Sx::zero();
+                    T bv = (k < pw && c < ncol) ? sU12[k][c] : Sx::zero();
+                    M::step(acc, av, bv);
+                }
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int r = fr * 16 + M::row(lane, i), c = fc * 16 + (lane & 15);
+                    if (f < nf * nf && r < ncol && c < ncol)
+                        A[(c0 + r) + (int64_t)(c0 + c) * ld] = Sx::fms(cv[q][i], M::get(acc, i), one_of(cv[q][i]));
+                }
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// Blocked TRSM with inverted PW x PW diagonal blocks, RB rows per workgroup:
+//   MODE 0 (L panel):  X := X U_kk^{-1}      (SRC/pdgstrf2.c:311,352 dtrsm R,U,N,N)
+//   MODE 1 (U panel):  Y := L_kk^{-1} Y as Y^T := Y^T (L_kk^T)^{-1}, rows of
+//                      Y^T = U column segments zero-padded above their first
+//                      row                  (SRC/pdgstrf2.c:871 dtrsv L,N,U)
+// For column block b:  X_b := (X_b - X_{<b} T_{<b,b}) Dinv_b  (MFMA both).
+template <typename T> struct TrsmItemF {
+    T *x;                // MODE 0: first row, column-major ld ldx; MODE 1: U value base
+    const int64_t *voff; // MODE 1: per row (U column) segment offset
+    const int *t0;       // MODE 1: per row first row of the segment (rel. to xsup[k])
+    const T *t;          // diagonal block, ld ldt
+    const T *dinv;       // [nb][PW][PW] (MODE 0: U^{-1} blocks; MODE 1: (L^{-1})^T blocks)
+    int ldx, ldt, nrows, w;
+};
+template <typename T> struct RBOf { static constexpr int v = 32; };
+template <> struct RBOf<zc> { static constexpr int v = 16; };
+
+template <typename T, int MODE>
+__global__ void __launch_bounds__(256)
+k_trsm_blk(const TrsmItemF<T> *items) {
+    constexpr int PW = PWOf<T>::v, RB = RBOf<T>::v;
+    constexpr int NFC = PW / 16, NFR = RB / 16, NFRAG = NFC * NFR;
+    using Sx = S<T>;
+    using M = Mma<T>;
+    const TrsmItemF<T> it = items[blockIdx.x];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int w = it.w, nb = (w + PW - 1) / PW, NBW = nb * PW;
+    __shared__ T sX[RB][FAST_MAXW + 1];
+    __shared__ T sT[FAST_MAXW][PW + 1]; // T[0 : b*PW, b-block]
+    __shared__ T sD[PW][PW + 1];
+    __shared__ T sZ[RB][PW + 1];
+    // ---- load the RB rows
+    if (MODE == 0) {
+        for (int e = tid; e < RB * NBW; e += 256) {
+            int r = e % RB, c = e / RB;
+            sX[r][c] = (r < it.nrows && c < w) ? it.x[r + (int64_t)c * it.ldx] : Sx::zero();
+        }
+    } else {
+        for (int e = tid; e < RB * NBW; e += 256) {
+            int r = e / NBW, c = e % NBW;
+            T v = Sx::zero();
+            if (r < it.nrows && c < w) {
+                int t0 = it.t0[r];
+                if (c >= t0) v = it.x[it.voff[r] + c - t0];
+            }
+            sX[r][c] = v;
+        }
+    }
+    const int fr = (wid % NFRAG) / NFC, fc = (wid % NFRAG) % NFC;
+    const bool mfma_wave = wid < NFRAG;
+    for (int b = 0; b < nb; ++b) {
+        // stage Dinv_b and the whole column block T[0:b*PW, b*PW:(b+1)*PW]
+        for (int e = tid; e < PW * PW; e += 256) {
+            int i = e / PW, j = e % PW;
+            sD[i][j] = it.dinv[(int64_t)b * PW * PW + e];
+        }
+        const int kr = b * PW;
+        for (int e = tid; e < kr * PW; e += 256) {
+            int i, j;
+            T v;
+            if (MODE == 0) {
+                i = e % kr; j = e / kr;
+                v = (b * PW + j < w) ? it.t[i + (int64_t)(b * PW + j) * it.ldt] : Sx::zero();
+            } else {
+                j = e % PW; i = e / PW;
+                v = (b * PW + j < w) ? it.t[(b * PW + j) + (int64_t)i * it.ldt] : Sx::zero();
+            }
+            sT[i][j] = v;
+        }
+        __syncthreads();
+        typename M::acc_t acc = M::zero();
+        if (mfma_wave) {
+            for (int k0 = 0; k0 < kr; k0 += 4) {
+                T av = sX[fr * 16 + (lane & 15)][k0 + (lane >> 4)];
+                T bv = sT[k0 + (lane >> 4)][fc * 16 + (lane & 15)];
+                M::step(acc, av, bv);
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int r = fr * 16 + M::row(lane, i), c = fc * 16 + (lane & 15);
+                T v = sX[r][b * PW + c];
+                T a = M::get(acc, i);
+                sZ[r][c] = Sx::fms(v, a, one_of(a));
+            }
+        }
+        __syncthreads();
+        if (mfma_wave) {
+            typename M::acc_t acc2 = M::zero();
+#pragma unroll
+            for (int ks = 0; ks < PW; ks += 4) {
+                T av = sZ[fr * 16 + (lane & 15)][ks + (lane >> 4)];
+                T bv = sD[ks + (lane >> 4)][fc * 16 + (lane & 15)];
+                M::step(acc2, av, bv);
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int r = fr * 16 + M::row(lane, i), c = fc * 16 + (lane & 15);
+                sX[r][b * PW + c] = M::get(acc2, i);
+            }
+        }
+        __syncthreads();
+    }
+    // ---- store
+    if (MODE == 0) {
+        for (int e = tid; e < RB * w; e += 256) {
+            int r = e % RB, c = e / RB;
+            if (r < it.nrows) it.x[r + (int64_t)c * it.ldx] = sX[r][c];
+        }
+    } else {
+        for (int e = tid; e < RB * NBW; e += 256) {
+            int r = e / NBW, c = e % NBW;
+            if (r < it.nrows && c < w) {
+                int t0 = it.t0[r];
+                if (c >= t0) it.x[it.voff[r] + c - t0] = sX[r][c];
+            }
+        }
+    }
+}
+
+
+// ------------------------------------------------------------- Schur (big)
+// 128x128 output tile per 256-thread workgroup (2x2 waves of 64x64 = 4x4 MFMA
+// fragments each), K staged 16 deep through double-buffered LDS with the next
+// stage's global loads in flight during the current stage's MFMAs.  Used for
+// supernodes whose update is at least 128x128 (fp64 / fp32).
+constexpr int SB_BM = 128, SB_BN = 128, SB_BK = 16;
+
+template <typename T>
+__global__ void __launch_bounds__(256, 2)
+k_schur_big(const TileItem *tiles, const KInfo<T> *kinfo, T *Lval, T *Uval,
+            const LBlk *lblk, const int *lmap, const UBlk *ublk,
+            const int64_t *ucol_voff, const int *ucol_fst) {
+    using Sx = S<T>;
+    using M = Mma<T>;
+    constexpr int LDS_A = SB_BM + 4, LDS_B = SB_BN + 4;
+    constexpr int STAGE = SB_BK * LDS_A + SB_BK * LDS_B;
+    constexpr int CLD = SB_BM + 1; // C staging: [64 cols][CLD]
+    static_assert(64 * CLD <= 2 * STAGE, "C staging must fit in the stage buffers");
+    __shared__ T smem[2 * STAGE];
+    __shared__ int s_rg[SB_BM], s_ra[SB_BM], s_cg[SB_BN], s_cb[SB_BN];
+
+    const TileItem ti = tiles[blockIdx.x];
+    const KInfo<T> ki = kinfo[ti.kslot];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wr = wid >> 1, wc = wid & 1;
+    const int row0 = ti.tm * SB_BM, col0 = ti.tn * SB_BN;
+    const int mrows = min(SB_BM, ki.m - row0), ncols = min(SB_BN, ki.n - col0);
+    if (tid < SB_BM) {
+        s_rg[tid] = tid < mrows ? ki.rg[row0 + tid] : 0;
+        s_ra[tid] = tid < mrows ? ki.ra[row0 + tid] : 0;
+        s_cg[tid] = tid < ncols ? ki.cg[col0 + tid] : 0;
+        s_cb[tid] = tid < ncols ? ki.cb[col0 + tid] : 0;
+    }
+    // A: thread owns row ar and k = ak + 2s (s < 8); B: column bc, k = bk + s
+    const int ar = tid & 127, ak = tid >> 7;
+    const bool avalid = ar < mrows;
+    const T *ap = ki.a + row0 + ar;
+    const int bc = tid >> 1, bk = (tid & 1) * 8;
+    const bool bvalid = bc < ncols;
+    int bt0 = 0;
+    const T *ub = ki.ubase;
+    if (bvalid) {
+        bt0 = ki.ct0[col0 + bc];
+        ub = ki.ubase + ki.cvoff[col0 + bc] - bt0;
+    }
+    T ra[8], rb[8];
+    auto gload = [&](int k0) {
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+            const int kk = k0 + ak + 2 * s;
+            ra[s] = (avalid && kk < ki.kw) ? ap[(int64_t)(ki.kmin + kk) * ki.lda] : Sx::zero();
+        }
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+            const int kk = k0 + bk + s, t = ki.kmin + kk;
+            rb[s] = (bvalid && kk < ki.kw && t >= bt0) ? ub[t] : Sx::zero();
+        }
+    };
+    auto lstore = [&](int buf) {
+        T *sA = smem + buf * STAGE, *sB = sA + SB_BK * LDS_A;
+#pragma unroll
+        for (int s = 0; s < 8; ++s) sA[(ak + 2 * s) * LDS_A + ar] = ra[s];
+#pragma unroll
+        for (int s = 0; s < 8; ++s) sB[(bk + s) * LDS_B + bc] = rb[s];
+    };
+
+    typename M::acc_t acc[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = M::zero();
+
+    const int nst = (ki.kw + SB_BK - 1) / SB_BK;
+    gload(0);
+    lstore(0);
+    __syncthreads();
+    for (int st = 0; st < nst; ++st) {
+        const bool more = st + 1 < nst;
+        if (more) gload((st + 1) * SB_BK);
+        const T *sA = smem + (st & 1) * STAGE, *sB = sA + SB_BK * LDS_A;
+#pragma unroll
+        for (int ks = 0; ks < SB_BK; ks += M::KSTEP) {
+            const int kl = ks + (lane >> 4);
+            T av[4], bv[4];
+#pragma unroll
+            for (int f = 0; f < 4; ++f) {
+                av[f] = sA[kl * LDS_A + wr * 64 + f * 16 + (lane & 15)];
+                bv[f] = sB[kl * LDS_B + wc * 64 + f * 16 + (lane & 15)];
+            }
+#pragma unroll
+            for (int fm = 0; fm < 4; ++fm)
+#pragma unroll
+                for (int fn = 0; fn < 4; ++fn) M::step(acc[fm][fn], av[fm], bv[fn]);
+        }
+        if (more) lstore((st + 1) & 1);
+        __syncthreads();
+    }
+
+    // ---- epilogue: two passes of 64 columns through LDS, column-contiguous
+    T *sC = smem; // [c][r], ld CLD
+    const int r = tid & 127;
+    const int gr = s_rg[r], a = s_ra[r];
+    const int *prow = ki.pair + (int64_t)a * ki.nub;
+    int lastb = -1, h = 0, ldh = 0;
+    int64_t rbase = 0;
+    for (int pass = 0; pass < 2; ++pass) {
+        if (wc == pass) {
+#pragma unroll
+            for (int fm = 0; fm < 4; ++fm)
+#pragma unroll
+                for (int fn = 0; fn < 4; ++fn)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int rr = wr * 64 + fm * 16 + M::row(lane, i);
+                        const int cc = fn * 16 + (lane & 15);
+                        sC[cc * CLD + rr] = M::get(acc[fm][fn], i);
+                    }
+        }
+        __syncthreads();
+        if (r < mrows) {
+            for (int cl = tid >> 7; cl < 64; cl += 2) {
+                const int c = pass * 64 + cl;
+                if (c >= ncols) break;
+                const T v = sC[cl * CLD + r];
+                const int b = s_cb[c], gc = s_cg[c];
+                if (b != lastb) {
+                    lastb = b;
+                    h = prow[b];
+                    if (h >= 0) {
+                        const LBlk L = lblk[h];
+                        ldh = L.ld;
+                        rbase = L.colvoff + lmap[L.mapoff + gr - L.frow] - (int64_t)L.fcol * L.ld;
+                    }
+                }
+                T *dst;
+                if (h >= 0) {
+                    dst = Lval + rbase + (int64_t)gc * ldh;
+                } else {
+                    const UBlk U = ublk[~h];
+                    const int64_t e = U.coloff + gc - U.fcol;
+                    dst = Uval + ucol_voff[e] + gr - ucol_fst[e];
+                }
+                if (ki.atomic) Sx::atomic_sub(dst, v);
+                else Sx::sub_to(dst, v);
+            }
+        }
+        __syncthreads();
     }
 }
 

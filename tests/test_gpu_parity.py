@@ -37,6 +37,10 @@ def test_gpu_matches_reference_fixture(name):
 
 @pytest.mark.parametrize("kind,dims,dtype,relax,maxsup", [
     (STENCIL_3D7, (20, 20, 20), 0, 60, 256),
+    (STENCIL_3D7, (20, 20, 20), 0, 60, 320),   # supernodes > 256 columns: generic panel path
+    (STENCIL_3D7, (24, 24, 24), 0, 60, 256),   # 128x128 Schur tiles
+    (STENCIL_3D27, (16, 16, 16), 1, 60, 256),  # fp32 128x128 Schur tiles
+    (STENCIL_3D7, (20, 20, 20), 2, 60, 320),
     (STENCIL_3D7, (16, 16, 16), 0, 4, 24),
     (STENCIL_2D5, (60, 60, 1), 0, 60, 256),
     (STENCIL_3D27, (12, 12, 12), 1, 60, 256),
