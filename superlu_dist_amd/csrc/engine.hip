@@ -387,7 +387,7 @@ struct Plan : PlanBase {
         // ---- diagonal block
         i64 diag_off = -1;
         int diag_ld = 0;
-        constexpr int PW = PWOf<T>::v, RB = RBOf<T>::v;
+        constexpr int PW = PWOf<T>::v, RB = cplx ? RBOf<T>::v : 16 * TR_WAVES;
         const bool fast = w <= FAST_MAXW;
         const int nbk = (w + PW - 1) / PW;
         const i64 dinv_off = dinv_level_off;           // U^{-1} blocks at +0, (L^{-1})^T at +nbk*PW*PW
@@ -724,6 +724,24 @@ struct Plan : PlanBase {
         }
     }
 
+    void launch_trsm_fast(const LevelRange &R) {
+        if constexpr (sizeof(T) == 16) {
+            if (R.lf_n)
+                hipLaunchKernelGGL((k_trsm_blk<T, 0>), dim3(R.lf_n), dim3(256), 0, stream,
+                                   d_lf.p + R.lf_off);
+            if (R.uf_n)
+                hipLaunchKernelGGL((k_trsm_blk<T, 1>), dim3(R.uf_n), dim3(256), 0, stream,
+                                   d_uf.p + R.uf_off);
+        } else {
+            if (R.lf_n)
+                hipLaunchKernelGGL((k_trsm_reg<T, 0>), dim3(R.lf_n), dim3(64 * TR_WAVES), 0, stream,
+                                   d_lf.p + R.lf_off);
+            if (R.uf_n)
+                hipLaunchKernelGGL((k_trsm_reg<T, 1>), dim3(R.uf_n), dim3(64 * TR_WAVES), 0, stream,
+                                   d_uf.p + R.uf_off);
+        }
+    }
+
     void launch_big(const LevelRange &R) {
         if constexpr (sizeof(T) == 16) {
             SLU_REQUIRE(false, "no 128x128 Schur tiles for complex");
@@ -773,12 +791,7 @@ struct Plan : PlanBase {
             }
             if (R.lf_n || R.uf_n) {
                 int a = timing ? mark() : -1;
-                if (R.lf_n)
-                    hipLaunchKernelGGL((k_trsm_blk<T, 0>), dim3(R.lf_n), dim3(256), 0, stream,
-                                       d_lf.p + R.lf_off);
-                if (R.uf_n)
-                    hipLaunchKernelGGL((k_trsm_blk<T, 1>), dim3(R.uf_n), dim3(256), 0, stream,
-                                       d_uf.p + R.uf_off);
+                launch_trsm_fast(R);
                 if (timing) spans.push_back({a, mark(), 1, false});
             }
             if (R.tl_n || R.tu_n) {

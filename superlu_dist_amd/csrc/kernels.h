@@ -556,46 +556,52 @@ k_diag_lu_blk(const DiagItemF<T> *items, double thresh, int replace_tiny, int *t
     __shared__ T sP[FAST_MAXW][PW + 1];
     __shared__ T sU12[PW][FAST_MAXW + 1];
     __shared__ T sLinv[PW][PW + 1];
-    __shared__ T s_rp;
-    __shared__ int s_zero;
+    __shared__ T s_row[2][PW];
+    __shared__ T s_piv[2];
+    __shared__ int s_pz[2];
     for (int p = 0; p < nb; ++p) {
         const int p0 = p * PW, pw = min(PW, w - p0), nrow = w - p0;
-        for (int e = tid; e < nrow * pw; e += 256) {
-            int r = e % nrow, c = e / nrow;
-            sP[r][c] = A[(p0 + r) + (int64_t)(p0 + c) * ld];
-        }
-        __syncthreads();
-        for (int j = 0; j < pw; ++j) {
-            if (tid == 0) {
-                T piv = sP[j][j];
+        // ---- unblocked LU of the nrow x pw panel: thread r keeps row r in
+        // registers; the pivot row is broadcast through LDS (double buffered,
+        // one barrier per column).
+        T xr[PW];
+        const bool own = tid < nrow;
+#pragma unroll
+        for (int c = 0; c < PW; ++c)
+            xr[c] = (own && c < pw) ? A[(p0 + tid) + (int64_t)(p0 + c) * ld] : Sx::zero();
+#pragma unroll
+        for (int j = 0; j < PW; ++j) {
+            if (j < pw && tid == j) { // pivot row owner
+                T piv = xr[j];
                 if (replace_tiny && Sx::abs1(piv) < thresh) {
                     piv = Sx::thresh(piv, thresh);
-                    sP[j][j] = piv;
                     atomicAdd(tiny_count, 1);
                 }
-                if (Sx::iszero(piv)) {
-                    s_zero = 1;
-                    atomicMax(&zpiv[it.k], it.fcol + p0 + j + 1);
-                } else {
-                    s_zero = 0;
-                    s_rp = Sx::recip(piv);
-                }
+                xr[j] = piv;
+                const int z = Sx::iszero(piv);
+                if (z) atomicMax(&zpiv[it.k], it.fcol + p0 + j + 1);
+                s_piv[j & 1] = z ? Sx::zero() : Sx::recip(piv);
+                s_pz[j & 1] = z;
+#pragma unroll
+                for (int c = j + 1; c < PW; ++c) s_row[j & 1][c] = xr[c];
             }
             __syncthreads();
-            const bool z = s_zero;
-            const T rp = s_rp;
-            for (int r = j + 1 + tid; r < nrow; r += 256) {
-                T l = sP[r][j];
-                if (!z) l = Sx::mul(l, rp);
-                sP[r][j] = l;
-                for (int c = j + 1; c < pw; ++c) sP[r][c] = Sx::fms(sP[r][c], l, sP[j][c]);
+            if (j < pw && own && tid > j) {
+                const T rp = s_piv[j & 1];
+                const T l = s_pz[j & 1] ? xr[j] : Sx::mul(xr[j], rp);
+                xr[j] = l;
+#pragma unroll
+                for (int c = j + 1; c < PW; ++c)
+                    if (c < pw) xr[c] = Sx::fms(xr[c], l, s_row[j & 1][c]);
             }
-            __syncthreads();
         }
-        for (int e = tid; e < nrow * pw; e += 256) {
-            int r = e % nrow, c = e / nrow;
-            A[(p0 + r) + (int64_t)(p0 + c) * ld] = sP[r][c];
-        }
+#pragma unroll
+        for (int c = 0; c < PW; ++c)
+            if (own && c < pw) {
+                sP[tid][c] = xr[c];
+                A[(p0 + tid) + (int64_t)(p0 + c) * ld] = xr[c];
+            }
+        __syncthreads();
         // inverses of the diagonal PW x PW blocks
         if (tid < PW) { // column j of U11^{-1}
             const int j = tid;
@@ -959,6 +965,108 @@ k_schur_big(const TileItem *tiles, const KInfo<T> *kinfo, T *Lval, T *Uval,
             }
         }
         __syncthreads();
+    }
+}
+
+
+// TRSM with the RB x w row slab of X held in MFMA A-operand registers
+// (fp64 / fp32): wave q owns rows 16q..16q+15; lane keeps X[row lane&15]
+// [4s + lane>>4] for k-step s.  Column block b: acc = X_{<b} T_{<b,b} (B from
+// LDS), Z = X_b - acc, X_b = Z Dinv_b; results return to A layout through a
+// per-wave LDS tile.  Same MODE convention as k_trsm_blk.
+constexpr int TR_WAVES = 4;
+template <typename T, int MODE>
+__global__ void __launch_bounds__(64 * TR_WAVES, 1)
+k_trsm_reg(const TrsmItemF<T> *items) {
+    constexpr int PW = 32, NKS = FAST_MAXW / 4, NBMAX = FAST_MAXW / PW;
+    using Sx = S<T>;
+    using M = Mma<T>;
+    const TrsmItemF<T> it = items[blockIdx.x];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int w = it.w, nb = (w + PW - 1) / PW;
+    __shared__ T sT[FAST_MAXW - PW][PW + 1];
+    __shared__ T sD[PW][PW + 1];
+    __shared__ T sW[TR_WAVES][16][PW + 1];
+    const int rl = lane & 15, kq = lane >> 4;
+    const int myr = wid * 16 + rl;
+    const bool rv = myr < it.nrows;
+    int64_t rbase = 0;
+    int t0 = 0;
+    if (MODE == 1 && rv) {
+        t0 = it.t0[myr];
+        rbase = it.voff[myr] - t0;
+    }
+    T xa[NKS];
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) {
+        const int k = 4 * s + kq;
+        T v = Sx::zero();
+        if (rv && k < w) {
+            if (MODE == 0) v = it.x[myr + (int64_t)k * it.ldx];
+            else if (k >= t0) v = it.x[rbase + k];
+        }
+        xa[s] = v;
+    }
+    T (*W)[PW + 1] = sW[wid];
+#pragma unroll
+    for (int b = 0; b < NBMAX; ++b) {
+        if (b >= nb) break;
+        __syncthreads();
+        for (int e = tid; e < PW * PW; e += 64 * TR_WAVES) sD[e / PW][e % PW] = it.dinv[(int64_t)b * PW * PW + e];
+        const int kr = b * PW;
+        for (int e = tid; e < kr * PW; e += 64 * TR_WAVES) {
+            int i, j;
+            T v;
+            if (MODE == 0) {
+                i = e % kr; j = e / kr;
+                v = (b * PW + j < w) ? it.t[i + (int64_t)(b * PW + j) * it.ldt] : Sx::zero();
+            } else {
+                j = e % PW; i = e / PW;
+                v = (b * PW + j < w) ? it.t[(b * PW + j) + (int64_t)i * it.ldt] : Sx::zero();
+            }
+            sT[i][j] = v;
+        }
+        __syncthreads();
+        typename M::acc_t a0 = M::zero(), a1 = M::zero();
+#pragma unroll
+        for (int s = 0; s < 8 * b; ++s) {
+            T b0 = sT[4 * s + kq][rl], b1 = sT[4 * s + kq][16 + rl];
+            M::step(a0, xa[s], b0);
+            M::step(a1, xa[s], b1);
+        }
+        // Z = X_b - acc: acc (C layout) -> LDS, read back in A layout
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            W[M::row(lane, i)][rl] = M::get(a0, i);
+            W[M::row(lane, i)][16 + rl] = M::get(a1, i);
+        }
+        __syncthreads();
+        T za[8];
+#pragma unroll
+        for (int s = 0; s < 8; ++s) za[s] = Sx::fms(xa[8 * b + s], W[rl][4 * s + kq], one_of(xa[0]));
+        typename M::acc_t c0 = M::zero(), c1 = M::zero();
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+            M::step(c0, za[s], sD[4 * s + kq][rl]);
+            M::step(c1, za[s], sD[4 * s + kq][16 + rl]);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            W[M::row(lane, i)][rl] = M::get(c0, i);
+            W[M::row(lane, i)][16 + rl] = M::get(c1, i);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int s = 0; s < 8; ++s) xa[8 * b + s] = W[rl][4 * s + kq];
+    }
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) {
+        const int k = 4 * s + kq;
+        if (rv && k < w) {
+            if (MODE == 0) it.x[myr + (int64_t)k * it.ldx] = xa[s];
+            else if (k >= t0) it.x[rbase + k] = xa[s];
+        }
     }
 }
 
