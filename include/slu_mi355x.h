@@ -108,6 +108,15 @@ typedef struct slu_comm slu_comm;
 int slu_comm_unique_id(void *uid_out128);
 slu_comm *slu_comm_create(const void *uid128, int nprow, int npcol, int iam,
                           int device);
+/* Test transport: broadcasts are staged through host memory and delegated
+ * to fn (group 0 = whole grid, 1 = my process row, 2 = my process column;
+ * root = rank within that group; buf holds bytes bytes, valid on the root
+ * and to be filled on the others).  Lets several ranks share one GPU, which
+ * RCCL refuses ("Duplicate GPU"); the kernels are the same as with RCCL. */
+typedef int (*slu_host_bcast_fn)(void *ctx, int group, int root, void *buf,
+                                 int64_t bytes);
+slu_comm *slu_comm_create_host(slu_host_bcast_fn fn, void *ctx, int nprow,
+                               int npcol, int iam, int device);
 void slu_comm_destroy(slu_comm *c);
 
 /* Engine options (everything the kernels need beyond the LUstruct). */
@@ -150,9 +159,11 @@ typedef struct {
     double index_bytes;        /* device bytes of plan index tables */
     /* timing of the last slu_plan_factor (ms), when opts.timing */
     double t_total_ms, t_diag_ms, t_trsm_ms, t_schur_ms, t_comm_ms;
-    double t_schur_big_ms;     /* Schur launches of levels with >= 1 big GEMM */
-    double schur_big_flops;
+    double t_schur_big_ms;     /* k_schur_big launches (128x128 tiles) */
+    double schur_big_flops;    /* flops of the supernodes on 128x128 tiles */
     int64_t n_schur_launches;
+    int64_t n_schur_big_launches;
+    double comm_bytes;         /* bytes this rank sends + receives per factor */
 } slu_plan_stats;
 int slu_plan_get_stats(const slu_plan *p, slu_plan_stats *st);
 

@@ -1,19 +1,23 @@
 // MI355X numeric factorization engine: plan construction (host), level-
 // synchronous execution of the batched kernels in kernels.h, RCCL panel
-// exchange for 2D grids, and the engine C API of include/slu_mi355x.h.
+// exchange for 2D process grids, and the engine C API of include/slu_mi355x.h.
 //
 // Algorithm (what replaces the k-loop of SRC/pdgstrf.c:1108-1756):
 //   The supernodal dependency DAG (k -> ib for every block L(ib,k), k -> jb
 //   for every block U(k,jb)) is levelled once at plan time.  Supernodes of one
-//   level are independent, so for each level the engine launches
-//     1. k_diag_lu  on all diagonal blocks of the level owned by this rank,
-//     2. (grids) broadcast of the factored diagonal blocks along process rows
-//        and columns,
-//     3. k_trsm_l / k_trsm_u on every local L / U panel block of the level,
-//     4. (grids) broadcast of L panels along process rows and U panels along
-//        process columns (RCCL grouped broadcasts),
-//     5. k_schur over every (L row tile x U column tile) of every supernode of
-//        the level, scattering straight into the destination blocks.
+//   level are independent, so for each level every rank launches
+//     1. k_diag_lu(_blk) on the diagonal blocks of the level it owns
+//        (SRC/pdgstrf2.c:213-269),
+//     2. (grids) one grouped broadcast of the factored diagonal blocks (+ their
+//        inverted 32x32 diagonal sub-blocks) along process rows and columns
+//        (SRC/pdgstrf2.c:280-289 sends U(k,k) down the column),
+//     3. k_trsm_* on every local L / U panel block of the level
+//        (SRC/pdgstrf2.c:302-355, 843-887),
+//     4. (grids) one grouped broadcast of the level's L panels along process
+//        rows and U panels along process columns (SRC/pdgstrf.c:1020-1729),
+//     5. k_schur(_big) over every (L row tile x U column tile) of every
+//        supernode of the level, scattering straight into the destination
+//        blocks (SRC/dSchCompUdt-2Ddynamic.c, SRC/dscatter.c:110-277).
 //   The set of updates and the per-element arithmetic are those of the
 //   reference; only the order in which independent updates are applied
 //   differs (the reference orders them by its static schedule,
@@ -68,14 +72,103 @@ template <typename T> struct DevBuf {
 } // namespace slu
 
 // ------------------------------------------------------------------ comm
+// One rank per GPU.  Production transport: RCCL communicators for the whole
+// grid, its process rows and its process columns (the reference's
+// grid->comm / rscp / cscp, SRC/superlu_grid.c:158-172).  Test transport
+// (slu_comm_create_host): host-staged broadcasts through a caller callback,
+// for several ranks sharing one GPU where RCCL refuses duplicate devices.
 struct slu_comm {
     int nprow = 1, npcol = 1, iam = 0, myrow = 0, mycol = 0, device = 0;
     ncclComm_t world = nullptr, row = nullptr, col = nullptr;
+    slu_host_bcast_fn host_fn = nullptr;
+    void *host_ctx = nullptr;
 };
 
 namespace slu {
 
 using i64 = int64_t;
+
+enum { G_WORLD = 0, G_ROW = 1, G_COL = 2 };
+
+// Grouped broadcasts of device buffers within the world / a process row /
+// a process column.  Ops are queued and issued together by flush() (one
+// ncclGroupStart/End); every member of a communicator queues the same ops in
+// the same order, which the plan guarantees by construction.
+struct Xport {
+    slu_comm *c = nullptr;
+    hipStream_t s = nullptr;
+    struct Op {
+        int g, root;
+        void *buf;
+        size_t bytes;
+    };
+    vector<Op> ops;
+    vector<char> hbuf;
+    int gsize(int g) const {
+        return g == G_WORLD ? c->nprow * c->npcol : g == G_ROW ? c->npcol : c->nprow;
+    }
+    int grank(int g) const { return g == G_WORLD ? c->iam : g == G_ROW ? c->mycol : c->myrow; }
+    ncclComm_t comm_of(int g) const { return g == G_WORLD ? c->world : g == G_ROW ? c->row : c->col; }
+    void bcast(int g, int root, void *buf, size_t bytes) {
+        if (bytes && gsize(g) > 1) ops.push_back({g, root, buf, bytes});
+    }
+    void flush() {
+        if (ops.empty()) return;
+        if (c->host_fn) {
+            HIPCHK(hipStreamSynchronize(s));
+            for (auto &o : ops) {
+                hbuf.resize(o.bytes);
+                const bool root = grank(o.g) == o.root;
+                if (root) HIPCHK(hipMemcpy(hbuf.data(), o.buf, o.bytes, hipMemcpyDeviceToHost));
+                SLU_REQUIRE(c->host_fn(c->host_ctx, o.g, o.root, hbuf.data(), (int64_t)o.bytes) == 0,
+                            "host broadcast (group %d, root %d, %zu bytes) failed", o.g, o.root,
+                            o.bytes);
+                if (!root) HIPCHK(hipMemcpy(o.buf, hbuf.data(), o.bytes, hipMemcpyHostToDevice));
+            }
+        } else {
+            NCCLCHK(ncclGroupStart());
+            for (auto &o : ops)
+                NCCLCHK(ncclBroadcast(o.buf, o.buf, o.bytes, ncclChar, o.root, comm_of(o.g), s));
+            NCCLCHK(ncclGroupEnd());
+        }
+        ops.clear();
+    }
+    // plan-time all-gather of variable-length int64 blobs within group g
+    vector<vector<i64>> allgatherv(int g, const vector<i64> &mine) {
+        const int P = gsize(g), me = grank(g);
+        vector<vector<i64>> out(P);
+        if (P == 1) {
+            out[0] = mine;
+            return out;
+        }
+        DevBuf<i64> dsz;
+        dsz.alloc(P);
+        vector<i64> sz(P, 0);
+        sz[me] = (i64)mine.size();
+        HIPCHK(hipMemcpy(dsz.p, sz.data(), P * sizeof(i64), hipMemcpyHostToDevice));
+        for (int r = 0; r < P; ++r) bcast(g, r, dsz.p + r, sizeof(i64));
+        flush();
+        HIPCHK(hipStreamSynchronize(s));
+        HIPCHK(hipMemcpy(sz.data(), dsz.p, P * sizeof(i64), hipMemcpyDeviceToHost));
+        vector<i64> off(P + 1, 0);
+        for (int r = 0; r < P; ++r) off[r + 1] = off[r] + sz[r];
+        DevBuf<i64> d;
+        d.alloc(std::max<i64>(off[P], 1));
+        if (!mine.empty())
+            HIPCHK(hipMemcpy(d.p + off[me], mine.data(), mine.size() * sizeof(i64),
+                             hipMemcpyHostToDevice));
+        for (int r = 0; r < P; ++r) bcast(g, r, d.p + off[r], sz[r] * sizeof(i64));
+        flush();
+        HIPCHK(hipStreamSynchronize(s));
+        for (int r = 0; r < P; ++r) {
+            out[r].resize(sz[r]);
+            if (sz[r])
+                HIPCHK(hipMemcpy(out[r].data(), d.p + off[r], sz[r] * sizeof(i64),
+                                 hipMemcpyDeviceToHost));
+        }
+        return out;
+    }
+};
 
 struct LevelRange {
     int diag_off = 0, diag_n = 0;
@@ -87,8 +180,18 @@ struct LevelRange {
     int df_off = 0, df_n = 0;   // fast diag items
     int lf_off = 0, lf_n = 0;   // fast L-panel TRSM items
     int uf_off = 0, uf_n = 0;   // fast U-panel TRSM items
-    double schur_flops = 0;
+    int dc_off = 0, dc_n = 0;   // diag-package copy items (2D grids)
+    int pc_off = 0, pc_n = 0;   // panel-section copy items (2D grids)
+    int ds_off = 0, ds_n = 0;   // diag-package broadcasts
+    int ps_off = 0, ps_n = 0;   // panel broadcasts
+    double schur_flops = 0, big_flops = 0;
     bool big = false;
+};
+
+// one broadcast of a contiguous section of a device arena
+struct Sec {
+    int g, root, arena; // arena 0: diag packages, 1: panels
+    i64 off, cnt;       // in elements
 };
 
 struct PlanBase {
@@ -104,6 +207,17 @@ struct PlanBase {
 
 // One rank's plan for value type T (double / float / zc) over the host
 // LUstruct layout LocalLU / LUS.
+//
+// 2D grid (SRC/superlu_defs.h:260-270): block (I,J) lives on rank
+// (I mod Pr, J mod Pc).  For supernode k, rank (r,c) needs
+//   * L(:,k) restricted to process row r   -- held by (r, k mod Pc),
+//   * U(k,:) restricted to process column c -- held by (k mod Pr, c),
+//   * the factored diagonal block           -- held by (k mod Pr, k mod Pc)
+//     when r == k mod Pr (U-panel TRSM) or c == k mod Pc (L-panel TRSM).
+// The plan exchanges the index arrays once (row / column all-gathers), levels
+// the global dependency DAG identically on every rank, and lays out per-level
+// broadcast sections so that a level is: diag LU -> diag-package broadcast ->
+// panel TRSMs -> L-panel (row) / U-panel (column) broadcasts -> Schur update.
 template <typename T, typename HT, typename LocalLU, typename LUS>
 struct Plan : PlanBase {
     // ---- problem
@@ -114,26 +228,36 @@ struct Plan : PlanBase {
     vector<i64> xsup;
     int nlc = 0, nlr = 0;
     hipStream_t stream = nullptr;
+    bool xmode = false; // 2D grid with exchanges
+    Xport X;
 
-    // ---- local storage layout
+    // ---- local storage layout (destinations)
     vector<i64> lval_off, uval_off; // per local column / row, -1 if empty
     vector<int> lval_ld;            // nsupr per local column
     i64 lval_total = 0, uval_total = 0;
     bool l_contig = false, u_contig = false;
-    // L blocks (column-major order of columns, storage order within)
     vector<LBlk> lblk;
-    vector<int> lblk_ib, lblk_rowstart, lblk_nrows;
+    vector<int> lblk_ib;
     vector<int> lcol_first, lcol_nblk; // per local column
     vector<int> lmap;
-    // U blocks
     vector<UBlk> ublk;
     vector<int> ublk_jb;
     vector<int> urow_first, urow_nblk;
     vector<i64> ucol_voff;
     vector<int> ucol_fst;
 
+    // ---- panels of every supernode as seen from this rank
+    vector<const int_t *> lidx; // L(:,k) on my process row (reference index format) or null
+    vector<const int_t *> uidx; // U(k,:) on my process column or null
+    vector<vector<i64>> xL, xU; // received index blobs (own the remote lidx/uidx)
+    vector<i64> lpos, upos;     // remote panel value offsets in d_pan (-1: local / none)
+    vector<i64> pkg;            // diag package offset in d_dpk (2D grids), -1 none
+    vector<i64> dscr;           // 1x1: Dinv offset in the per-level scratch
+    i64 dpk_total = 0, pan_total = 0, dscr_max = 0;
+
     // ---- schedule
     vector<int> level_of;
+    vector<vector<int>> bylev;
     vector<LevelRange> levels;
     vector<DiagItem<T>> diag_items;
     vector<TrsmLItem<T>> tl_items;
@@ -142,13 +266,14 @@ struct Plan : PlanBase {
     vector<TileItem> tiles, tiles_big;
     vector<DiagItemF<T>> df_items;
     vector<TrsmItemF<T>> lf_items, uf_items;
-    i64 dinv_level_off = 0, dinv_max = 0; // per-level Dinv scratch
+    vector<CopyItem<T>> dcopy, pcopy;
+    vector<Sec> dsecs, psecs;
     // per-k panel arrays (device copies referenced by KInfo / TrsmUItem)
     vector<int> h_rg, h_ra, h_cg, h_cb, h_pair, h_ct0;
     vector<i64> h_cvoff;
 
     // ---- device
-    DevBuf<T> d_L, d_U;
+    DevBuf<T> d_L, d_U, d_dpk, d_pan, d_dinv;
     DevBuf<LBlk> d_lblk;
     DevBuf<int> d_lmap;
     DevBuf<UBlk> d_ublk;
@@ -161,13 +286,19 @@ struct Plan : PlanBase {
     DevBuf<TileItem> d_tiles, d_tiles_big;
     DevBuf<DiagItemF<T>> d_df;
     DevBuf<TrsmItemF<T>> d_lf, d_uf;
-    DevBuf<T> d_dinv;
+    DevBuf<CopyItem<T>> d_dcopy, d_pcopy;
     DevBuf<int> d_rg, d_ra, d_cg, d_cb, d_pair, d_ct0;
     DevBuf<i64> d_cvoff;
-    DevBuf<int> d_counters; // [0] tiny pivots, [1..] unused
+    DevBuf<int> d_counters; // [0] tiny pivots
     DevBuf<int> d_zpiv;     // per supernode: max zero-pivot column + 1
+    DevBuf<i64> d_info;     // 2D grids: all-gather of the per-rank info
+
+    static constexpr bool cplx = sizeof(T) == 16;
+    static constexpr int PW = PWOf<T>::v;
 
     int W(i64 k) const { return (int)(xsup[k + 1] - xsup[k]); }
+    bool fast_w(int w) const { return w <= FAST_MAXW; }
+    i64 dinv_len(int w) const { return fast_w(w) ? 2 * (i64)((w + PW - 1) / PW) * PW * PW : 0; }
 
     Plan(LUS *lu, int n_, int nprow, int npcol, int iam_, slu_comm *c,
          const slu_engine_opts *o) {
@@ -180,10 +311,17 @@ struct Plan : PlanBase {
         mycol = iam % Pc;
         comm = c;
         if (o) opts = *o;
-        SLU_REQUIRE(Pr * Pc == 1 || (comm && comm->world),
-                    "a %dx%d grid needs an RCCL communicator", Pr, Pc);
+        xmode = Pr * Pc > 1;
+        SLU_REQUIRE(!xmode || (comm && (comm->world || comm->host_fn)),
+                    "a %dx%d grid needs a communicator (slu_comm_create)", Pr, Pc);
+        if (xmode)
+            SLU_REQUIRE(comm->nprow == Pr && comm->npcol == Pc && comm->iam == iam,
+                        "communicator is for a %dx%d grid rank %d, plan for %dx%d rank %d",
+                        comm->nprow, comm->npcol, comm->iam, Pr, Pc, iam);
         if (comm) HIPCHK(hipSetDevice(comm->device));
         HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+        X.c = comm;
+        X.s = stream;
         int_t *hx = LU->Glu_persist->xsup;
         nsupers = (int)(LU->Glu_persist->supno[n - 1] + 1);
         xsup.assign(hx, hx + nsupers + 1);
@@ -191,8 +329,10 @@ struct Plan : PlanBase {
         nlr = (nsupers + Pr - 1) / Pr;
         for (int k = 0; k < nsupers; ++k)
             SLU_REQUIRE(W(k) <= 512, "supernode %d has %d columns (> MAX_SUPER_SIZE 512)", k, W(k));
-        SLU_REQUIRE(Pr * Pc == 1, "multi-rank grids: see build_exchange (not yet enabled)");
         build_local();
+        exchange_index();
+        compute_levels();
+        layout_values();
         build_schedule();
         build_device();
     }
@@ -224,6 +364,7 @@ struct Plan : PlanBase {
             int rs = 0;
             for (int b = 0; b < nb; ++b) {
                 int gb = (int)index[p], nr = (int)index[p + 1];
+                SLU_REQUIRE(gb % Pr == myrow, "L block (%d,%d) is not on process row %d", gb, jb, myrow);
                 LBlk L{};
                 L.colvoff = off;
                 L.mapoff = (i64)lmap.size();
@@ -237,8 +378,6 @@ struct Plan : PlanBase {
                 }
                 lblk.push_back(L);
                 lblk_ib.push_back(gb);
-                lblk_rowstart.push_back(rs);
-                lblk_nrows.push_back(nr);
                 rs += nr;
                 p += SLU_LB_DESCRIPTOR + nr;
             }
@@ -267,6 +406,7 @@ struct Plan : PlanBase {
             i64 klst = xsup[gb + 1];
             for (int b = 0; b < nb; ++b) {
                 int jb = (int)index[p];
+                SLU_REQUIRE(jb % Pc == mycol, "U block (%d,%d) is not on process column %d", gb, jb, mycol);
                 UBlk U{};
                 U.coloff = (i64)ucol_voff.size();
                 U.fcol = (int)xsup[jb];
@@ -302,33 +442,294 @@ struct Plan : PlanBase {
         return (int)(it - ublk_jb.begin());
     }
 
-    // ------------------------------------------------------- schedule
-    void build_schedule() {
-        // dependency levels (1x1: the whole DAG is local)
+    // length of an index array in the reference formats
+    i64 lidx_len(const int_t *ix) const {
+        i64 p = SLU_BC_HEADER;
+        for (i64 b = 0; b < ix[0]; ++b) p += SLU_LB_DESCRIPTOR + ix[p + 1];
+        return p;
+    }
+    i64 uidx_len(const int_t *ix) const {
+        i64 p = SLU_BR_HEADER;
+        for (i64 b = 0; b < ix[0]; ++b) p += SLU_UB_DESCRIPTOR + W(ix[p]);
+        return p;
+    }
+    // rows of L(:,k) on my process row below the diagonal block, and the
+    // number of rows of the diagonal block stored on top (0 or W(k))
+    void lrows(int k, int &m, int &r0) const {
+        m = r0 = 0;
+        const int_t *ix = lidx[k];
+        if (!ix) return;
+        i64 p = SLU_BC_HEADER;
+        for (i64 b = 0; b < ix[0]; ++b) {
+            int nr = (int)ix[p + 1];
+            if (ix[p] == k) r0 += nr;
+            else m += nr;
+            p += SLU_LB_DESCRIPTOR + nr;
+        }
+    }
+
+    // ------------------------------------------------------- index exchange
+    // The reference ships lsub/usub with every panel message
+    // (SRC/pdgstrf.c:1039-1044,1330-1335); the structure never changes during
+    // the factorization, so it is exchanged once here.
+    void exchange_index() {
+        LocalLU *Llu = LU->Llu;
+        lidx.assign(nsupers, nullptr);
+        uidx.assign(nsupers, nullptr);
+        for (int ljb = 0; ljb < nlc; ++ljb)
+            if (ljb * Pc + mycol < nsupers) lidx[ljb * Pc + mycol] = Llu->Lrowind_bc_ptr[ljb];
+        for (int lb = 0; lb < nlr; ++lb)
+            if (lb * Pr + myrow < nsupers) uidx[lb * Pr + myrow] = Llu->Ufstnz_br_ptr[lb];
+        if (!xmode) return;
+        if (Pc > 1) {
+            vector<i64> blob;
+            for (int ljb = 0; ljb < nlc; ++ljb) {
+                const int_t *ix = Llu->Lrowind_bc_ptr[ljb];
+                if (!ix) continue;
+                i64 len = lidx_len(ix);
+                blob.push_back(ljb);
+                blob.push_back(len);
+                blob.insert(blob.end(), ix, ix + len);
+            }
+            xL = X.allgatherv(G_ROW, blob);
+            for (int c = 0; c < Pc; ++c) {
+                if (c == mycol) continue;
+                const vector<i64> &v = xL[c];
+                for (size_t p = 0; p < v.size();) {
+                    i64 ljb = v[p], len = v[p + 1];
+                    lidx[ljb * Pc + c] = (const int_t *)&v[p + 2];
+                    p += 2 + len;
+                }
+            }
+        }
+        if (Pr > 1) {
+            vector<i64> blob;
+            for (int lb = 0; lb < nlr; ++lb) {
+                const int_t *ix = Llu->Ufstnz_br_ptr[lb];
+                if (!ix) continue;
+                i64 len = uidx_len(ix);
+                blob.push_back(lb);
+                blob.push_back(len);
+                blob.insert(blob.end(), ix, ix + len);
+            }
+            xU = X.allgatherv(G_COL, blob);
+            for (int r = 0; r < Pr; ++r) {
+                if (r == myrow) continue;
+                const vector<i64> &v = xU[r];
+                for (size_t p = 0; p < v.size();) {
+                    i64 lb = v[p], len = v[p + 1];
+                    uidx[lb * Pr + r] = (const int_t *)&v[p + 2];
+                    p += 2 + len;
+                }
+            }
+        }
+    }
+
+    // ------------------------------------------------------- levels
+    // Dependency DAG k -> ib (L(ib,k) != 0) and k -> jb (U(k,jb) != 0); all
+    // edges point to larger supernode numbers, so one ascending sweep gives
+    // the longest-path level.  On a grid every rank contributes its local
+    // blocks and all ranks compute the same levels.
+    void compute_levels() {
+        vector<i64> edges;
+        for (int ljb = 0; ljb < nlc; ++ljb) {
+            int k = ljb * Pc + mycol;
+            if (k >= nsupers || !lidx[k]) continue;
+            const int_t *ix = lidx[k];
+            i64 p = SLU_BC_HEADER;
+            for (i64 b = 0; b < ix[0]; ++b) {
+                if (ix[p] != k) {
+                    edges.push_back(k);
+                    edges.push_back(ix[p]);
+                }
+                p += SLU_LB_DESCRIPTOR + ix[p + 1];
+            }
+        }
+        for (int lb = 0; lb < nlr; ++lb) {
+            int k = lb * Pr + myrow;
+            if (k >= nsupers || !uidx[k]) continue;
+            const int_t *ix = uidx[k];
+            i64 p = SLU_BR_HEADER;
+            for (i64 b = 0; b < ix[0]; ++b) {
+                edges.push_back(k);
+                edges.push_back(ix[p]);
+                p += SLU_UB_DESCRIPTOR + W(ix[p]);
+            }
+        }
+        vector<vector<i64>> all;
+        if (xmode) all = X.allgatherv(G_WORLD, edges);
+        else all.push_back(std::move(edges));
+        // CSR of the edges by source
+        vector<i64> cnt(nsupers + 1, 0);
+        for (auto &v : all)
+            for (size_t e = 0; e < v.size(); e += 2) cnt[v[e] + 1]++;
+        for (int k = 0; k < nsupers; ++k) cnt[k + 1] += cnt[k];
+        vector<int> tgt(cnt[nsupers]);
+        vector<i64> fill(cnt.begin(), cnt.end() - 1);
+        for (auto &v : all)
+            for (size_t e = 0; e < v.size(); e += 2) {
+                SLU_REQUIRE(v[e + 1] > v[e] && v[e + 1] < nsupers, "bad dependency %lld -> %lld",
+                            (long long)v[e], (long long)v[e + 1]);
+                tgt[fill[v[e]]++] = (int)v[e + 1];
+            }
         level_of.assign(nsupers, 0);
         int maxlev = 0;
         for (int k = 0; k < nsupers; ++k) {
-            int lk = level_of[k];
-            maxlev = std::max(maxlev, lk);
-            int ljb = k / Pc;
-            for (int b = 0; b < lcol_nblk[ljb]; ++b) {
-                int ib = lblk_ib[lcol_first[ljb] + b];
-                if (ib != k) level_of[ib] = std::max(level_of[ib], lk + 1);
-            }
-            int lb = k / Pr;
-            for (int b = 0; b < urow_nblk[lb]; ++b) {
-                int jb = ublk_jb[urow_first[lb] + b];
-                level_of[jb] = std::max(level_of[jb], lk + 1);
-            }
+            maxlev = std::max(maxlev, level_of[k]);
+            for (i64 e = cnt[k]; e < cnt[k + 1]; ++e)
+                level_of[tgt[e]] = std::max(level_of[tgt[e]], level_of[k] + 1);
         }
-        vector<vector<int>> bylev(maxlev + 1);
+        bylev.assign(maxlev + 1, {});
         for (int k = 0; k < nsupers; ++k) bylev[level_of[k]].push_back(k);
-        levels.resize(maxlev + 1);
+        levels.assign(maxlev + 1, LevelRange{});
         stats.nsupers = nsupers;
         stats.nlevels = maxlev + 1;
+    }
 
+    // ------------------------------------------------------- value layout
+    // Diagonal packages [w*w factored block, ld w | Dinv] and remote panels
+    // are laid out per level in broadcast order: sections of the owners in my
+    // process column (root = their process row), then of my process row.
+    bool lsend(int k) const { // L(:,k) on my process row has rows below the diagonal block
+        int m, r0;
+        lrows(k, m, r0);
+        return m > 0;
+    }
+    void layout_values() {
+        pkg.assign(nsupers, -1);
+        dscr.assign(nsupers, -1);
+        lpos.assign(nsupers, -1);
+        upos.assign(nsupers, -1);
+        for (size_t L = 0; L < levels.size(); ++L) {
+            LevelRange &R = levels[L];
+            const vector<int> &ks = bylev[L];
+            if (!xmode) { // 1x1: Dinv in a per-level scratch
+                i64 off = 0;
+                for (int k : ks) {
+                    dscr[k] = off;
+                    off += dinv_len(W(k));
+                }
+                dscr_max = std::max(dscr_max, off);
+                continue;
+            }
+            // ---- diag packages: owner (r, mycol) for all r, then (myrow, c), c != mycol
+            vector<i64> own_off(Pr * Pc, -1), own_cnt(Pr * Pc, 0);
+            auto lay_owner = [&](int orow, int ocol) {
+                const int o = orow * Pc + ocol;
+                i64 start = dpk_total;
+                for (int k : ks)
+                    if (k % Pr == orow && k % Pc == ocol) {
+                        pkg[k] = dpk_total;
+                        dpk_total += (i64)W(k) * W(k) + dinv_len(W(k));
+                    }
+                own_off[o] = start;
+                own_cnt[o] = dpk_total - start;
+            };
+            for (int r = 0; r < Pr; ++r) lay_owner(r, mycol);
+            for (int c = 0; c < Pc; ++c)
+                if (c != mycol) lay_owner(myrow, c);
+            R.ds_off = (int)dsecs.size();
+            if (Pr > 1)
+                for (int r = 0; r < Pr; ++r) {
+                    int o = r * Pc + mycol;
+                    if (own_cnt[o]) dsecs.push_back({G_COL, r, 0, own_off[o], own_cnt[o]});
+                }
+            if (Pc > 1)
+                for (int c = 0; c < Pc; ++c) {
+                    int o = myrow * Pc + c;
+                    if (own_cnt[o]) dsecs.push_back({G_ROW, c, 0, own_off[o], own_cnt[o]});
+                }
+            R.ds_n = (int)dsecs.size() - R.ds_off;
+            // ---- panels: L(:,k) along my process row (root = owning column),
+            //      U(k,:) along my process column (root = owning row)
+            R.ps_off = (int)psecs.size();
+            R.pc_off = (int)pcopy.size();
+            if (Pc > 1)
+                for (int c = 0; c < Pc; ++c) {
+                    i64 start = pan_total;
+                    for (int k : ks) {
+                        if (k % Pc != c || !lsend(k)) continue;
+                        int m, r0;
+                        lrows(k, m, r0);
+                        if (c == mycol) { // pack my rows below the diagonal block
+                            int ljb = k / Pc;
+                            add_copy(pcopy, /*src*/ 0, lval_off[ljb] + r0, lval_ld[ljb], 1, pan_total,
+                                     m, m, W(k));
+                        } else {
+                            lpos[k] = pan_total;
+                        }
+                        pan_total += (i64)m * W(k);
+                    }
+                    if (pan_total > start) psecs.push_back({G_ROW, c, 1, start, pan_total - start});
+                }
+            if (Pr > 1)
+                for (int r = 0; r < Pr; ++r) {
+                    i64 start = pan_total;
+                    for (int k : ks) {
+                        if (k % Pr != r || !uidx[k]) continue;
+                        i64 len = uidx[k][1];
+                        if (r == myrow) {
+                            add_copy(pcopy, /*src*/ 1, uval_off[k / Pr], len, 1, pan_total, len, len, 1);
+                        } else {
+                            upos[k] = pan_total;
+                        }
+                        pan_total += len;
+                    }
+                    if (pan_total > start) psecs.push_back({G_COL, r, 1, start, pan_total - start});
+                }
+            R.ps_n = (int)psecs.size() - R.ps_off;
+            R.pc_n = (int)pcopy.size() - R.pc_off;
+        }
+    }
+
+    // Copy items are recorded with symbolic bases (src space 0 = L values,
+    // 1 = U values; dst = d_dpk (dst_space 0) or d_pan (1)) and relocated in
+    // build_device.  Chunked to <= COPY_CHUNK elements.
+    vector<char> pcopy_src, dcopy_src;
+    void add_copy(vector<CopyItem<T>> &v, int src_space, i64 src_off, i64 lds, int dst_space,
+                  i64 dst_off, i64 ldd, i64 rows, i64 cols) {
+        vector<char> &tag = (&v == &pcopy) ? pcopy_src : dcopy_src;
+        if (cols == 1) {
+            for (i64 e = 0; e < rows; e += COPY_CHUNK) {
+                CopyItem<T> c{};
+                c.src = (const T *)(intptr_t)(src_off + e);
+                c.dst = (T *)(intptr_t)(dst_off + e);
+                c.lds = c.ldd = 0;
+                c.rows = (int)std::min<i64>(COPY_CHUNK, rows - e);
+                c.cols = 1;
+                v.push_back(c);
+                tag.push_back((char)(src_space | (dst_space << 1)));
+            }
+            return;
+        }
+        if (lds == rows && ldd == rows) { // contiguous: copy as 1D
+            add_copy(v, src_space, src_off, 0, dst_space, dst_off, 0, rows * cols, 1);
+            return;
+        }
+        const i64 cpc = std::max<i64>(1, COPY_CHUNK / std::max<i64>(rows, 1));
+        for (i64 c0 = 0; c0 < cols; c0 += cpc) {
+            CopyItem<T> c{};
+            c.src = (const T *)(intptr_t)(src_off + c0 * lds);
+            c.dst = (T *)(intptr_t)(dst_off + c0 * ldd);
+            c.lds = lds;
+            c.ldd = ldd;
+            c.rows = (int)rows;
+            c.cols = (int)std::min<i64>(cpc, cols - c0);
+            v.push_back(c);
+            tag.push_back((char)(src_space | (dst_space << 1)));
+        }
+    }
+
+    // ------------------------------------------------------- schedule
+    void build_schedule() {
+        // value buffers first: work items point straight into them
+        d_L.alloc(std::max<i64>(lval_total, 1));
+        d_U.alloc(std::max<i64>(uval_total, 1));
+        d_dpk.alloc(std::max<i64>(dpk_total, 1));
+        d_pan.alloc(std::max<i64>(pan_total, 1));
+        d_dinv.alloc(std::max<i64>(dscr_max, 1));
         vector<int> owner(lblk.size() + ublk.size(), -1), touched;
-        for (int L = 0; L <= maxlev; ++L) {
+        for (size_t L = 0; L < levels.size(); ++L) {
             LevelRange &R = levels[L];
             R.diag_off = (int)diag_items.size();
             R.tl_off = (int)tl_items.size();
@@ -339,9 +740,8 @@ struct Plan : PlanBase {
             R.df_off = (int)df_items.size();
             R.lf_off = (int)lf_items.size();
             R.uf_off = (int)uf_items.size();
-            dinv_level_off = 0;
+            R.dc_off = (int)dcopy.size();
             for (int k : bylev[L]) add_supernode(k, R);
-            dinv_max = std::max(dinv_max, dinv_level_off);
             R.big_n = (int)tiles_big.size() - R.big_off;
             R.df_n = (int)df_items.size() - R.df_off;
             R.lf_n = (int)lf_items.size() - R.lf_off;
@@ -351,6 +751,7 @@ struct Plan : PlanBase {
             R.tu_n = (int)tu_items.size() - R.tu_off;
             R.k_n = (int)kinfos.size() - R.k_off;
             R.tile_n = (int)tiles.size() - R.tile_off;
+            R.dc_n = (int)dcopy.size() - R.dc_off;
             // conflicting destinations inside the level -> atomics
             touched.clear();
             for (int s = R.k_off; s < R.k_off + R.k_n; ++s) {
@@ -376,124 +777,133 @@ struct Plan : PlanBase {
     };
     vector<KInfoHost> khost;
 
-    static constexpr bool cplx = sizeof(T) == 16;
-
     void add_supernode(int k, LevelRange &R) {
-        LocalLU *Llu = LU->Llu;
         const int w = W(k);
         const int ljb = k / Pc, lb = k / Pr;
-        const bool lcol_local = (k % Pc) == mycol && Llu->Lrowind_bc_ptr[ljb];
-        const bool diag_here = lcol_local && (k % Pr) == myrow;
-        // ---- diagonal block
-        i64 diag_off = -1;
-        int diag_ld = 0;
-        constexpr int PW = PWOf<T>::v, RB = cplx ? RBOf<T>::v : 16 * TR_WAVES;
-        const bool fast = w <= FAST_MAXW;
+        const bool lcol_here = (k % Pc) == mycol && lidx[k];
+        const bool urow_here = (k % Pr) == myrow && uidx[k];
+        const bool diag_here = lcol_here && (k % Pr) == myrow;
+        const bool fast = fast_w(w);
         const int nbk = (w + PW - 1) / PW;
-        const i64 dinv_off = dinv_level_off;           // U^{-1} blocks at +0, (L^{-1})^T at +nbk*PW*PW
-        if (fast) dinv_level_off += 2 * (i64)nbk * PW * PW;
+        constexpr int RB = cplx ? RBOf<T>::v : 16 * TR_WAVES;
+        // ---- diagonal block: factored in place by its owner; other ranks of
+        // its process row / column read the broadcast package
+        T *dT = nullptr, *dinv = nullptr;
+        int dld = 0;
         if (diag_here) {
-            diag_off = lval_off[ljb];
-            diag_ld = lval_ld[ljb];
             SLU_REQUIRE(lblk_ib[lcol_first[ljb]] == k, "diagonal block of %d is not first", k);
+            dT = d_L.p + lval_off[ljb];
+            dld = lval_ld[ljb];
+            dinv = xmode ? d_dpk.p + pkg[k] + (i64)w * w : d_dinv.p + dscr[k];
+        } else if (pkg[k] >= 0) {
+            dT = d_dpk.p + pkg[k];
+            dld = w;
+            dinv = dT + (i64)w * w;
+        }
+        if (diag_here) {
             if (fast) {
                 DiagItemF<T> d{};
-                d.a = (T *)(intptr_t)diag_off; // relocated in build_device
-                d.dinv = (T *)(intptr_t)dinv_off;
-                d.ld = diag_ld;
+                d.a = dT;
+                d.dinv = dinv;
+                d.ld = dld;
                 d.w = w;
                 d.k = k;
                 d.fcol = (int)xsup[k];
                 df_items.push_back(d);
             } else {
                 DiagItem<T> d{};
-                d.a = (T *)(intptr_t)diag_off; // relocated in build_device
-                d.ld = diag_ld;
+                d.a = dT;
+                d.ld = dld;
                 d.w = w;
                 d.k = k;
                 d.fcol = (int)xsup[k];
                 diag_items.push_back(d);
             }
+            if (xmode) add_copy(dcopy, 0, lval_off[ljb], dld, 0, pkg[k], w, w, w);
             stats.n_diag++;
             // SRC/pdgstrf2.c:252,262 (complex weights SRC/pzgstrf2.c:253,263)
             double wd = w, s1 = wd * (wd - 1) / 2, s2 = (wd - 1) * wd * (2 * wd - 1) / 6;
             stats.panel_flops += cplx ? 6 * s1 + 10 * wd + 8 * s2 : s1 + 2 * s2;
         }
-        // ---- L panel (rows of column k below the diagonal block)
-        int r0 = 0, m = 0;
-        vector<int> lbs; // L block ids of the panel (excluding the diagonal block)
-        if (lcol_local) {
-            int f = lcol_first[ljb], nb = lcol_nblk[ljb];
-            for (int b = 0; b < nb; ++b) {
-                if (lblk_ib[f + b] == k) { r0 += lblk_nrows[f + b]; continue; }
-                lbs.push_back(f + b);
-                m += lblk_nrows[f + b];
-            }
-            if (m > 0 && fast) {
+        // ---- L panel TRSM (rows of column k below the diagonal block)
+        int m = 0, r0 = 0;
+        lrows(k, m, r0);
+        if (lcol_here && m > 0) {
+            SLU_REQUIRE(dT, "no diagonal block for the L panel of %d", k);
+            if (fast) {
                 for (int c0 = 0; c0 < m; c0 += RB) {
                     TrsmItemF<T> t{};
-                    t.x = (T *)(intptr_t)(lval_off[ljb] + r0 + c0);
-                    t.t = (const T *)(intptr_t)diag_off;
-                    t.dinv = (const T *)(intptr_t)dinv_off;
+                    t.x = d_L.p + lval_off[ljb] + r0 + c0;
+                    t.t = dT;
+                    t.dinv = dinv;
                     t.ldx = lval_ld[ljb];
-                    t.ldt = diag_ld;
+                    t.ldt = dld;
                     t.w = w;
                     t.nrows = std::min(RB, m - c0);
                     lf_items.push_back(t);
                     stats.n_trsm_items++;
                 }
-                stats.panel_flops += (cplx ? 4.0 : 1.0) * (double)w * (w + 1) * m;
-            } else if (m > 0) {
+            } else {
                 for (int c0 = 0; c0 < m; c0 += TRSM_THREADS) {
                     TrsmLItem<T> t{};
-                    t.x = (T *)(intptr_t)(lval_off[ljb] + r0 + c0);
-                    t.u = (const T *)(intptr_t)diag_off;
+                    t.x = d_L.p + lval_off[ljb] + r0 + c0;
+                    t.u = dT;
                     t.ldx = lval_ld[ljb];
-                    t.ldu = diag_ld;
+                    t.ldu = dld;
                     t.w = w;
                     t.nrows = std::min(TRSM_THREADS, m - c0);
                     tl_items.push_back(t);
                     stats.n_trsm_items++;
                 }
-                stats.panel_flops += (cplx ? 4.0 : 1.0) * (double)w * (w + 1) * m;
             }
+            stats.panel_flops += (cplx ? 4.0 : 1.0) * (double)w * (w + 1) * m;
         }
-        // ---- U panel (nonempty columns of block row k)
-        vector<int> ubs; // U block ids
+        // ---- U panel: nonempty columns of block row k on my process column
+        vector<int> ujb; // U blocks with a nonempty column
         int ncols = 0, kmin = w;
         const int cols_off = (int)h_cg.size();
-        if ((k % Pr) == myrow && Llu->Ufstnz_br_ptr[lb]) {
-            int f = urow_first[lb], nb = urow_nblk[lb];
-            i64 klst = xsup[k + 1];
-            for (int b = 0; b < nb; ++b) {
-                int ub = f + b, jb = ublk_jb[ub];
-                int bidx = (int)ubs.size();
+        if (uidx[k]) {
+            const int_t *ix = uidx[k];
+            const i64 klst = xsup[k + 1];
+            const i64 base = urow_here ? uval_off[lb] : upos[k];
+            i64 p = SLU_BR_HEADER, run = 0;
+            for (i64 b = 0; b < ix[0]; ++b) {
+                const int jb = (int)ix[p];
+                const int bidx = (int)ujb.size();
                 bool any = false;
                 for (int c = 0; c < W(jb); ++c) {
-                    i64 e = ublk[ub].coloff + c;
-                    int fst = ucol_fst[e];
+                    const i64 fst = ix[p + SLU_UB_DESCRIPTOR + c];
                     if (fst >= klst) continue;
                     any = true;
                     h_cg.push_back((int)xsup[jb] + c);
                     h_cb.push_back(bidx);
-                    h_cvoff.push_back(ucol_voff[e]);
-                    int t0 = (int)(fst - xsup[k]);
+                    h_cvoff.push_back(base + run);
+                    const int t0 = (int)(fst - xsup[k]);
                     h_ct0.push_back(t0);
                     kmin = std::min(kmin, t0);
                     ++ncols;
-                    double seg = (double)(klst - fst);
-                    stats.panel_flops += seg * (seg + 1);
+                    run += klst - fst;
+                    if (urow_here) {
+                        double seg = (double)(klst - fst);
+                        stats.panel_flops += seg * (seg + 1);
+                    }
                 }
-                if (any) ubs.push_back(ub);
+                if (any) ujb.push_back(jb);
+                p += SLU_UB_DESCRIPTOR + W(jb);
             }
+            SLU_REQUIRE(run == ix[1], "U row %d: segment lengths %lld != %lld", k, (long long)run,
+                        (long long)ix[1]);
+        }
+        if (urow_here && ncols > 0) {
+            SLU_REQUIRE(dT, "no diagonal block for the U panel of %d", k);
             for (int c0 = 0; fast && c0 < ncols; c0 += RB) {
                 TrsmItemF<T> t{};
-                t.x = nullptr; // Uval
-                t.voff = (const i64 *)(intptr_t)(cols_off + c0);
+                t.x = d_U.p;
+                t.voff = (const i64 *)(intptr_t)(cols_off + c0); // relocated
                 t.t0 = (const int *)(intptr_t)(cols_off + c0);
-                t.t = (const T *)(intptr_t)diag_off;
-                t.dinv = (const T *)(intptr_t)(dinv_off + (i64)nbk * PW * PW);
-                t.ldt = diag_ld;
+                t.t = dT;
+                t.dinv = dinv + (i64)nbk * PW * PW;
+                t.ldt = dld;
                 t.w = w;
                 t.nrows = std::min(RB, ncols - c0);
                 uf_items.push_back(t);
@@ -501,8 +911,9 @@ struct Plan : PlanBase {
             }
             for (int c0 = 0; !fast && c0 < ncols; c0 += TRSM_THREADS) {
                 TrsmUItem<T> t{};
-                t.l = (const T *)(intptr_t)diag_off;
-                t.ldl = diag_ld;
+                t.l = dT;
+                t.ubase = d_U.p;
+                t.ldl = dld;
                 t.w = w;
                 t.ncols = std::min(TRSM_THREADS, ncols - c0);
                 t.voff = (const i64 *)(intptr_t)(cols_off + c0); // relocated
@@ -515,35 +926,42 @@ struct Plan : PlanBase {
             }
         }
         if (m == 0 || ncols == 0) return; // nothing to update from k here
-        // ---- Schur update of k
+        // ---- Schur update of k on this rank's destinations
         KInfo<T> ki{};
-        ki.a = (const T *)(intptr_t)(lval_off[ljb] + r0);
-        ki.lda = lval_ld[ljb];
+        if (lcol_here) {
+            ki.a = d_L.p + lval_off[ljb] + r0;
+            ki.lda = lval_ld[ljb];
+        } else {
+            SLU_REQUIRE(lpos[k] >= 0, "L panel %d not received", k);
+            ki.a = d_pan.p + lpos[k];
+            ki.lda = m;
+        }
+        SLU_REQUIRE(urow_here || upos[k] >= 0, "U panel %d not received", k);
+        ki.ubase = urow_here ? d_U.p : d_pan.p;
         ki.m = m;
         ki.n = ncols;
         ki.kmin = kmin;
         ki.kw = w - kmin;
-        ki.nub = (int)ubs.size();
+        ki.nub = (int)ujb.size();
         ki.cvoff = (const i64 *)(intptr_t)cols_off;
         ki.ct0 = (const int *)(intptr_t)cols_off;
         ki.cg = (const int *)(intptr_t)cols_off;
         ki.cb = (const int *)(intptr_t)cols_off;
-        ki.ubase = nullptr; // Uval
         const int rows_off = (int)h_rg.size();
-        for (size_t a = 0; a < lbs.size(); ++a)
-            for (int i = 0; i < lblk_nrows[lbs[a]]; ++i) {
-                h_rg.push_back(0); // filled from the index array below
-                h_ra.push_back((int)a);
-            }
-        // fill global rows from the index array of column k
+        vector<int> lib_; // L blocks (ib) of the panel below the diagonal
         {
-            int_t *index = Llu->Lrowind_bc_ptr[ljb];
+            const int_t *ix = lidx[k];
             i64 p = SLU_BC_HEADER;
-            int w_ = rows_off;
-            for (int b = 0; b < (int)index[0]; ++b) {
-                int gb = (int)index[p], nr = (int)index[p + 1];
-                if (gb != k)
-                    for (int i = 0; i < nr; ++i) h_rg[w_++] = (int)index[p + 2 + i];
+            for (i64 b = 0; b < ix[0]; ++b) {
+                const int gb = (int)ix[p], nr = (int)ix[p + 1];
+                if (gb != k) {
+                    const int a = (int)lib_.size();
+                    lib_.push_back(gb);
+                    for (int i = 0; i < nr; ++i) {
+                        h_rg.push_back((int)ix[p + 2 + i]);
+                        h_ra.push_back(a);
+                    }
+                }
                 p += SLU_LB_DESCRIPTOR + nr;
             }
         }
@@ -551,15 +969,12 @@ struct Plan : PlanBase {
         ki.ra = (const int *)(intptr_t)rows_off;
         const int pair_off = (int)h_pair.size();
         KInfoHost kh;
-        for (size_t a = 0; a < lbs.size(); ++a) {
-            int ib = lblk_ib[lbs[a]];
-            for (size_t b = 0; b < ubs.size(); ++b) {
-                int jb = ublk_jb[ubs[b]];
+        for (int ib : lib_)
+            for (int jb : ujb) {
                 int h = ib >= jb ? find_lblk(ib, jb) : ~find_ublk(ib, jb);
                 h_pair.push_back(h);
                 kh.dests.push_back(h);
             }
-        }
         ki.pair = (const int *)(intptr_t)pair_off;
         ki.atomic = 0;
         kinfos.push_back(ki);
@@ -573,21 +988,18 @@ struct Plan : PlanBase {
         // algorithmic work: exact unpadded flops and padded flops
         double fl = 0;
         for (int c = 0; c < ncols; ++c) fl += 2.0 * m * (w - h_ct0[cols_off + c]);
-        double mult = sizeof(T) == 16 ? 4.0 : 1.0; // complex: 8 real flops per multiply-add
+        const double mult = cplx ? 4.0 : 1.0; // complex: 8 real flops per multiply-add
         stats.schur_flops += fl * mult;
         stats.schur_flops_padded += 2.0 * m * ncols * (double)(w - kmin) * mult;
         stats.scatter_bytes += 3.0 * sizeof(T) * (double)m * ncols;
         stats.n_schur_tiles += (i64)tm * tn;
-        stats.n_diag += 0;
         R.schur_flops += fl * mult;
+        if (big) R.big_flops += fl * mult;
         if (w >= 64 && m >= 256 && ncols >= 256) R.big = true;
     }
 
     // ------------------------------------------------------- device
     void build_device() {
-        d_L.alloc(std::max<i64>(lval_total, 1));
-        d_U.alloc(std::max<i64>(uval_total, 1));
-        T *L = d_L.p, *U = d_U.p;
         d_rg.upload(h_rg);
         d_ra.upload(h_ra);
         d_cg.upload(h_cg);
@@ -595,21 +1007,12 @@ struct Plan : PlanBase {
         d_pair.upload(h_pair);
         d_ct0.upload(h_ct0);
         d_cvoff.upload(h_cvoff);
-        for (auto &d : diag_items) d.a = L + (intptr_t)d.a;
-        for (auto &t : tl_items) {
-            t.x = L + (intptr_t)t.x;
-            t.u = L + (intptr_t)t.u;
-        }
         for (auto &t : tu_items) {
-            t.l = L + (intptr_t)t.l;
-            t.ubase = U;
             intptr_t co = (intptr_t)t.voff;
             t.voff = d_cvoff.p + co;
             t.t0 = d_ct0.p + co;
         }
         for (auto &k : kinfos) {
-            k.a = L + (intptr_t)k.a;
-            k.ubase = U;
             intptr_t co = (intptr_t)k.cvoff, ro = (intptr_t)k.rg, po = (intptr_t)k.pair;
             k.cvoff = d_cvoff.p + co;
             k.ct0 = d_ct0.p + co;
@@ -619,24 +1022,20 @@ struct Plan : PlanBase {
             k.ra = d_ra.p + ro;
             k.pair = d_pair.p + po;
         }
-        d_dinv.alloc(std::max<i64>(dinv_max, 1));
-        for (auto &d : df_items) {
-            d.a = L + (intptr_t)d.a;
-            d.dinv = d_dinv.p + (intptr_t)d.dinv;
-        }
-        for (auto &t : lf_items) {
-            t.x = L + (intptr_t)t.x;
-            t.t = L + (intptr_t)t.t;
-            t.dinv = d_dinv.p + (intptr_t)t.dinv;
-        }
         for (auto &t : uf_items) {
-            t.x = U;
             intptr_t co = (intptr_t)t.voff;
             t.voff = d_cvoff.p + co;
             t.t0 = d_ct0.p + co;
-            t.t = L + (intptr_t)t.t;
-            t.dinv = d_dinv.p + (intptr_t)t.dinv;
         }
+        auto reloc = [&](vector<CopyItem<T>> &v, const vector<char> &tag) {
+            for (size_t i = 0; i < v.size(); ++i) {
+                const int ss = tag[i] & 1, ds = tag[i] >> 1;
+                v[i].src = (ss ? d_U.p : d_L.p) + (intptr_t)v[i].src;
+                v[i].dst = (ds ? d_pan.p : d_dpk.p) + (intptr_t)v[i].dst;
+            }
+        };
+        reloc(dcopy, dcopy_src);
+        reloc(pcopy, pcopy_src);
         d_df.upload(df_items);
         d_lf.upload(lf_items);
         d_uf.upload(uf_items);
@@ -646,6 +1045,8 @@ struct Plan : PlanBase {
         d_kinfo.upload(kinfos);
         d_tiles.upload(tiles);
         d_tiles_big.upload(tiles_big);
+        d_dcopy.upload(dcopy);
+        d_pcopy.upload(pcopy);
         d_lblk.upload(lblk);
         d_lmap.upload(lmap);
         d_ublk.upload(ublk);
@@ -653,6 +1054,7 @@ struct Plan : PlanBase {
         d_ucol_fst.upload(ucol_fst);
         d_counters.alloc(4);
         d_zpiv.alloc(nsupers);
+        d_info.alloc(Pr * Pc);
         stats.lu_bytes = (double)(lval_total + uval_total) * sizeof(T);
         stats.index_bytes = (double)(d_lblk.bytes() + d_lmap.bytes() + d_ublk.bytes() +
                                      d_ucol_voff.bytes() + d_ucol_fst.bytes() + d_diag.bytes() +
@@ -660,7 +1062,9 @@ struct Plan : PlanBase {
                                      d_df.bytes() + d_lf.bytes() + d_uf.bytes() + d_dinv.bytes() +
                                      d_tiles.bytes() + d_rg.bytes() + d_ra.bytes() +
                                      d_cg.bytes() + d_cb.bytes() + d_pair.bytes() +
-                                     d_ct0.bytes() + d_cvoff.bytes());
+                                     d_ct0.bytes() + d_cvoff.bytes() + d_dcopy.bytes() +
+                                     d_pcopy.bytes());
+        stats.comm_bytes = (double)(dpk_total + pan_total) * sizeof(T);
     }
 
     // ------------------------------------------------------- values
@@ -725,7 +1129,7 @@ struct Plan : PlanBase {
     }
 
     void launch_trsm_fast(const LevelRange &R) {
-        if constexpr (sizeof(T) == 16) {
+        if constexpr (cplx) {
             if (R.lf_n)
                 hipLaunchKernelGGL((k_trsm_blk<T, 0>), dim3(R.lf_n), dim3(256), 0, stream,
                                    d_lf.p + R.lf_off);
@@ -743,13 +1147,22 @@ struct Plan : PlanBase {
     }
 
     void launch_big(const LevelRange &R) {
-        if constexpr (sizeof(T) == 16) {
+        if constexpr (cplx) {
             SLU_REQUIRE(false, "no 128x128 Schur tiles for complex");
         } else {
             hipLaunchKernelGGL(k_schur_big<T>, dim3(R.big_n), dim3(256), 0, stream,
                                d_tiles_big.p + R.big_off, d_kinfo.p + R.k_off, d_L.p, d_U.p,
                                d_lblk.p, d_lmap.p, d_ublk.p, d_ucol_voff.p, d_ucol_fst.p);
         }
+    }
+
+    void issue(const vector<Sec> &secs, int off, int n_) {
+        for (int i = off; i < off + n_; ++i) {
+            const Sec &s = secs[i];
+            T *base = s.arena ? d_pan.p : d_dpk.p;
+            X.bcast(s.g, s.root, base + s.off, (size_t)s.cnt * sizeof(T));
+        }
+        X.flush();
     }
 
     // ------------------------------------------------------- factor
@@ -769,50 +1182,65 @@ struct Plan : PlanBase {
             ev.push_back(e);
             return (int)ev.size() - 1;
         };
-        struct Span { int a, b, kind; bool big; };
+        // kind: 0 diag, 1 trsm, 2 schur (128x128 tiles), 3 schur (64x64), 4 comm
+        struct Span { int a, b, kind; };
         vector<Span> spans;
+        auto span = [&](int kind, auto &&fn) {
+            int a = timing ? mark() : -1;
+            fn();
+            if (timing) spans.push_back({a, mark(), kind});
+        };
         int e_start = timing ? mark() : -1;
         stats.n_schur_launches = 0;
         for (size_t L = 0; L < levels.size(); ++L) {
             const LevelRange &R = levels[L];
-            if (R.diag_n) {
-                int a = timing ? mark() : -1;
-                hipLaunchKernelGGL(k_diag_lu<T>, dim3(R.diag_n), dim3(DIAG_THREADS), 0, stream,
-                                   d_diag.p + R.diag_off, thresh, opts.replace_tiny_pivot,
-                                   d_counters.p, d_zpiv.p);
-                if (timing) spans.push_back({a, mark(), 0, false});
+            if (R.diag_n)
+                span(0, [&] {
+                    hipLaunchKernelGGL(k_diag_lu<T>, dim3(R.diag_n), dim3(DIAG_THREADS), 0, stream,
+                                       d_diag.p + R.diag_off, thresh, opts.replace_tiny_pivot,
+                                       d_counters.p, d_zpiv.p);
+                });
+            if (R.df_n)
+                span(0, [&] {
+                    hipLaunchKernelGGL(k_diag_lu_blk<T>, dim3(R.df_n), dim3(256), 0, stream,
+                                       d_df.p + R.df_off, thresh, opts.replace_tiny_pivot,
+                                       d_counters.p, d_zpiv.p);
+                });
+            if (R.dc_n || R.ds_n)
+                span(4, [&] {
+                    if (R.dc_n)
+                        hipLaunchKernelGGL(k_copy<T>, dim3(R.dc_n), dim3(256), 0, stream,
+                                           d_dcopy.p + R.dc_off);
+                    issue(dsecs, R.ds_off, R.ds_n);
+                });
+            if (R.lf_n || R.uf_n) span(1, [&] { launch_trsm_fast(R); });
+            if (R.tl_n || R.tu_n)
+                span(1, [&] {
+                    if (R.tl_n)
+                        hipLaunchKernelGGL(k_trsm_l<T>, dim3(R.tl_n), dim3(TRSM_THREADS), 0, stream,
+                                           d_tl.p + R.tl_off);
+                    if (R.tu_n)
+                        hipLaunchKernelGGL(k_trsm_u<T>, dim3(R.tu_n), dim3(TRSM_THREADS), 0, stream,
+                                           d_tu.p + R.tu_off);
+                });
+            if (R.pc_n || R.ps_n)
+                span(4, [&] {
+                    if (R.pc_n)
+                        hipLaunchKernelGGL(k_copy<T>, dim3(R.pc_n), dim3(256), 0, stream,
+                                           d_pcopy.p + R.pc_off);
+                    issue(psecs, R.ps_off, R.ps_n);
+                });
+            if (R.big_n) {
+                span(2, [&] { launch_big(R); });
+                stats.n_schur_launches++;
             }
-            if (R.df_n) {
-                int a = timing ? mark() : -1;
-                hipLaunchKernelGGL(k_diag_lu_blk<T>, dim3(R.df_n), dim3(256), 0, stream,
-                                   d_df.p + R.df_off, thresh, opts.replace_tiny_pivot,
-                                   d_counters.p, d_zpiv.p);
-                if (timing) spans.push_back({a, mark(), 0, false});
-            }
-            if (R.lf_n || R.uf_n) {
-                int a = timing ? mark() : -1;
-                launch_trsm_fast(R);
-                if (timing) spans.push_back({a, mark(), 1, false});
-            }
-            if (R.tl_n || R.tu_n) {
-                int a = timing ? mark() : -1;
-                if (R.tl_n)
-                    hipLaunchKernelGGL(k_trsm_l<T>, dim3(R.tl_n), dim3(TRSM_THREADS), 0, stream,
-                                       d_tl.p + R.tl_off);
-                if (R.tu_n)
-                    hipLaunchKernelGGL(k_trsm_u<T>, dim3(R.tu_n), dim3(TRSM_THREADS), 0, stream,
-                                       d_tu.p + R.tu_off);
-                if (timing) spans.push_back({a, mark(), 1, false});
-            }
-            if (R.tile_n || R.big_n) {
-                int a = timing ? mark() : -1;
-                if (R.big_n) launch_big(R);
-                if (R.tile_n)
+            if (R.tile_n) {
+                span(3, [&] {
                     hipLaunchKernelGGL(k_schur<T>, dim3(R.tile_n), dim3(SC_THREADS), 0, stream,
                                        d_tiles.p + R.tile_off, d_kinfo.p + R.k_off, d_L.p, d_U.p,
                                        d_lblk.p, d_lmap.p, d_ublk.p, d_ucol_voff.p, d_ucol_fst.p);
+                });
                 stats.n_schur_launches++;
-                if (timing) spans.push_back({a, mark(), 2, R.big});
             }
         }
         HIPCHK(hipGetLastError());
@@ -823,10 +1251,18 @@ struct Plan : PlanBase {
         vector<int> zp(nsupers);
         HIPCHK(hipMemcpy(zp.data(), d_zpiv.p, nsupers * sizeof(int), hipMemcpyDeviceToHost));
         // per-rank info: the zero pivot of the last supernode (in elimination
-        // order) that had one (SRC/pdgstrf2.c:246-247 overwrites *info)
+        // order) that had one (SRC/pdgstrf2.c:246-247 overwrites *info); the
+        // grid value is the MIN over ranks (SRC/pdgstrf.c:1927-1931)
         int my_info = 0;
         for (int k = 0; k < nsupers; ++k)
             if (zp[k]) my_info = zp[k];
+        if (xmode) {
+            vector<i64> mine(1, my_info ? my_info : n + 1);
+            auto all = X.allgatherv(G_WORLD, mine);
+            i64 g = n + 1;
+            for (auto &v : all) g = std::min(g, v[0]);
+            my_info = g == n + 1 ? 0 : (int)g;
+        }
         *info = my_info;
         *tiny = hc[0];
         if (timing) {
@@ -834,18 +1270,23 @@ struct Plan : PlanBase {
             HIPCHK(hipEventElapsedTime(&ms, ev[e_start], ev[e_end]));
             stats.t_total_ms = ms;
             stats.t_diag_ms = stats.t_trsm_ms = stats.t_schur_ms = stats.t_schur_big_ms = 0;
+            stats.t_comm_ms = 0;
             stats.schur_big_flops = 0;
+            stats.n_schur_big_launches = 0;
             for (auto &s : spans) {
                 HIPCHK(hipEventElapsedTime(&ms, ev[s.a], ev[s.b]));
                 if (s.kind == 0) stats.t_diag_ms += ms;
                 else if (s.kind == 1) stats.t_trsm_ms += ms;
+                else if (s.kind == 4) stats.t_comm_ms += ms;
                 else {
                     stats.t_schur_ms += ms;
-                    if (s.big) stats.t_schur_big_ms += ms;
+                    if (s.kind == 2) {
+                        stats.t_schur_big_ms += ms;
+                        stats.n_schur_big_launches++;
+                    }
                 }
             }
-            for (auto &R : levels)
-                if (R.big) stats.schur_big_flops += R.schur_flops;
+            for (auto &R : levels) stats.schur_big_flops += R.big_flops;
             for (auto e : ev) (void)hipEventDestroy(e);
         }
     }
@@ -899,6 +1340,27 @@ slu_comm *slu_comm_create(const void *uid, int nprow, int npcol, int iam, int de
             NCCLCHK(ncclCommSplit(c->world, c->myrow, c->mycol, &c->row, nullptr));
             NCCLCHK(ncclCommSplit(c->world, c->mycol, c->myrow, &c->col, nullptr));
         }
+        return c;
+    } catch (const std::exception &e) {
+        set_last_error(e.what());
+        return nullptr;
+    }
+}
+
+slu_comm *slu_comm_create_host(slu_host_bcast_fn fn, void *ctx, int nprow, int npcol, int iam,
+                               int device) {
+    try {
+        SLU_REQUIRE(fn != nullptr, "host transport needs a broadcast callback");
+        auto *c = new slu_comm;
+        c->nprow = nprow;
+        c->npcol = npcol;
+        c->iam = iam;
+        c->myrow = iam / npcol;
+        c->mycol = iam % npcol;
+        c->device = device;
+        c->host_fn = fn;
+        c->host_ctx = ctx;
+        HIPCHK(hipSetDevice(device));
         return c;
     } catch (const std::exception &e) {
         set_last_error(e.what());

@@ -192,6 +192,34 @@ struct UBlk {          // one local U block (ib, jb)
     int pad;
 };
 
+// ------------------------------------------------------------- pack
+// Column-major 2D copies dst[r + c*ldd] = src[r + c*lds] that stage a rank's
+// own diagonal blocks and panels into the contiguous per-level sections the
+// 2D-grid broadcasts send (the reference sends lusup / uval straight from
+// Llu, SRC/pdgstrf.c:1039-1044,1330-1335).  Items are pre-chunked by the plan
+// to <= COPY_CHUNK elements.  HBM-bound.
+constexpr int COPY_CHUNK = 1 << 16;
+template <typename T> struct CopyItem {
+    const T *src;
+    T *dst;
+    int64_t lds, ldd;
+    int rows, cols;
+};
+
+template <typename T>
+__global__ void __launch_bounds__(256) k_copy(const CopyItem<T> *items) {
+    const CopyItem<T> it = items[blockIdx.x];
+    const int tot = it.rows * it.cols;
+    if (it.cols == 1) {
+        for (int e = threadIdx.x; e < tot; e += 256) it.dst[e] = it.src[e];
+    } else {
+        for (int e = threadIdx.x; e < tot; e += 256) {
+            const int r = e % it.rows, c = e / it.rows;
+            it.dst[r + c * it.ldd] = it.src[r + c * it.lds];
+        }
+    }
+}
+
 // ------------------------------------------------------------- diag LU
 // One workgroup per diagonal block; blocked right-looking LU (panels of NB
 // columns) in place, thread-per-row.  Tiny-pivot replacement and the zero

@@ -8,7 +8,9 @@ into the host LUstruct (the in-place contract of SRC/pdgstrf.c).
 """
 import ctypes as C
 
-from .lib import EngineOpts, PlanStats, lib
+import numpy as np
+
+from .lib import HOST_BCAST_FN, EngineOpts, PlanStats, lib
 
 SMACH_EPS = 5.9604644775390625e-08  # smach_dist("Epsilon"), SRC/smach_dist.c:64
 
@@ -26,6 +28,32 @@ class Comm:
         self.ptr = lib().slu_comm_create(buf, nprow, npcol, iam, device)
         if not self.ptr:
             raise RuntimeError(lib().slu_last_error().decode())
+
+    @classmethod
+    def host(cls, nprow, npcol, iam, device, bcast):
+        """Test transport: ``bcast(group, root, buf)`` broadcasts the uint8
+        numpy array ``buf`` in place within group 0 (grid), 1 (my process
+        row) or 2 (my process column) from the group-local rank ``root``.
+        For several ranks on one GPU (RCCL refuses duplicate devices); the
+        device kernels are the same as with RCCL."""
+        self = cls.__new__(cls)
+        self.nprow, self.npcol, self.iam = nprow, npcol, iam
+
+        def _cb(_ctx, group, root, buf, nbytes):
+            try:
+                arr = np.ctypeslib.as_array((C.c_uint8 * nbytes).from_address(buf))
+                bcast(group, root, arr)
+                return 0
+            except Exception as e:  # noqa: BLE001 -- reported through the C status
+                import sys
+                print(f"host broadcast failed: {e!r}", file=sys.stderr)
+                return 1
+
+        self._cb = HOST_BCAST_FN(_cb)  # keep alive as long as the comm
+        self.ptr = lib().slu_comm_create_host(self._cb, None, nprow, npcol, iam, device)
+        if not self.ptr:
+            raise RuntimeError(lib().slu_last_error().decode())
+        return self
 
     @staticmethod
     def unique_id():

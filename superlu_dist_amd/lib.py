@@ -20,6 +20,10 @@ c_i64p = C.POINTER(C.c_int64)
 c_intp = C.POINTER(C.c_int)
 
 
+# int (*)(void *ctx, int group, int root, void *buf, int64_t bytes)
+HOST_BCAST_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int64)
+
+
 class SluCsc(C.Structure):
     _fields_ = [("n", C.c_int64), ("nnz", C.c_int64), ("colptr", c_i64p),
                 ("rowind", c_i64p), ("val", C.c_void_p), ("dtype", C.c_int)]
@@ -50,7 +54,8 @@ class PlanStats(C.Structure):
                 ("t_total_ms", C.c_double), ("t_diag_ms", C.c_double),
                 ("t_trsm_ms", C.c_double), ("t_schur_ms", C.c_double),
                 ("t_comm_ms", C.c_double), ("t_schur_big_ms", C.c_double),
-                ("schur_big_flops", C.c_double), ("n_schur_launches", C.c_int64)]
+                ("schur_big_flops", C.c_double), ("n_schur_launches", C.c_int64),
+                ("n_schur_big_launches", C.c_int64), ("comm_bytes", C.c_double)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -87,6 +92,7 @@ def lib():
         "slu_lu_get_view": (C.c_int, [P, C.c_int, C.POINTER(SluLuView)]),
         "slu_comm_unique_id": (C.c_int, [P]),
         "slu_comm_create": (P, [P, C.c_int, C.c_int, C.c_int, C.c_int]),
+        "slu_comm_create_host": (P, [HOST_BCAST_FN, P, C.c_int, C.c_int, C.c_int, C.c_int]),
         "slu_comm_destroy": (None, [P]),
         "slu_plan_create": (P, [C.c_int, P, C.c_int, C.c_int, C.c_int, C.c_int, P,
                                 C.POINTER(EngineOpts), C.c_char_p, C.c_int]),

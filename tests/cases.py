@@ -119,3 +119,12 @@ def factor_error(lus, ref):
             d = np.abs(mine.astype(np.complex128) - r.astype(np.complex128)).max()
             worst = max(worst, d / max(np.abs(r).max(), 1e-300))
     return worst
+
+
+def stencil_case(kind, dims, dtype, grid, relax, maxsup):
+    """cases.build()-style recipe for a seeded stencil (picklable via partial)."""
+    kw = {}
+    if dtype == SLU_Z:
+        kw = dict(diag=6 - 0.25, diag_im=-0.0025)
+    A, perm = _stencil(kind, *dims, dtype, **kw)
+    return A, perm, dtype, grid, relax, maxsup, False

@@ -1,0 +1,125 @@
+"""Multi-rank (2D process grid) runs of the engine for the tests.
+
+``run_grid`` spawns Pr*Pc processes.  Each is one rank of the grid: it builds
+its own LUstruct with the front-end, factors it with the MI355X engine and
+returns its factors.  The ranks exchange panels either through RCCL (one GPU
+per rank) or, where the box has fewer GPUs than ranks, through the engine's
+host-staged test transport over torch.distributed gloo (RCCL refuses two ranks
+on one GPU).  The CPU-only variant (``device=None``) exercises the same gloo
+group plumbing without the engine.
+"""
+import os
+import socket
+import traceback
+
+import numpy as np
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+class GlooGrid:
+    """torch.distributed gloo groups of a Pr x Pc grid (world / rows / columns)."""
+
+    def __init__(self, rank, pr, pc):
+        import torch.distributed as dist
+        self.dist = dist
+        self.rank, self.pr, self.pc = rank, pr, pc
+        self.myrow, self.mycol = rank // pc, rank % pc
+        rows = [dist.new_group([r * pc + c for c in range(pc)]) for r in range(pr)]
+        cols = [dist.new_group([r * pc + c for r in range(pr)]) for c in range(pc)]
+        self.row, self.col = rows[self.myrow], cols[self.mycol]
+
+    def global_root(self, group, root):
+        if group == 0:
+            return root
+        if group == 1:
+            return self.myrow * self.pc + root
+        return root * self.pc + self.mycol
+
+    def bcast(self, group, root, arr):
+        import torch
+        t = torch.from_numpy(arr)
+        g = None if group == 0 else (self.row if group == 1 else self.col)
+        self.dist.broadcast(t, src=self.global_root(group, root), group=g)
+
+
+def _worker(rank, world, port, recipe, out_dir, device):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    try:
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import cases
+        from superlu_dist_amd.engine import Comm, Plan
+        from superlu_dist_amd.frontend import Symbolic
+        A, perm, dtype, (pr, pc), relax, maxsup, tiny = recipe()
+        gg = GlooGrid(rank, pr, pc)
+        S = Symbolic(A, perm, relax, maxsup)
+        lu = S.distribute(pr, pc, rank // pc, rank % pc)
+        res = {}
+        if device is not None:
+            comm = Comm.host(pr, pc, rank, device, gg.bcast)
+            p = Plan(lu, comm=comm, replace_tiny=tiny)
+            p.upload()
+            info, ntiny = p.factor(cases.anorm(A))
+            p.download()
+            st = p.stats()
+            res = dict(info=info, tiny=ntiny, flops=st["schur_flops"] + st["panel_flops"],
+                       comm_bytes=st["comm_bytes"])
+            del p
+        else:  # group plumbing only
+            buf = np.full(16, rank, dtype=np.uint8)
+            gg.bcast(1, 0, buf)
+            res["row_root"] = int(buf[0])
+            buf = np.full(16, rank, dtype=np.uint8)
+            gg.bcast(2, pr - 1, buf)
+            res["col_root"] = int(buf[0])
+        np.savez(os.path.join(out_dir, f"rank{rank}.npz"), L=lu.Lval, U=lu.Uval,
+                 **{k: np.asarray(v) for k, v in res.items()})
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception:
+        with open(os.path.join(out_dir, f"rank{rank}.err"), "w") as fh:
+            fh.write(traceback.format_exc())
+        raise
+
+
+def run_grid(recipe, pr, pc, out_dir, device=0, timeout=240):
+    """Run ``recipe`` (picklable callable returning cases.build()-style
+    tuples) on a pr x pc grid; returns the per-rank result dicts.
+
+    The parent never imports torch: torch bundles its own ROCm runtime, and a
+    process that loads libslu_mi355x.so (system ROCm) before torch ends up
+    with two HIP runtimes.  Each worker imports torch.distributed first."""
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    world = pr * pc
+    port = free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, recipe, str(out_dir), device))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout)
+    bad = []
+    for r, p in enumerate(procs):
+        if p.is_alive():
+            p.kill()
+            p.join()
+            bad.append(f"rank {r}: timed out")
+        elif p.exitcode != 0:
+            err = os.path.join(out_dir, f"rank{r}.err")
+            msg = open(err).read() if os.path.exists(err) else ""
+            bad.append(f"rank {r}: exit {p.exitcode}\n{msg}")
+    if bad:
+        raise RuntimeError("grid run failed:\n" + "\n".join(bad))
+    out = []
+    for r in range(world):
+        z = np.load(os.path.join(out_dir, f"rank{r}.npz"))
+        out.append({k: z[k] for k in z.files})
+    return out
