@@ -78,10 +78,15 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--n", type=int, default=100, help="grid points per dimension")
+    ap.add_argument("--nx", type=int, default=100, help="grid points per dimension")
     ap.add_argument("--cpu-sample", type=int, default=80)
     ap.add_argument("--cpu-ranks", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--level-log", action="store_true",
+                    help="per-level phase breakdown of the last step on stderr")
+    ap.add_argument("--host-transport", action="store_true",
+                    help="REHEARSAL ONLY: several ranks on one GPU through the host-staged "
+                         "test transport (RCCL refuses duplicate devices); not a measurement")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -95,26 +100,40 @@ def main():
     from superlu_dist_amd.engine import Comm, Plan
     dist = None
     uid = None
+    grid = None
     if world > 1:
+        # torch first: it bundles a ROCm runtime with the same sonames as the
+        # system one libslu_mi355x.so links; the first loaded is shared.
         import torch
         import torch.distributed as dist
         dist.init_process_group("gloo")
-        buf = torch.zeros(128, dtype=torch.uint8)
-        if rank == 0:
-            buf[:] = torch.tensor(list(Comm.unique_id()), dtype=torch.uint8)
-        dist.broadcast(buf, 0)
-        uid = bytes(buf.tolist())
+        if args.host_transport:
+            sys.path.insert(0, os.path.join(ROOT, "tests"))
+            from gridrun import GlooGrid
+            grid = GlooGrid(rank, pr, pc)
+            local = 0
+        else:
+            buf = torch.zeros(128, dtype=torch.uint8)
+            if rank == 0:
+                buf[:] = torch.tensor(list(Comm.unique_id()), dtype=torch.uint8)
+            dist.broadcast(buf, 0)
+            uid = bytes(buf.tolist())
 
     def barrier():
         if dist is not None:
             dist.barrier()
 
     t0 = time.time()
-    A, S, lu = build_lu(args.n, pr, pc, myrow, mycol)
+    A, S, lu = build_lu(args.nx, pr, pc, myrow, mycol)
     t_front = time.time() - t0
-    comm = Comm(pr, pc, rank, device=local, uid=uid) if world > 1 else None
+    if world == 1:
+        comm = None
+    elif grid is not None:
+        comm = Comm.host(pr, pc, rank, 0, grid.bcast)
+    else:
+        comm = Comm(pr, pc, rank, device=local, uid=uid)
     t0 = time.time()
-    plan = Plan(lu, comm=comm, timing=True)
+    plan = Plan(lu, comm=comm, timing=2 if args.level_log else 1)
     t_plan = time.time() - t0
     t0 = time.time()
     plan.upload()
@@ -138,17 +157,15 @@ def main():
 
     for _ in range(args.warmup):
         one_step()
-    times, schur_ms, schur_big_ms, tot_ms = [], 0.0, 0.0, 0.0
-    diag_ms = trsm_ms = 0.0
+    times = []
+    acc = {k: 0.0 for k in ("t_schur_ms", "t_schur_big_ms", "t_diag_ms", "t_trsm_ms",
+                            "t_comm_ms", "t_total_ms")}
     for _ in range(args.steps):
         dt, info = one_step()
         times.append(dt)
         st = plan.stats()
-        schur_ms += st["t_schur_ms"]
-        schur_big_ms += st["t_schur_big_ms"]
-        diag_ms += st["t_diag_ms"]
-        trsm_ms += st["t_trsm_ms"]
-        tot_ms += st["t_total_ms"]
+        for k in acc:
+            acc[k] += st[k]
     st = plan.stats()
     t_step = float(np.mean(times))
     flops_all = my_flops
@@ -163,20 +180,22 @@ def main():
 
     if rank == 0:
         K = args.steps
-        sch_s = schur_ms / 1e3 / K
-        achieved = st["schur_flops"] / sch_s / 1e12 if sch_s > 0 else 0.0
+        big_s = acc["t_schur_big_ms"] / 1e3 / K
+        launches = max(int(st["n_schur_big_launches"]), 1)
+        achieved = st["schur_big_flops"] / big_s / 1e12 if big_s > 0 else 0.0
         roof = {"bound": "mfma", "achieved": round(achieved, 3),
                 "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(achieved / FP64_MFMA_PEAK_TFLOPS, 4), "traffic": None,
-                "kernel": "k_schur<double> (fp64 MFMA GEMM + fused scatter)",
-                "launches_per_step": st["n_schur_launches"],
-                "schur_flops_per_step": st["schur_flops"],
-                "kernel_ms_per_step": round(schur_ms / K, 3)}
-        big_s = schur_big_ms / 1e3 / K
-        if big_s > 0:
-            roof["achieved_big_levels"] = round(st["schur_big_flops"] / big_s / 1e12, 3)
+                "frac": round(achieved / FP64_MFMA_PEAK_TFLOPS, 4),
+                "traffic": pmc_traffic(args.nx, pr, pc),
+                "kernel": "k_schur_big<double> (128x128 fp64 MFMA GEMM + fused scatter)",
+                "launches_per_step": launches,
+                "flops_per_launch": st["schur_big_flops"] / launches,
+                "avg_launch_ms": round(acc["t_schur_big_ms"] / K / launches, 4),
+                "timer": "HIP events on the engine stream around each k_schur_big launch",
+                "all_schur_tflops": round(st["schur_flops"] / (acc["t_schur_ms"] / 1e3 / K) / 1e12,
+                                          3) if acc["t_schur_ms"] else None}
         cpu = None
-        if not args.no_cpu:
+        if not args.no_cpu and world == 1:
             cpu = cpu_baseline(args.cpu_sample, args.cpu_ranks, timeout=600)
         out = {
             "metric": "pdgstrf fp64 GFLOP/s + factor time, 3D Laplacian n~1M",
@@ -191,23 +210,38 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (generated 7-point stencil, diag 6 / off -1)",
-            "config": {"workload": f"3D 7-point Laplacian {args.n}^3 (n={args.n**3}), nested "
+            "config": {"workload": f"3D 7-point Laplacian {args.nx}^3 (n={args.nx**3}), nested "
                                    f"dissection, relax 60, maxsup 256",
                        "grid": f"{pr}x{pc}", "nsupers": int(S.nsupers),
                        "flops_per_factorization": flops_all,
-                       "nnz_L": S.nnzL, "parallelism": f"2D block-cyclic {pr}x{pc}"},
+                       "nnz_L": S.nnzL, "parallelism": f"2D block-cyclic {pr}x{pc}",
+                       "transport": ("host-staged gloo (REHEARSAL, not a measurement)"
+                                     if grid is not None else
+                                     ("rccl" if world > 1 else "none"))},
             "roofline": roof,
             "cpu_baseline": cpu,
-            "phases_ms_per_step": {"diag_lu": round(diag_ms / K, 3), "trsm": round(trsm_ms / K, 3),
-                                   "schur": round(schur_ms / K, 3),
-                                   "events_total": round(tot_ms / K, 3)},
+            "phases_ms_per_step_rank0": {k[2:-3]: round(v / K, 3) for k, v in acc.items()},
             "setup_s": {"frontend": round(t_front, 2), "plan": round(t_plan, 2),
-                        "h2d_upload": round(t_upload, 2)},
+                        "h2d_upload_pcie": round(t_upload, 2)},
             "info": info,
         }
-        print(json.dumps(out))
+        print(json.dumps(out), flush=True)
     if dist is not None:
+        dist.barrier()
         dist.destroy_process_group()
+
+
+def pmc_traffic(nx, pr, pc):
+    """HBM bytes per k_schur_big launch from the committed rocprofv3 PMC passes
+    (profiles/traffic.json, written by tools/pmc_traffic.py: FETCH_SIZE x2
+    gfx950 correction + WRITE_SIZE) for this exact workload, else None."""
+    f = os.path.join(ROOT, "profiles", "traffic.json")
+    try:
+        d = json.load(open(f))
+    except (OSError, ValueError):
+        return None
+    e = d.get(f"lap3d_{nx}_{pr}x{pc}", {}).get("k_schur_big<double>")
+    return e
 
 
 if __name__ == "__main__":

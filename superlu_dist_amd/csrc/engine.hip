@@ -27,6 +27,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <array>
 #include <chrono>
 #include <cstring>
 #include <memory>
@@ -1183,17 +1184,19 @@ struct Plan : PlanBase {
             return (int)ev.size() - 1;
         };
         // kind: 0 diag, 1 trsm, 2 schur (128x128 tiles), 3 schur (64x64), 4 comm
-        struct Span { int a, b, kind; };
+        struct Span { int a, b, kind, level; };
         vector<Span> spans;
+        int cur_level = 0;
         auto span = [&](int kind, auto &&fn) {
             int a = timing ? mark() : -1;
             fn();
-            if (timing) spans.push_back({a, mark(), kind});
+            if (timing) spans.push_back({a, mark(), kind, cur_level});
         };
         int e_start = timing ? mark() : -1;
         stats.n_schur_launches = 0;
         for (size_t L = 0; L < levels.size(); ++L) {
             const LevelRange &R = levels[L];
+            cur_level = (int)L;
             if (R.diag_n)
                 span(0, [&] {
                     hipLaunchKernelGGL(k_diag_lu<T>, dim3(R.diag_n), dim3(DIAG_THREADS), 0, stream,
@@ -1287,6 +1290,22 @@ struct Plan : PlanBase {
                 }
             }
             for (auto &R : levels) stats.schur_big_flops += R.big_flops;
+            if (opts.timing >= 2) { // per-level breakdown (stderr)
+                vector<std::array<double, 5>> t(levels.size(), {0, 0, 0, 0, 0});
+                for (auto &s : spans) {
+                    HIPCHK(hipEventElapsedTime(&ms, ev[s.a], ev[s.b]));
+                    t[s.level][s.kind] += ms;
+                }
+                fprintf(stderr, "[slu rank %d] lvl nsup diag trsm big small  GFLOP  diag_ms trsm_ms big_ms small_ms comm_ms  TF/s\n", iam);
+                for (size_t L = 0; L < levels.size(); ++L) {
+                    const LevelRange &R = levels[L];
+                    double sch = t[L][2] + t[L][3];
+                    fprintf(stderr, "[slu rank %d] %3zu %5zu %4d %5d %5d %5d %7.2f %8.3f %7.3f %7.3f %7.3f %7.3f %6.2f\n",
+                            iam, L, bylev[L].size(), R.diag_n + R.df_n, R.lf_n + R.uf_n + R.tl_n + R.tu_n,
+                            R.big_n, R.tile_n, R.schur_flops / 1e9, t[L][0], t[L][1], t[L][2], t[L][3],
+                            t[L][4], sch > 0 ? R.schur_flops / sch / 1e9 : 0.0);
+                }
+            }
             for (auto e : ev) (void)hipEventDestroy(e);
         }
     }

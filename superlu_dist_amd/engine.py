@@ -73,7 +73,7 @@ class Plan:
         self.lu = lu
         o = EngineOpts()
         o.replace_tiny_pivot = int(bool(replace_tiny))
-        o.timing = int(bool(timing))
+        o.timing = int(timing)
         err = C.create_string_buffer(1024)
         iam = lu.myrow * lu.npcol + lu.mycol
         self.comm = comm

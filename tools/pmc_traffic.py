@@ -5,7 +5,9 @@ Units and corrections (MI355X_MICROARCH.md, HBM section): both counters are in
 KiB; on gfx950 FETCH_SIZE tallies 128-B read requests at 64 B, i.e. it reports
 1/2 of the bytes of a wide coalesced read, so it is doubled here.  WRITE_SIZE
 is taken as is.
-usage: python tools/pmc_traffic.py FETCH_DIR WRITE_DIR [out.txt]
+usage: python tools/pmc_traffic.py FETCH_DIR WRITE_DIR [out.txt [KEY]]
+With KEY (e.g. lap3d_100_1x1) the bytes per launch are also merged into
+profiles/traffic.json, which bench.py reports as roofline.traffic.
 """
 import collections
 import csv
@@ -47,4 +49,13 @@ def main(fd, wd, out=None):
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:4])
+    res = main(*sys.argv[1:4])
+    if len(sys.argv) > 4:
+        import json
+        key = sys.argv[4]
+        jf = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "profiles",
+                          "traffic.json")
+        d = json.load(open(jf)) if os.path.exists(jf) else {}
+        d[key] = {k.replace("slu::", ""): round(v) for k, v in res.items() if "slu::" in k}
+        d[key]["source"] = os.path.basename(sys.argv[3]) if len(sys.argv) > 3 else ""
+        json.dump(d, open(jf, "w"), indent=1, sort_keys=True)
