@@ -84,6 +84,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--level-log", action="store_true",
                     help="per-level phase breakdown of the last step on stderr")
+    ap.add_argument("--roofline-only", action="store_true",
+                    help="only the serialized (single-stream) profiling step: for rocprofv3 runs")
     ap.add_argument("--host-transport", action="store_true",
                     help="REHEARSAL ONLY: several ranks on one GPU through the host-staged "
                          "test transport (RCCL refuses duplicate devices); not a measurement")
@@ -157,6 +159,8 @@ def main():
 
     for _ in range(args.warmup):
         one_step()
+    if args.roofline_only:
+        args.steps = 0
     times = []
     acc = {k: 0.0 for k in ("t_schur_ms", "t_schur_big_ms", "t_diag_ms", "t_trsm_ms",
                             "t_comm_ms", "t_total_ms")}
@@ -166,7 +170,20 @@ def main():
         st = plan.stats()
         for k in acc:
             acc[k] += st[k]
+    # kernel-level roofline: one more factorization with every launch on one
+    # stream, so k_schur_big launch durations are not stretched by the
+    # look-ahead kernels running beside them (not part of the timed steps)
+    plan.set_timing(1, serial=True)
+    one_step()
+    sst = plan.stats()
+    plan.set_timing(2 if args.level_log else 1, serial=False)
     st = plan.stats()
+    if args.roofline_only:
+        if rank == 0:
+            print(json.dumps({"roofline_only": True, "t_schur_big_ms": sst["t_schur_big_ms"],
+                              "n_schur_big_launches": sst["n_schur_big_launches"],
+                              "t_total_ms": sst["t_total_ms"]}), flush=True)
+        return
     t_step = float(np.mean(times))
     flops_all = my_flops
     if dist is not None:
@@ -180,18 +197,20 @@ def main():
 
     if rank == 0:
         K = args.steps
-        big_s = acc["t_schur_big_ms"] / 1e3 / K
-        launches = max(int(st["n_schur_big_launches"]), 1)
-        achieved = st["schur_big_flops"] / big_s / 1e12 if big_s > 0 else 0.0
+        big_s = sst["t_schur_big_ms"] / 1e3
+        launches = max(int(sst["n_schur_big_launches"]), 1)
+        achieved = sst["schur_big_flops"] / big_s / 1e12 if big_s > 0 else 0.0
         roof = {"bound": "mfma", "achieved": round(achieved, 3),
                 "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved / FP64_MFMA_PEAK_TFLOPS, 4),
                 "traffic": pmc_traffic(args.nx, pr, pc),
                 "kernel": "k_schur_big<double> (128x128 fp64 MFMA GEMM + fused scatter)",
                 "launches_per_step": launches,
-                "flops_per_launch": st["schur_big_flops"] / launches,
-                "avg_launch_ms": round(acc["t_schur_big_ms"] / K / launches, 4),
-                "timer": "HIP events on the engine stream around each k_schur_big launch",
+                "flops_per_launch": sst["schur_big_flops"] / launches,
+                "avg_launch_ms": round(sst["t_schur_big_ms"] / launches, 4),
+                "timer": "HIP events around each k_schur_big launch, in one extra "
+                         "factorization with all launches on one stream (untimed for value)",
+                "serial_factor_ms": round(sst["t_total_ms"], 3),
                 "all_schur_tflops": round(st["schur_flops"] / (acc["t_schur_ms"] / 1e3 / K) / 1e12,
                                           3) if acc["t_schur_ms"] else None}
         cpu = None

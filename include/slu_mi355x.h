@@ -122,8 +122,9 @@ void slu_comm_destroy(slu_comm *c);
 /* Engine options (everything the kernels need beyond the LUstruct). */
 typedef struct {
     int replace_tiny_pivot; /* options->ReplaceTinyPivot */
-    int timing;             /* 1: record per-phase HIP events */
-    int reserved[6];
+    int timing;             /* 1: per-phase HIP events; 2: + per-level log on stderr */
+    int serial;             /* 1: one stream, no look-ahead overlap (kernel profiling) */
+    int reserved[5];
 } slu_engine_opts;
 
 /* A plan = device-resident factors + every index table the kernels use.
@@ -141,6 +142,8 @@ int slu_plan_factor(slu_plan *p, double anorm, int *info, int *tiny_pivots);
  * the working factor storage from it (benchmark repetitions; device-to-device). */
 int slu_plan_snapshot(slu_plan *p);
 int slu_plan_restore(slu_plan *p);
+/* Change the measurement options of an existing plan (timing, serial). */
+int slu_plan_set_timing(slu_plan *p, int timing, int serial);
 /* Wait for all work of the plan's stream. */
 int slu_plan_sync(slu_plan *p);
 /* Copy factors back into the host LUstruct arrays. */

@@ -177,7 +177,8 @@ struct LevelRange {
     int tu_off = 0, tu_n = 0;
     int k_off = 0, k_n = 0;
     int tile_off = 0, tile_n = 0;
-    int big_off = 0, big_n = 0; // 128x128 Schur tiles
+    int big_off = 0, big_n = 0; // 128x128 Schur tiles (first bigc_n: critical)
+    int bigc_n = 0, tilec_n = 0; // critical tiles (destinations in the next level's panels)
     int df_off = 0, df_n = 0;   // fast diag items
     int lf_off = 0, lf_n = 0;   // fast L-panel TRSM items
     int uf_off = 0, uf_n = 0;   // fast U-panel TRSM items
@@ -203,6 +204,7 @@ struct PlanBase {
     virtual void snapshot() = 0;
     virtual void restore() = 0;
     virtual void sync() = 0;
+    virtual void set_timing(int timing, int serial) = 0;
     slu_plan_stats stats{};
 };
 
@@ -228,7 +230,10 @@ struct Plan : PlanBase {
     LUS *LU = nullptr;
     vector<i64> xsup;
     int nlc = 0, nlr = 0;
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;  // Schur updates that are off the critical path
+    hipStream_t pstream = nullptr; // panels, exchanges, critical Schur tiles
+    vector<hipEvent_t> ev_pan, ev_rest; // per level
+    hipEvent_t ev_start = nullptr, ev_pend = nullptr;
     bool xmode = false; // 2D grid with exchanges
     Xport X;
 
@@ -265,6 +270,7 @@ struct Plan : PlanBase {
     vector<TrsmUItem<T>> tu_items;
     vector<KInfo<T>> kinfos;
     vector<TileItem> tiles, tiles_big;
+    vector<TileItem> lv_big[2], lv_small[2]; // per level being built: [0] critical, [1] rest
     vector<DiagItemF<T>> df_items;
     vector<TrsmItemF<T>> lf_items, uf_items;
     vector<CopyItem<T>> dcopy, pcopy;
@@ -321,8 +327,9 @@ struct Plan : PlanBase {
                         comm->nprow, comm->npcol, comm->iam, Pr, Pc, iam);
         if (comm) HIPCHK(hipSetDevice(comm->device));
         HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+        HIPCHK(hipStreamCreateWithFlags(&pstream, hipStreamNonBlocking));
         X.c = comm;
-        X.s = stream;
+        X.s = pstream;
         int_t *hx = LU->Glu_persist->xsup;
         nsupers = (int)(LU->Glu_persist->supno[n - 1] + 1);
         xsup.assign(hx, hx + nsupers + 1);
@@ -339,7 +346,12 @@ struct Plan : PlanBase {
     }
 
     ~Plan() override {
+        for (auto e : ev_pan) (void)hipEventDestroy(e);
+        for (auto e : ev_rest) (void)hipEventDestroy(e);
+        if (ev_start) (void)hipEventDestroy(ev_start);
+        if (ev_pend) (void)hipEventDestroy(ev_pend);
         if (stream) (void)hipStreamDestroy(stream);
+        if (pstream) (void)hipStreamDestroy(pstream);
     }
 
     // ------------------------------------------------------- local layout
@@ -742,7 +754,16 @@ struct Plan : PlanBase {
             R.lf_off = (int)lf_items.size();
             R.uf_off = (int)uf_items.size();
             R.dc_off = (int)dcopy.size();
+            for (int c = 0; c < 2; ++c) lv_big[c].clear(), lv_small[c].clear();
             for (int k : bylev[L]) add_supernode(k, R);
+            // critical tiles first: they are launched ahead of the rest so the
+            // next level's panels can be factored while the rest runs
+            R.bigc_n = (int)lv_big[0].size();
+            R.tilec_n = (int)lv_small[0].size();
+            for (int c = 0; c < 2; ++c) {
+                tiles_big.insert(tiles_big.end(), lv_big[c].begin(), lv_big[c].end());
+                tiles.insert(tiles.end(), lv_small[c].begin(), lv_small[c].end());
+            }
             R.big_n = (int)tiles_big.size() - R.big_off;
             R.df_n = (int)df_items.size() - R.df_off;
             R.lf_n = (int)lf_items.size() - R.lf_off;
@@ -984,8 +1005,21 @@ struct Plan : PlanBase {
         const bool big = !cplx && m >= SB_BM && ncols >= SB_BN;
         const int BM = big ? SB_BM : SC_BM, BN = big ? SB_BN : SC_BN;
         const int tm = (m + BM - 1) / BM, tn = (ncols + BN - 1) / BN;
+        // A destination (ib,jb) belongs to the panel of supernode min(ib,jb);
+        // it is critical when that panel is factored at the next level.  All
+        // destinations in a row of L block ib (resp. a column of U block jb)
+        // with level(ib) == level(k)+1 are critical, and no others.
+        const int nl = level_of[k] + 1;
+        vector<char> crow(tm, 0), ccol(tn, 0);
+        for (int r = 0; r < m; ++r)
+            if (level_of[lib_[h_ra[rows_off + r]]] == nl) crow[r / BM] = 1;
+        for (int c = 0; c < ncols; ++c)
+            if (level_of[ujb[h_cb[cols_off + c]]] == nl) ccol[c / BN] = 1;
         for (int i = 0; i < tm; ++i)
-            for (int j = 0; j < tn; ++j) (big ? tiles_big : tiles).push_back(TileItem{slot, i, j});
+            for (int j = 0; j < tn; ++j) {
+                const int cls = (crow[i] || ccol[j]) ? 0 : 1;
+                (big ? lv_big[cls] : lv_small[cls]).push_back(TileItem{slot, i, j});
+            }
         // algorithmic work: exact unpadded flops and padded flops
         double fl = 0;
         for (int c = 0; c < ncols; ++c) fl += 2.0 * m * (w - h_ct0[cols_off + c]);
@@ -1055,6 +1089,14 @@ struct Plan : PlanBase {
         d_ucol_fst.upload(ucol_fst);
         d_counters.alloc(4);
         d_zpiv.alloc(nsupers);
+        ev_pan.resize(levels.size());
+        ev_rest.resize(levels.size());
+        for (size_t L = 0; L < levels.size(); ++L) {
+            HIPCHK(hipEventCreateWithFlags(&ev_pan[L], hipEventDisableTiming));
+            HIPCHK(hipEventCreateWithFlags(&ev_rest[L], hipEventDisableTiming));
+        }
+        HIPCHK(hipEventCreateWithFlags(&ev_start, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&ev_pend, hipEventDisableTiming));
         d_info.alloc(Pr * Pc);
         stats.lu_bytes = (double)(lval_total + uval_total) * sizeof(T);
         stats.index_bytes = (double)(d_lblk.bytes() + d_lmap.bytes() + d_ublk.bytes() +
@@ -1104,11 +1146,18 @@ struct Plan : PlanBase {
         HIPCHK(hipMemcpyAsync(d_L.p, d_L0.p, d_L.bytes(), hipMemcpyDeviceToDevice, stream));
         HIPCHK(hipMemcpyAsync(d_U.p, d_U0.p, d_U.bytes(), hipMemcpyDeviceToDevice, stream));
     }
-    void sync() override { HIPCHK(hipStreamSynchronize(stream)); }
+    void set_timing(int timing, int serial) override {
+        opts.timing = timing;
+        opts.serial = serial;
+    }
+    void sync() override {
+        HIPCHK(hipStreamSynchronize(pstream));
+        HIPCHK(hipStreamSynchronize(stream));
+    }
 
     void download() override {
         LocalLU *Llu = LU->Llu;
-        HIPCHK(hipStreamSynchronize(stream));
+        sync();
         if (l_contig && lval_total) {
             HIPCHK(hipMemcpy(Llu->Lnzval_bc_dat, d_L.p, lval_total * sizeof(T), hipMemcpyDeviceToHost));
         } else {
@@ -1129,32 +1178,37 @@ struct Plan : PlanBase {
         }
     }
 
-    void launch_trsm_fast(const LevelRange &R) {
+    void launch_trsm_fast(const LevelRange &R, hipStream_t st) {
         if constexpr (cplx) {
             if (R.lf_n)
-                hipLaunchKernelGGL((k_trsm_blk<T, 0>), dim3(R.lf_n), dim3(256), 0, stream,
+                hipLaunchKernelGGL((k_trsm_blk<T, 0>), dim3(R.lf_n), dim3(256), 0, st,
                                    d_lf.p + R.lf_off);
             if (R.uf_n)
-                hipLaunchKernelGGL((k_trsm_blk<T, 1>), dim3(R.uf_n), dim3(256), 0, stream,
+                hipLaunchKernelGGL((k_trsm_blk<T, 1>), dim3(R.uf_n), dim3(256), 0, st,
                                    d_uf.p + R.uf_off);
         } else {
             if (R.lf_n)
-                hipLaunchKernelGGL((k_trsm_reg<T, 0>), dim3(R.lf_n), dim3(64 * TR_WAVES), 0, stream,
+                hipLaunchKernelGGL((k_trsm_reg<T, 0>), dim3(R.lf_n), dim3(64 * TR_WAVES), 0, st,
                                    d_lf.p + R.lf_off);
             if (R.uf_n)
-                hipLaunchKernelGGL((k_trsm_reg<T, 1>), dim3(R.uf_n), dim3(64 * TR_WAVES), 0, stream,
+                hipLaunchKernelGGL((k_trsm_reg<T, 1>), dim3(R.uf_n), dim3(64 * TR_WAVES), 0, st,
                                    d_uf.p + R.uf_off);
         }
     }
 
-    void launch_big(const LevelRange &R) {
+    void launch_big(const LevelRange &R, int off, int cnt, hipStream_t st) {
         if constexpr (cplx) {
             SLU_REQUIRE(false, "no 128x128 Schur tiles for complex");
         } else {
-            hipLaunchKernelGGL(k_schur_big<T>, dim3(R.big_n), dim3(256), 0, stream,
-                               d_tiles_big.p + R.big_off, d_kinfo.p + R.k_off, d_L.p, d_U.p,
+            hipLaunchKernelGGL(k_schur_big<T>, dim3(cnt), dim3(256), 0, st,
+                               d_tiles_big.p + off, d_kinfo.p + R.k_off, d_L.p, d_U.p,
                                d_lblk.p, d_lmap.p, d_ublk.p, d_ucol_voff.p, d_ucol_fst.p);
         }
+    }
+    void launch_small(const LevelRange &R, int off, int cnt, hipStream_t st) {
+        hipLaunchKernelGGL(k_schur<T>, dim3(cnt), dim3(SC_THREADS), 0, st, d_tiles.p + off,
+                           d_kinfo.p + R.k_off, d_L.p, d_U.p, d_lblk.p, d_lmap.p, d_ublk.p,
+                           d_ucol_voff.p, d_ucol_fst.p);
     }
 
     void issue(const vector<Sec> &secs, int off, int n_) {
@@ -1187,68 +1241,104 @@ struct Plan : PlanBase {
         struct Span { int a, b, kind, level; };
         vector<Span> spans;
         int cur_level = 0;
-        auto span = [&](int kind, auto &&fn) {
-            int a = timing ? mark() : -1;
+        auto mark_on = [&](hipStream_t st) -> int {
+            hipEvent_t e;
+            HIPCHK(hipEventCreate(&e));
+            HIPCHK(hipEventRecord(e, st));
+            ev.push_back(e);
+            return (int)ev.size() - 1;
+        };
+        auto span = [&](int kind, hipStream_t st, auto &&fn) {
+            int a = timing ? mark_on(st) : -1;
             fn();
-            if (timing) spans.push_back({a, mark(), kind, cur_level});
+            if (timing) spans.push_back({a, mark_on(st), kind, cur_level});
         };
         int e_start = timing ? mark() : -1;
+        HIPCHK(hipEventRecord(ev_start, stream));
+        HIPCHK(hipStreamWaitEvent(pstream, ev_start, 0));
+        X.s = opts.serial ? stream : pstream;
         stats.n_schur_launches = 0;
+        stats.n_schur_big_launches = 0;
+        // Look-ahead of one level on two streams:
+        //   pstream: panel(L) -> [wait rest(L-1)] -> critical tiles(L) -> panel(L+1) ...
+        //   stream : [wait panel(L)] -> rest tiles(L) -> [rest(L) done] ...
+        // Critical tiles update exactly the destinations in the panels of
+        // level L+1, so panel(L+1) (diag LU, TRSM, exchanges) runs beside the
+        // bulk of level L's Schur update (SRC/pdgstrf.c:1115-1356 look-ahead).
         for (size_t L = 0; L < levels.size(); ++L) {
             const LevelRange &R = levels[L];
             cur_level = (int)L;
+            hipStream_t P = opts.serial ? stream : pstream;
             if (R.diag_n)
-                span(0, [&] {
-                    hipLaunchKernelGGL(k_diag_lu<T>, dim3(R.diag_n), dim3(DIAG_THREADS), 0, stream,
+                span(0, P, [&] {
+                    hipLaunchKernelGGL(k_diag_lu<T>, dim3(R.diag_n), dim3(DIAG_THREADS), 0, P,
                                        d_diag.p + R.diag_off, thresh, opts.replace_tiny_pivot,
                                        d_counters.p, d_zpiv.p);
                 });
             if (R.df_n)
-                span(0, [&] {
-                    hipLaunchKernelGGL(k_diag_lu_blk<T>, dim3(R.df_n), dim3(256), 0, stream,
+                span(0, P, [&] {
+                    hipLaunchKernelGGL(k_diag_lu_blk<T>, dim3(R.df_n), dim3(256), 0, P,
                                        d_df.p + R.df_off, thresh, opts.replace_tiny_pivot,
                                        d_counters.p, d_zpiv.p);
                 });
             if (R.dc_n || R.ds_n)
-                span(4, [&] {
+                span(4, P, [&] {
                     if (R.dc_n)
-                        hipLaunchKernelGGL(k_copy<T>, dim3(R.dc_n), dim3(256), 0, stream,
+                        hipLaunchKernelGGL(k_copy<T>, dim3(R.dc_n), dim3(256), 0, P,
                                            d_dcopy.p + R.dc_off);
                     issue(dsecs, R.ds_off, R.ds_n);
                 });
-            if (R.lf_n || R.uf_n) span(1, [&] { launch_trsm_fast(R); });
+            if (R.lf_n || R.uf_n) span(1, P, [&] { launch_trsm_fast(R, P); });
             if (R.tl_n || R.tu_n)
-                span(1, [&] {
+                span(1, P, [&] {
                     if (R.tl_n)
-                        hipLaunchKernelGGL(k_trsm_l<T>, dim3(R.tl_n), dim3(TRSM_THREADS), 0, stream,
+                        hipLaunchKernelGGL(k_trsm_l<T>, dim3(R.tl_n), dim3(TRSM_THREADS), 0, P,
                                            d_tl.p + R.tl_off);
                     if (R.tu_n)
-                        hipLaunchKernelGGL(k_trsm_u<T>, dim3(R.tu_n), dim3(TRSM_THREADS), 0, stream,
+                        hipLaunchKernelGGL(k_trsm_u<T>, dim3(R.tu_n), dim3(TRSM_THREADS), 0, P,
                                            d_tu.p + R.tu_off);
                 });
             if (R.pc_n || R.ps_n)
-                span(4, [&] {
+                span(4, P, [&] {
                     if (R.pc_n)
-                        hipLaunchKernelGGL(k_copy<T>, dim3(R.pc_n), dim3(256), 0, stream,
+                        hipLaunchKernelGGL(k_copy<T>, dim3(R.pc_n), dim3(256), 0, P,
                                            d_pcopy.p + R.pc_off);
                     issue(psecs, R.ps_off, R.ps_n);
                 });
-            if (R.big_n) {
-                span(2, [&] { launch_big(R); });
+            HIPCHK(hipEventRecord(ev_pan[L], P));
+            // critical tiles of L on the panel stream, after the rest of L-1
+            if (L > 0) HIPCHK(hipStreamWaitEvent(P, ev_rest[L - 1], 0));
+            if (R.bigc_n) {
+                span(2, P, [&] { launch_big(R, R.big_off, R.bigc_n, P); });
+                stats.n_schur_launches++;
+                stats.n_schur_big_launches++;
+            }
+            if (R.tilec_n) {
+                span(3, P, [&] { launch_small(R, R.tile_off, R.tilec_n, P); });
                 stats.n_schur_launches++;
             }
-            if (R.tile_n) {
-                span(3, [&] {
-                    hipLaunchKernelGGL(k_schur<T>, dim3(R.tile_n), dim3(SC_THREADS), 0, stream,
-                                       d_tiles.p + R.tile_off, d_kinfo.p + R.k_off, d_L.p, d_U.p,
-                                       d_lblk.p, d_lmap.p, d_ublk.p, d_ucol_voff.p, d_ucol_fst.p);
+            // the rest of L on the Schur stream, once the panels of L exist
+            HIPCHK(hipStreamWaitEvent(stream, ev_pan[L], 0));
+            if (R.big_n > R.bigc_n) {
+                span(2, stream, [&] {
+                    launch_big(R, R.big_off + R.bigc_n, R.big_n - R.bigc_n, stream);
+                });
+                stats.n_schur_launches++;
+                stats.n_schur_big_launches++;
+            }
+            if (R.tile_n > R.tilec_n) {
+                span(3, stream, [&] {
+                    launch_small(R, R.tile_off + R.tilec_n, R.tile_n - R.tilec_n, stream);
                 });
                 stats.n_schur_launches++;
             }
+            HIPCHK(hipEventRecord(ev_rest[L], stream));
         }
+        HIPCHK(hipEventRecord(ev_pend, pstream));
+        HIPCHK(hipStreamWaitEvent(stream, ev_pend, 0));
         HIPCHK(hipGetLastError());
         int e_end = timing ? mark() : -1;
-        HIPCHK(hipStreamSynchronize(stream));
+        sync();
         int hc[4];
         HIPCHK(hipMemcpy(hc, d_counters.p, sizeof hc, hipMemcpyDeviceToHost));
         vector<int> zp(nsupers);
@@ -1275,7 +1365,6 @@ struct Plan : PlanBase {
             stats.t_diag_ms = stats.t_trsm_ms = stats.t_schur_ms = stats.t_schur_big_ms = 0;
             stats.t_comm_ms = 0;
             stats.schur_big_flops = 0;
-            stats.n_schur_big_launches = 0;
             for (auto &s : spans) {
                 HIPCHK(hipEventElapsedTime(&ms, ev[s.a], ev[s.b]));
                 if (s.kind == 0) stats.t_diag_ms += ms;
@@ -1283,10 +1372,7 @@ struct Plan : PlanBase {
                 else if (s.kind == 4) stats.t_comm_ms += ms;
                 else {
                     stats.t_schur_ms += ms;
-                    if (s.kind == 2) {
-                        stats.t_schur_big_ms += ms;
-                        stats.n_schur_big_launches++;
-                    }
+                    if (s.kind == 2) stats.t_schur_big_ms += ms;
                 }
             }
             for (auto &R : levels) stats.schur_big_flops += R.big_flops;
@@ -1467,6 +1553,16 @@ int slu_plan_snapshot(slu_plan *p) {
 int slu_plan_restore(slu_plan *p) {
     try {
         p->impl->restore();
+        return 0;
+    } catch (const std::exception &e) {
+        set_last_error(e.what());
+        return -1;
+    }
+}
+
+int slu_plan_set_timing(slu_plan *p, int timing, int serial) {
+    try {
+        p->impl->set_timing(timing, serial);
         return 0;
     } catch (const std::exception &e) {
         set_last_error(e.what());

@@ -103,6 +103,12 @@ class Plan:
         """Restore the working factor storage from the snapshot (device to device)."""
         self._chk(lib().slu_plan_restore(self.ptr))
 
+    def set_timing(self, timing, serial=False):
+        """timing: 0 off, 1 phase events, 2 + per-level log; serial: run every
+        launch on one stream (no look-ahead overlap) so kernel durations are
+        not inflated by concurrent kernels."""
+        self._chk(lib().slu_plan_set_timing(self.ptr, int(timing), int(bool(serial))))
+
     def sync(self):
         self._chk(lib().slu_plan_sync(self.ptr))
 

@@ -40,8 +40,8 @@ class SluLuView(C.Structure):
 
 
 class EngineOpts(C.Structure):
-    _fields_ = [("replace_tiny_pivot", C.c_int), ("timing", C.c_int),
-                ("reserved", C.c_int * 6)]
+    _fields_ = [("replace_tiny_pivot", C.c_int), ("timing", C.c_int), ("serial", C.c_int),
+                ("reserved", C.c_int * 5)]
 
 
 class PlanStats(C.Structure):
@@ -102,6 +102,7 @@ def lib():
         "slu_plan_snapshot": (C.c_int, [P]),
         "slu_plan_restore": (C.c_int, [P]),
         "slu_plan_sync": (C.c_int, [P]),
+        "slu_plan_set_timing": (C.c_int, [P, C.c_int, C.c_int]),
         "slu_plan_destroy": (None, [P]),
         "slu_plan_get_stats": (C.c_int, [P, C.POINTER(PlanStats)]),
         "slu_last_error": (C.c_char_p, []),

@@ -15,11 +15,11 @@ echo "== bench" && \
 timeout -k 10 600 python -u bench.py "$@" > $OUT/bench.json 2> $OUT/bench.err && cat $OUT/bench.json && \
 echo "== rocprofv3 kernel stats" && \
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run \
-    -- python3 bench.py --no-cpu --steps 2 --warmup 1 "$@" > $OUT/prof_bench.json 2> $OUT/prof.err && \
+    -- python3 bench.py --no-cpu --roofline-only --warmup 0 "$@" > $OUT/prof_bench.json 2> $OUT/prof.err && \
 echo "== pmc FETCH_SIZE" && \
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $OUT/pmc_fetch -o run \
-    -- python3 bench.py --no-cpu --steps 1 --warmup 0 "$@" > $OUT/pmc_fetch.json 2> $OUT/pmc_fetch.err && \
+    -- python3 bench.py --no-cpu --roofline-only --warmup 0 "$@" > $OUT/pmc_fetch.json 2> $OUT/pmc_fetch.err && \
 echo "== pmc WRITE_SIZE" && \
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $OUT/pmc_write -o run \
-    -- python3 bench.py --no-cpu --steps 1 --warmup 0 "$@" > $OUT/pmc_write.json 2> $OUT/pmc_write.err && \
+    -- python3 bench.py --no-cpu --roofline-only --warmup 0 "$@" > $OUT/pmc_write.json 2> $OUT/pmc_write.err && \
 echo "== done"
