@@ -1,0 +1,107 @@
+// Microbenchmarks for the Schur-update kernel (not part of the product).
+//   1. peak: independent v_mfma_f64_16x16x4f64 chains from registers
+//   2. k_schur_big on one synthetic dense supernode update: C(m x n) -= A(m x kw) B(kw x n)
+//      with an identity destination map (one L block), i.e. GEMM + fused scatter
+// usage: schur_micro [m n kw reps]
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "kernels.h"
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
+
+using namespace slu;
+
+__global__ void __launch_bounds__(256) k_peak(double *out, int iters) {
+    typedef __attribute__((ext_vector_type(4))) double v4;
+    v4 acc[8];
+    for (int i = 0; i < 8; ++i) acc[i] = v4{0, 0, 0, 0};
+    double a = threadIdx.x * 1e-3, b = blockIdx.x * 1e-3;
+    for (int it = 0; it < iters; ++it) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[i] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[i], 0, 0, 0);
+    }
+    double s = 0;
+    for (int i = 0; i < 8; ++i) s += acc[i][0] + acc[i][1] + acc[i][2] + acc[i][3];
+    if (s == 123.456) out[0] = s;
+}
+
+int main(int argc, char **argv) {
+    int m = argc > 1 ? atoi(argv[1]) : 8192, n = argc > 2 ? atoi(argv[2]) : 8192;
+    int kw = argc > 3 ? atoi(argv[3]) : 256, reps = argc > 4 ? atoi(argv[4]) : 5;
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    float ms;
+    double *dout;
+    CK(hipMalloc(&dout, 8));
+    for (int wg : {256, 512, 1024, 2048}) {
+        int iters = 2000;
+        hipLaunchKernelGGL(k_peak, dim3(wg), dim3(256), 0, 0, dout, iters);
+        CK(hipEventRecord(e0));
+        hipLaunchKernelGGL(k_peak, dim3(wg), dim3(256), 0, 0, dout, iters);
+        CK(hipEventRecord(e1));
+        CK(hipEventSynchronize(e1));
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        double fl = (double)wg * 4 * iters * 8 * 2048.0;
+        printf("peak f64 mfma 16x16x4: %4d WGs x 4 waves: %.2f TFLOP/s\n", wg, fl / ms / 1e9);
+    }
+    // ---- synthetic supernode update
+    std::vector<double> hA((size_t)m * kw), hB((size_t)kw * n);
+    for (size_t i = 0; i < hA.size(); ++i) hA[i] = (double)((i * 2654435761u) % 1000) / 1000.0;
+    for (size_t i = 0; i < hB.size(); ++i) hB[i] = (double)((i * 40503u) % 1000) / 1000.0;
+    double *dA, *dB, *dC;
+    CK(hipMalloc(&dA, hA.size() * 8));
+    CK(hipMalloc(&dB, hB.size() * 8));
+    CK(hipMalloc(&dC, (size_t)m * n * 8));
+    CK(hipMemcpy(dA, hA.data(), hA.size() * 8, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dB, hB.data(), hB.size() * 8, hipMemcpyHostToDevice));
+    CK(hipMemset(dC, 0, (size_t)m * n * 8));
+    std::vector<int64_t> cvoff(n);
+    std::vector<int> ct0(n, 0), cg(n), cb(n, 0), rg(m), ra(m, 0), pair(1, 0), lmap(m);
+    for (int c = 0; c < n; ++c) { cvoff[c] = (int64_t)c * kw; cg[c] = c; }
+    for (int r = 0; r < m; ++r) { rg[r] = r; lmap[r] = r; }
+    auto up = [](const void *h, size_t bytes) { void *d; CK(hipMalloc(&d, bytes)); CK(hipMemcpy(d, h, bytes, hipMemcpyHostToDevice)); return d; };
+    KInfo<double> ki{};
+    ki.a = dA; ki.lda = m; ki.m = m; ki.n = n; ki.kmin = 0; ki.kw = kw; ki.nub = 1; ki.atomic = 0;
+    ki.ubase = dB;
+    ki.cvoff = (const int64_t *)up(cvoff.data(), n * 8);
+    ki.ct0 = (const int *)up(ct0.data(), n * 4);
+    ki.cg = (const int *)up(cg.data(), n * 4);
+    ki.cb = (const int *)up(cb.data(), n * 4);
+    ki.rg = (const int *)up(rg.data(), m * 4);
+    ki.ra = (const int *)up(ra.data(), m * 4);
+    ki.pair = (const int *)up(pair.data(), 4);
+    LBlk L{};
+    L.colvoff = 0; L.mapoff = 0; L.ld = m; L.fcol = 0; L.frow = 0;
+    auto *dk = (KInfo<double> *)up(&ki, sizeof ki);
+    auto *dl = (LBlk *)up(&L, sizeof L);
+    auto *dmap = (int *)up(lmap.data(), m * 4);
+    int tm = (m + SB_BM - 1) / SB_BM, tn = (n + SB_BN - 1) / SB_BN;
+    std::vector<TileItem> tiles;
+    for (int i = 0; i < tm; ++i)
+        for (int j = 0; j < tn; ++j) tiles.push_back(TileItem{0, i, j});
+    auto *dt = (TileItem *)up(tiles.data(), tiles.size() * sizeof(TileItem));
+    double fl = 2.0 * m * n * kw;
+    for (int r = 0; r < reps; ++r) {
+        CK(hipEventRecord(e0));
+        hipLaunchKernelGGL(k_schur_big<double>, dim3(tiles.size()), dim3(256), 0, 0, dt, dk, dC,
+                           (double *)nullptr, dl, dmap, (const UBlk *)nullptr, (const int64_t *)nullptr,
+                           (const int *)nullptr);
+        CK(hipEventRecord(e1));
+        CK(hipEventSynchronize(e1));
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        printf("k_schur_big m=%d n=%d kw=%d tiles=%zu: %.3f ms  %.2f TFLOP/s\n", m, n, kw,
+               tiles.size(), ms, fl / ms / 1e9);
+    }
+    // check one entry of C after reps updates
+    std::vector<double> hC(4);
+    CK(hipMemcpy(hC.data(), dC + (size_t)5 + (size_t)7 * m, 8, hipMemcpyDeviceToHost));
+    double ref = 0;
+    for (int k = 0; k < kw; ++k) ref += hA[5 + (size_t)k * m] * hB[(size_t)7 * kw + k];
+    printf("check C(5,7) = %.12g expected %.12g\n", hC[0], -ref * reps);
+    return 0;
+}
