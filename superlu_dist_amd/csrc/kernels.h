@@ -90,6 +90,14 @@ __device__ inline double one_of(double) { return 1.0; }
 __device__ inline float one_of(float) { return 1.0f; }
 __device__ inline zc one_of(zc) { return {1.0, 0.0}; }
 
+// Loads through the global address space.  Pointers that come out of the
+// work-item structs are generic; dereferencing them emits flat_load, which
+// also counts against lgkmcnt, so every s_waitcnt lgkmcnt(0) for an LDS read
+// would wait for the in-flight global prefetch too.
+template <typename T> __device__ __forceinline__ T gld(const T *p) {
+    return *(const __attribute__((address_space(1))) T *)p;
+}
+
 // ------------------------------------------------------------ MFMA
 template <typename T> struct Mma;
 
@@ -847,22 +855,30 @@ k_trsm_blk(const TrsmItemF<T> *items) {
 
 
 // ------------------------------------------------------------- Schur (big)
-// 128x128 output tile per 256-thread workgroup (2x2 waves of 64x64 = 4x4 MFMA
-// fragments each), K staged 16 deep through double-buffered LDS with the next
-// stage's global loads in flight during the current stage's MFMAs.  Used for
-// supernodes whose update is at least 128x128 (fp64 / fp32).
-constexpr int SB_BM = 128, SB_BN = 128, SB_BK = 16;
+// 128x128 output tile per 512-thread workgroup: 4x2 waves, each 32x64 = 2x4
+// v_mfma_f64_16x16x4 fragments (64 accumulator VGPRs, so 4 waves per SIMD fit
+// beside the 2 workgroups per CU the 66 KB of LDS allow -- measured: more
+// resident waves, not more ILP per wave, is what feeds the fp64 MFMA pipe,
+// tools/micro/gemm_exp.hip).  K is staged 16 deep through double-buffered LDS
+// with the next stage's global loads in flight during the current stage's
+// MFMAs.  Epilogue: the C tile goes through LDS in two 64-column passes and
+// is scatter-subtracted column-contiguously into the destination blocks
+// (dscatter_l / dscatter_u, SRC/dscatter.c:175-187,240-272).
+constexpr int SB_BM = 128, SB_BN = 128, SB_BK = 16, SB_THREADS = 512;
 
 template <typename T>
-__global__ void __launch_bounds__(256, 2)
+__global__ void __launch_bounds__(SB_THREADS, 2)
 k_schur_big(const TileItem *tiles, const KInfo<T> *kinfo, T *Lval, T *Uval,
             const LBlk *lblk, const int *lmap, const UBlk *ublk,
             const int64_t *ucol_voff, const int *ucol_fst) {
     using Sx = S<T>;
     using M = Mma<T>;
+    constexpr int WN = 2;                   // waves along N
+    constexpr int FM = 2, FN = 4;           // fragments per wave (32 x 64)
     constexpr int LDS_A = SB_BM + 4, LDS_B = SB_BN + 4;
     constexpr int STAGE = SB_BK * LDS_A + SB_BK * LDS_B;
     constexpr int CLD = SB_BM + 1; // C staging: [64 cols][CLD]
+    constexpr int AE = SB_BM * SB_BK / SB_THREADS, BE = SB_BN * SB_BK / SB_THREADS; // 4, 4
     static_assert(64 * CLD <= 2 * STAGE, "C staging must fit in the stage buffers");
     __shared__ T smem[2 * STAGE];
     __shared__ int s_rg[SB_BM], s_ra[SB_BM], s_cg[SB_BN], s_cb[SB_BN];
@@ -870,53 +886,57 @@ k_schur_big(const TileItem *tiles, const KInfo<T> *kinfo, T *Lval, T *Uval,
     const TileItem ti = tiles[blockIdx.x];
     const KInfo<T> ki = kinfo[ti.kslot];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int wr = wid >> 1, wc = wid & 1;
+    const int wr = wid / WN, wc = wid % WN;
     const int row0 = ti.tm * SB_BM, col0 = ti.tn * SB_BN;
     const int mrows = min(SB_BM, ki.m - row0), ncols = min(SB_BN, ki.n - col0);
     if (tid < SB_BM) {
         s_rg[tid] = tid < mrows ? ki.rg[row0 + tid] : 0;
         s_ra[tid] = tid < mrows ? ki.ra[row0 + tid] : 0;
-        s_cg[tid] = tid < ncols ? ki.cg[col0 + tid] : 0;
-        s_cb[tid] = tid < ncols ? ki.cb[col0 + tid] : 0;
+    } else if (tid < SB_BM + SB_BN) {
+        const int c = tid - SB_BM;
+        s_cg[c] = c < ncols ? ki.cg[col0 + c] : 0;
+        s_cb[c] = c < ncols ? ki.cb[col0 + c] : 0;
     }
-    // A: thread owns row ar and k = ak + 2s (s < 8); B: column bc, k = bk + s
-    const int ar = tid & 127, ak = tid >> 7;
+    // A: thread owns row ar and k = ak + 4s (s < 4); B: column bc, k = bk..bk+3.
+    // Loads are unconditional from clamped in-bounds addresses; out-of-range
+    // elements are zeroed afterwards (no per-element branches).
+    const int ar = tid & (SB_BM - 1), ak = tid / SB_BM;
     const bool avalid = ar < mrows;
-    const T *ap = ki.a + row0 + ar;
-    const int bc = tid >> 1, bk = (tid & 1) * 8;
+    const T *ap = ki.a + row0 + (avalid ? ar : 0);
+    const int bc = tid / (SB_BK / BE), bk = (tid % (SB_BK / BE)) * BE;
     const bool bvalid = bc < ncols;
-    int bt0 = 0;
-    const T *ub = ki.ubase;
-    if (bvalid) {
-        bt0 = ki.ct0[col0 + bc];
-        ub = ki.ubase + ki.cvoff[col0 + bc] - bt0;
-    }
-    T ra[8], rb[8];
+    const int bcc = col0 + (bvalid ? bc : 0);
+    const int bt0 = ki.ct0[bcc];
+    const T *ub = ki.ubase + ki.cvoff[bcc] - bt0; // ub[t] valid for bt0 <= t < kmin + kw
+    const int tlast = ki.kmin + ki.kw - 1;
+    T ra[AE], rb[BE];
     auto gload = [&](int k0) {
 #pragma unroll
-        for (int s = 0; s < 8; ++s) {
-            const int kk = k0 + ak + 2 * s;
-            ra[s] = (avalid && kk < ki.kw) ? ap[(int64_t)(ki.kmin + kk) * ki.lda] : Sx::zero();
+        for (int s = 0; s < AE; ++s) {
+            const int kk = k0 + ak + (SB_THREADS / SB_BM) * s;
+            const T v = gld(ap + (int64_t)(ki.kmin + min(kk, ki.kw - 1)) * ki.lda);
+            ra[s] = (avalid && kk < ki.kw) ? v : Sx::zero();
         }
 #pragma unroll
-        for (int s = 0; s < 8; ++s) {
-            const int kk = k0 + bk + s, t = ki.kmin + kk;
-            rb[s] = (bvalid && kk < ki.kw && t >= bt0) ? ub[t] : Sx::zero();
+        for (int s = 0; s < BE; ++s) {
+            const int t = ki.kmin + k0 + bk + s;
+            const T v = gld(ub + max(min(t, tlast), bt0));
+            rb[s] = (bvalid && t <= tlast && t >= bt0) ? v : Sx::zero();
         }
     };
     auto lstore = [&](int buf) {
         T *sA = smem + buf * STAGE, *sB = sA + SB_BK * LDS_A;
 #pragma unroll
-        for (int s = 0; s < 8; ++s) sA[(ak + 2 * s) * LDS_A + ar] = ra[s];
+        for (int s = 0; s < AE; ++s) sA[(ak + (SB_THREADS / SB_BM) * s) * LDS_A + ar] = ra[s];
 #pragma unroll
-        for (int s = 0; s < 8; ++s) sB[(bk + s) * LDS_B + bc] = rb[s];
+        for (int s = 0; s < BE; ++s) sB[(bk + s) * LDS_B + bc] = rb[s];
     };
 
-    typename M::acc_t acc[4][4];
+    typename M::acc_t acc[FM][FN];
 #pragma unroll
-    for (int a = 0; a < 4; ++a)
+    for (int a = 0; a < FM; ++a)
 #pragma unroll
-        for (int b = 0; b < 4; ++b) acc[a][b] = M::zero();
+        for (int b = 0; b < FN; ++b) acc[a][b] = M::zero();
 
     const int nst = (ki.kw + SB_BK - 1) / SB_BK;
     gload(0);
@@ -929,16 +949,15 @@ k_schur_big(const TileItem *tiles, const KInfo<T> *kinfo, T *Lval, T *Uval,
 #pragma unroll
         for (int ks = 0; ks < SB_BK; ks += M::KSTEP) {
             const int kl = ks + (lane >> 4);
-            T av[4], bv[4];
+            T av[FM], bv[FN];
 #pragma unroll
-            for (int f = 0; f < 4; ++f) {
-                av[f] = sA[kl * LDS_A + wr * 64 + f * 16 + (lane & 15)];
-                bv[f] = sB[kl * LDS_B + wc * 64 + f * 16 + (lane & 15)];
-            }
+            for (int f = 0; f < FM; ++f) av[f] = sA[kl * LDS_A + wr * (16 * FM) + f * 16 + (lane & 15)];
 #pragma unroll
-            for (int fm = 0; fm < 4; ++fm)
+            for (int f = 0; f < FN; ++f) bv[f] = sB[kl * LDS_B + wc * (16 * FN) + f * 16 + (lane & 15)];
 #pragma unroll
-                for (int fn = 0; fn < 4; ++fn) M::step(acc[fm][fn], av[fm], bv[fn]);
+            for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+                for (int fn = 0; fn < FN; ++fn) M::step(acc[fm][fn], av[fm], bv[fn]);
         }
         if (more) lstore((st + 1) & 1);
         __syncthreads();
@@ -946,7 +965,7 @@ k_schur_big(const TileItem *tiles, const KInfo<T> *kinfo, T *Lval, T *Uval,
 
     // ---- epilogue: two passes of 64 columns through LDS, column-contiguous
     T *sC = smem; // [c][r], ld CLD
-    const int r = tid & 127;
+    const int r = tid & (SB_BM - 1);
     const int gr = s_rg[r], a = s_ra[r];
     const int *prow = ki.pair + (int64_t)a * ki.nub;
     int lastb = -1, h = 0, ldh = 0;
@@ -954,19 +973,19 @@ k_schur_big(const TileItem *tiles, const KInfo<T> *kinfo, T *Lval, T *Uval,
     for (int pass = 0; pass < 2; ++pass) {
         if (wc == pass) {
 #pragma unroll
-            for (int fm = 0; fm < 4; ++fm)
+            for (int fm = 0; fm < FM; ++fm)
 #pragma unroll
-                for (int fn = 0; fn < 4; ++fn)
+                for (int fn = 0; fn < FN; ++fn)
 #pragma unroll
                     for (int i = 0; i < 4; ++i) {
-                        const int rr = wr * 64 + fm * 16 + M::row(lane, i);
+                        const int rr = wr * (16 * FM) + fm * 16 + M::row(lane, i);
                         const int cc = fn * 16 + (lane & 15);
                         sC[cc * CLD + rr] = M::get(acc[fm][fn], i);
                     }
         }
         __syncthreads();
         if (r < mrows) {
-            for (int cl = tid >> 7; cl < 64; cl += 2) {
+            for (int cl = tid / SB_BM; cl < 64; cl += SB_THREADS / SB_BM) {
                 const int c = pass * 64 + cl;
                 if (c >= ncols) break;
                 const T v = sC[cl * CLD + r];

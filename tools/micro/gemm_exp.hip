@@ -1,0 +1,151 @@
+// GEMM main-loop experiments for the fp64 Schur kernel (not product code).
+// C(m x n) += A(m x kw, col-major) * B(kw x n, col-major, ld kw); 128-row
+// style tiles, v_mfma_f64_16x16x4f64, LDS staging, variants by template.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
+typedef __attribute__((ext_vector_type(4))) double v4d;
+typedef __attribute__((ext_vector_type(2))) double v2d;
+
+template <typename T> __device__ __forceinline__ T gld(const T *p) {
+    return *(const __attribute__((address_space(1))) T *)p;
+}
+
+// WM x WN waves, each wave FM x FN fragments of 16x16.
+template <int BM, int BN, int BK, int WM, int WN, bool PRIO, bool B2>
+__global__ void __launch_bounds__(64 * WM * WN)
+k_gemm(const double *A, const double *B, double *C, int m, int n, int kw) {
+    constexpr int NT = 64 * WM * WN, FM = BM / WM / 16, FN = BN / WN / 16;
+    constexpr int LA = BM + 4, LB = BN + 4, STAGE = BK * (LA + LB);
+    constexpr int AE = BM * BK / NT, BE = BN * BK / NT; // elements per thread
+    static_assert(AE >= 1 && BE >= 1, "");
+    __shared__ double smem[2 * STAGE];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wr = wid / WN, wc = wid % WN;
+    const int tn = (n + BN - 1) / BN;
+    const int row0 = (blockIdx.x / tn) * BM, col0 = (blockIdx.x % tn) * BN;
+    // A: thread -> row ar, k = ak + s*(NT/BM)
+    const int ar = tid % BM, ak = tid / BM;
+    constexpr int ASTR = NT / BM;
+    // B: thread -> column bc, k = bk .. bk+BE-1 (contiguous)
+    constexpr int TPC = BK / BE; // threads per column
+    const int bc = tid / TPC, bk = (tid % TPC) * BE;
+    const double *ap = A + row0 + ar;
+    const double *bp = B + (size_t)(col0 + bc) * kw;
+    double ra[AE], rb[BE];
+    auto gload = [&](int k0) {
+#pragma unroll
+        for (int s = 0; s < AE; ++s) ra[s] = gld(ap + (size_t)(k0 + ak + s * ASTR) * m);
+        if constexpr (B2 && BE % 2 == 0) {
+#pragma unroll
+            for (int s = 0; s < BE; s += 2) {
+                v2d v = gld((const v2d *)(bp + k0 + bk + s));
+                rb[s] = v[0];
+                rb[s + 1] = v[1];
+            }
+        } else {
+#pragma unroll
+            for (int s = 0; s < BE; ++s) rb[s] = gld(bp + k0 + bk + s);
+        }
+    };
+    auto lstore = [&](int buf) {
+        double *sA = smem + buf * STAGE, *sB = sA + BK * LA;
+#pragma unroll
+        for (int s = 0; s < AE; ++s) sA[(ak + s * ASTR) * LA + ar] = ra[s];
+#pragma unroll
+        for (int s = 0; s < BE; ++s) sB[(bk + s) * LB + bc] = rb[s];
+    };
+    v4d acc[FM][FN];
+#pragma unroll
+    for (int a = 0; a < FM; ++a)
+#pragma unroll
+        for (int b = 0; b < FN; ++b) acc[a][b] = v4d{0, 0, 0, 0};
+    const int nst = kw / BK;
+    gload(0);
+    lstore(0);
+    __syncthreads();
+    for (int st = 0; st < nst; ++st) {
+        const bool more = st + 1 < nst;
+        if (more) gload((st + 1) * BK);
+        const double *sA = smem + (st & 1) * STAGE, *sB = sA + BK * LA;
+        if (PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int ks = 0; ks < BK; ks += 4) {
+            const int kl = ks + (lane >> 4);
+            double av[FM], bv[FN];
+#pragma unroll
+            for (int f = 0; f < FM; ++f) av[f] = sA[kl * LA + wr * (BM / WM) + f * 16 + (lane & 15)];
+#pragma unroll
+            for (int f = 0; f < FN; ++f) bv[f] = sB[kl * LB + wc * (BN / WN) + f * 16 + (lane & 15)];
+#pragma unroll
+            for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+                for (int fn = 0; fn < FN; ++fn)
+                    acc[fm][fn] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[fm], bv[fn], acc[fm][fn], 0, 0, 0);
+        }
+        if (PRIO) __builtin_amdgcn_s_setprio(0);
+        if (more) lstore((st + 1) & 1);
+        __syncthreads();
+    }
+#pragma unroll
+    for (int fm = 0; fm < FM; ++fm)
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int r = row0 + wr * (BM / WM) + fm * 16 + (lane >> 4) + 4 * i;
+                const int c = col0 + wc * (BN / WN) + fn * 16 + (lane & 15);
+                C[r + (size_t)c * m] += acc[fm][fn][i];
+            }
+}
+
+template <int BM, int BN, int BK, int WM, int WN, bool PRIO, bool B2>
+void run(const char *name, const double *A, const double *B, double *C, int m, int n, int kw) {
+    int nb = (m / BM) * (n / BN);
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    float best = 1e30f;
+    for (int r = 0; r < 4; ++r) {
+        hipEventRecord(e0);
+        hipLaunchKernelGGL((k_gemm<BM, BN, BK, WM, WN, PRIO, B2>), dim3(nb), dim3(64 * WM * WN), 0, 0, A, B, C, m, n, kw);
+        hipEventRecord(e1);
+        hipEventSynchronize(e1);
+        float ms;
+        hipEventElapsedTime(&ms, e0, e1);
+        if (r) best = ms < best ? ms : best;
+    }
+    CK(hipGetLastError());
+    printf("%-44s %8.3f ms %7.2f TFLOP/s\n", name, best, 2.0 * m * n * kw / best / 1e9);
+}
+
+int main(int argc, char **argv) {
+    int m = argc > 1 ? atoi(argv[1]) : 8192, n = argc > 2 ? atoi(argv[2]) : 8192;
+    int kw = argc > 3 ? atoi(argv[3]) : 256;
+    std::vector<double> h((size_t)m * kw);
+    for (size_t i = 0; i < h.size(); ++i) h[i] = (double)((i * 2654435761u) % 1000) / 1000.0 - 0.5;
+    double *A, *B, *C;
+    CK(hipMalloc(&A, (size_t)m * kw * 8));
+    CK(hipMalloc(&B, (size_t)n * kw * 8));
+    CK(hipMalloc(&C, (size_t)m * n * 8));
+    CK(hipMemcpy(A, h.data(), (size_t)m * kw * 8, hipMemcpyHostToDevice));
+    CK(hipMemcpy(B, h.data(), (size_t)std::min(m, n) * kw * 8, hipMemcpyHostToDevice));
+    CK(hipMemset(C, 0, (size_t)m * n * 8));
+    run<128, 128, 16, 4, 2, false, true>("128x128x16 4x2w B-dwordx4", A, B, C, m, n, kw);
+    run<128, 128, 16, 4, 2, true, true>("128x128x16 4x2w prio", A, B, C, m, n, kw);
+    run<128, 128, 32, 4, 2, false, true>("128x128x32 4x2w", A, B, C, m, n, kw);
+    run<128, 128, 16, 2, 4, false, true>("128x128x16 2x4w", A, B, C, m, n, kw);
+    run<128, 128, 16, 4, 4, false, true>("128x128x16 4x4w (16 waves)", A, B, C, m, n, kw);
+    run<256, 128, 16, 8, 2, false, true>("256x128x16 8x2w (16 waves)", A, B, C, m, n, kw);
+    run<128, 256, 16, 4, 4, false, true>("128x256x16 4x4w (16 waves)", A, B, C, m, n, kw);
+    run<256, 128, 16, 4, 4, false, true>("256x128x16 4x4w (16 waves)", A, B, C, m, n, kw);
+    run<128, 64, 16, 4, 2, false, true>("128x64x16 4x2w", A, B, C, m, n, kw);
+    run<64, 128, 16, 2, 4, false, true>("64x128x16 2x4w", A, B, C, m, n, kw);
+    run<64, 64, 16, 2, 2, false, true>("64x64x16 2x2w", A, B, C, m, n, kw);
+    run<64, 64, 32, 2, 2, false, true>("64x64x32 2x2w", A, B, C, m, n, kw);
+    return 0;
+}

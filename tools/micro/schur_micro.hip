@@ -9,24 +9,43 @@
 #include <cstdlib>
 #include <vector>
 
+#include <rocblas/rocblas.h>
+
 #include "kernels.h"
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
 
 using namespace slu;
 
+template <int NACC>
 __global__ void __launch_bounds__(256) k_peak(double *out, int iters) {
     typedef __attribute__((ext_vector_type(4))) double v4;
-    v4 acc[8];
-    for (int i = 0; i < 8; ++i) acc[i] = v4{0, 0, 0, 0};
+    v4 acc[NACC];
+    for (int i = 0; i < NACC; ++i) acc[i] = v4{0, 0, 0, 0};
     double a = threadIdx.x * 1e-3, b = blockIdx.x * 1e-3;
     for (int it = 0; it < iters; ++it) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) acc[i] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[i], 0, 0, 0);
+        for (int i = 0; i < NACC; ++i) acc[i] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[i], 0, 0, 0);
     }
     double s = 0;
-    for (int i = 0; i < 8; ++i) s += acc[i][0] + acc[i][1] + acc[i][2] + acc[i][3];
+    for (int i = 0; i < NACC; ++i) s += acc[i][0] + acc[i][1] + acc[i][2] + acc[i][3];
     if (s == 123.456) out[0] = s;
+}
+template <int NACC>
+void peak(double *dout, int wg, int iters) {
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    hipLaunchKernelGGL(k_peak<NACC>, dim3(wg), dim3(256), 0, 0, dout, iters);
+    hipEventRecord(e0);
+    hipLaunchKernelGGL(k_peak<NACC>, dim3(wg), dim3(256), 0, 0, dout, iters);
+    hipEventRecord(e1);
+    hipEventSynchronize(e1);
+    float ms;
+    hipEventElapsedTime(&ms, e0, e1);
+    double fl = (double)wg * 4 * iters * NACC * 2048.0;
+    printf("peak f64 mfma 16x16x4: %5d WGs x 4 waves (%.1f waves/SIMD), %2d acc: %7.3f ms %.2f TFLOP/s\n",
+           wg, wg * 4.0 / 1024, NACC, ms, fl / ms / 1e9);
 }
 
 int main(int argc, char **argv) {
@@ -38,16 +57,38 @@ int main(int argc, char **argv) {
     float ms;
     double *dout;
     CK(hipMalloc(&dout, 8));
-    for (int wg : {256, 512, 1024, 2048}) {
-        int iters = 2000;
-        hipLaunchKernelGGL(k_peak, dim3(wg), dim3(256), 0, 0, dout, iters);
-        CK(hipEventRecord(e0));
-        hipLaunchKernelGGL(k_peak, dim3(wg), dim3(256), 0, 0, dout, iters);
-        CK(hipEventRecord(e1));
-        CK(hipEventSynchronize(e1));
-        CK(hipEventElapsedTime(&ms, e0, e1));
-        double fl = (double)wg * 4 * iters * 8 * 2048.0;
-        printf("peak f64 mfma 16x16x4: %4d WGs x 4 waves: %.2f TFLOP/s\n", wg, fl / ms / 1e9);
+    if (getenv("PEAK")) {
+        for (int wg : {256, 512, 1024, 2048, 4096}) {
+            peak<1>(dout, wg, 20000);
+            peak<4>(dout, wg, 5000);
+            peak<8>(dout, wg, 2500);
+            peak<16>(dout, wg, 1250);
+        }
+    }
+    if (getenv("BLAS")) {
+        rocblas_handle h;
+        rocblas_create_handle(&h);
+        for (int sz : {8192, 4096}) {
+            for (int kk : {256, 8192}) {
+                if (kk > sz) continue;
+                double *A, *B, *C;
+                CK(hipMalloc(&A, (size_t)sz * kk * 8));
+                CK(hipMalloc(&B, (size_t)sz * kk * 8));
+                CK(hipMalloc(&C, (size_t)sz * sz * 8));
+                CK(hipMemset(A, 0, (size_t)sz * kk * 8));
+                CK(hipMemset(B, 0, (size_t)sz * kk * 8));
+                double al = -1, be = 1;
+                for (int r = 0; r < 3; ++r) {
+                    CK(hipEventRecord(e0));
+                    rocblas_dgemm(h, rocblas_operation_none, rocblas_operation_none, sz, sz, kk, &al, A, sz, B, kk, &be, C, sz);
+                    CK(hipEventRecord(e1));
+                    CK(hipEventSynchronize(e1));
+                    CK(hipEventElapsedTime(&ms, e0, e1));
+                }
+                printf("rocblas_dgemm %d x %d x %d: %.3f ms %.2f TFLOP/s\n", sz, sz, kk, ms, 2.0 * sz * sz * kk / ms / 1e9);
+                hipFree(A); hipFree(B); hipFree(C);
+            }
+        }
     }
     // ---- synthetic supernode update
     std::vector<double> hA((size_t)m * kw), hB((size_t)kw * n);
@@ -88,7 +129,7 @@ int main(int argc, char **argv) {
     double fl = 2.0 * m * n * kw;
     for (int r = 0; r < reps; ++r) {
         CK(hipEventRecord(e0));
-        hipLaunchKernelGGL(k_schur_big<double>, dim3(tiles.size()), dim3(256), 0, 0, dt, dk, dC,
+        hipLaunchKernelGGL(k_schur_big<double>, dim3(tiles.size()), dim3(SB_THREADS), 0, 0, dt, dk, dC,
                            (double *)nullptr, dl, dmap, (const UBlk *)nullptr, (const int64_t *)nullptr,
                            (const int *)nullptr);
         CK(hipEventRecord(e1));
