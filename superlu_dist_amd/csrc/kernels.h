@@ -38,6 +38,7 @@ template <> struct S<double> {
     __device__ static bool iszero(T a) { return a == 0.0; }
     __device__ static T thresh(T a, double t) { return a < 0 ? -t : t; }
     __device__ static void sub_to(T *p, T v) { *p -= v; }
+    __device__ static T sub(T a, T b) { return a - b; }
     __device__ static void atomic_sub(T *p, T v) { unsafeAtomicAdd(p, -v); }
 };
 template <> struct S<float> {
@@ -52,6 +53,7 @@ template <> struct S<float> {
     __device__ static bool iszero(T a) { return a == 0.0f; }
     __device__ static T thresh(T a, double t) { return a < 0 ? -(float)t : (float)t; }
     __device__ static void sub_to(T *p, T v) { *p -= v; }
+    __device__ static T sub(T a, T b) { return a - b; }
     __device__ static void atomic_sub(T *p, T v) { unsafeAtomicAdd(p, -v); }
 };
 template <> struct S<zc> {
@@ -80,6 +82,7 @@ template <> struct S<zc> {
     __device__ static bool iszero(T a) { return a.r == 0.0 && a.i == 0.0; }
     __device__ static T thresh(T a, double t) { return {a.r < 0 ? -t : t, 0.0}; }
     __device__ static void sub_to(T *p, T v) { p->r -= v.r; p->i -= v.i; }
+    __device__ static T sub(T a, T b) { return {a.r - b.r, a.i - b.i}; }
     __device__ static void atomic_sub(T *p, T v) {
         unsafeAtomicAdd(&p->r, -v.r);
         unsafeAtomicAdd(&p->i, -v.i);
@@ -909,27 +912,35 @@ k_schur_big(const TileItem *tiles, const KInfo<T> *kinfo, T *Lval, T *Uval,
     const int bt0 = ki.ct0[bcc];
     const T *ub = ki.ubase + ki.cvoff[bcc] - bt0; // ub[t] valid for bt0 <= t < kmin + kw
     const int tlast = ki.kmin + ki.kw - 1;
+    // The zeroing of out-of-range elements happens at the LDS store, after
+    // the current stage's MFMAs, so the prefetch's latency is not waited on
+    // before them.
     T ra[AE], rb[BE];
     auto gload = [&](int k0) {
 #pragma unroll
         for (int s = 0; s < AE; ++s) {
             const int kk = k0 + ak + (SB_THREADS / SB_BM) * s;
-            const T v = gld(ap + (int64_t)(ki.kmin + min(kk, ki.kw - 1)) * ki.lda);
-            ra[s] = (avalid && kk < ki.kw) ? v : Sx::zero();
+            ra[s] = gld(ap + (int64_t)(ki.kmin + min(kk, ki.kw - 1)) * ki.lda);
         }
 #pragma unroll
         for (int s = 0; s < BE; ++s) {
             const int t = ki.kmin + k0 + bk + s;
-            const T v = gld(ub + max(min(t, tlast), bt0));
-            rb[s] = (bvalid && t <= tlast && t >= bt0) ? v : Sx::zero();
+            rb[s] = gld(ub + max(min(t, tlast), bt0));
         }
     };
-    auto lstore = [&](int buf) {
+    auto lstore = [&](int buf, int k0) {
         T *sA = smem + buf * STAGE, *sB = sA + SB_BK * LDS_A;
 #pragma unroll
-        for (int s = 0; s < AE; ++s) sA[(ak + (SB_THREADS / SB_BM) * s) * LDS_A + ar] = ra[s];
+        for (int s = 0; s < AE; ++s) {
+            const int kk = k0 + ak + (SB_THREADS / SB_BM) * s;
+            sA[(ak + (SB_THREADS / SB_BM) * s) * LDS_A + ar] =
+                (avalid && kk < ki.kw) ? ra[s] : Sx::zero();
+        }
 #pragma unroll
-        for (int s = 0; s < BE; ++s) sB[(bk + s) * LDS_B + bc] = rb[s];
+        for (int s = 0; s < BE; ++s) {
+            const int t = ki.kmin + k0 + bk + s;
+            sB[(bk + s) * LDS_B + bc] = (bvalid && t <= tlast && t >= bt0) ? rb[s] : Sx::zero();
+        }
     };
 
     typename M::acc_t acc[FM][FN];
@@ -940,7 +951,7 @@ k_schur_big(const TileItem *tiles, const KInfo<T> *kinfo, T *Lval, T *Uval,
 
     const int nst = (ki.kw + SB_BK - 1) / SB_BK;
     gload(0);
-    lstore(0);
+    lstore(0, 0);
     __syncthreads();
     for (int st = 0; st < nst; ++st) {
         const bool more = st + 1 < nst;
@@ -959,13 +970,18 @@ k_schur_big(const TileItem *tiles, const KInfo<T> *kinfo, T *Lval, T *Uval,
 #pragma unroll
                 for (int fn = 0; fn < FN; ++fn) M::step(acc[fm][fn], av[fm], bv[fn]);
         }
-        if (more) lstore((st + 1) & 1);
+        if (more) lstore((st + 1) & 1, (st + 1) * SB_BK);
         __syncthreads();
     }
 
-    // ---- epilogue: two passes of 64 columns through LDS, column-contiguous
+    // ---- epilogue: two passes of 64 columns through LDS, column-contiguous.
+    // Thread (r, q) owns row r and columns q, q+4, ...; destination addresses
+    // are formed for EB columns at a time and their EB read-modify-writes are
+    // issued as one batch of independent loads, then the stores (no two
+    // elements of a tile share a destination, so nothing aliases).
     T *sC = smem; // [c][r], ld CLD
-    const int r = tid & (SB_BM - 1);
+    constexpr int TPR = SB_THREADS / SB_BM, CPT = 64 / TPR, EB = 4;
+    const int r = tid & (SB_BM - 1), q = tid / SB_BM;
     const int gr = s_rg[r], a = s_ra[r];
     const int *prow = ki.pair + (int64_t)a * ki.nub;
     int lastb = -1, h = 0, ldh = 0;
@@ -985,30 +1001,49 @@ k_schur_big(const TileItem *tiles, const KInfo<T> *kinfo, T *Lval, T *Uval,
         }
         __syncthreads();
         if (r < mrows) {
-            for (int cl = tid / SB_BM; cl < 64; cl += SB_THREADS / SB_BM) {
-                const int c = pass * 64 + cl;
-                if (c >= ncols) break;
-                const T v = sC[cl * CLD + r];
-                const int b = s_cb[c], gc = s_cg[c];
-                if (b != lastb) {
-                    lastb = b;
-                    h = prow[b];
-                    if (h >= 0) {
-                        const LBlk L = lblk[h];
-                        ldh = L.ld;
-                        rbase = L.colvoff + lmap[L.mapoff + gr - L.frow] - (int64_t)L.fcol * L.ld;
+#pragma unroll
+            for (int j0 = 0; j0 < CPT; j0 += EB) {
+                T *dp[EB];
+                T v[EB];
+#pragma unroll
+                for (int j = 0; j < EB; ++j) {
+                    const int cl = q + TPR * (j0 + j), c = pass * 64 + cl;
+                    dp[j] = nullptr;
+                    v[j] = Sx::zero();
+                    if (c < ncols) {
+                        v[j] = sC[cl * CLD + r];
+                        const int b = s_cb[c], gc = s_cg[c];
+                        if (b != lastb) {
+                            lastb = b;
+                            h = prow[b];
+                            if (h >= 0) {
+                                const LBlk L = lblk[h];
+                                ldh = L.ld;
+                                rbase = L.colvoff + lmap[L.mapoff + gr - L.frow] -
+                                        (int64_t)L.fcol * L.ld;
+                            }
+                        }
+                        if (h >= 0) {
+                            dp[j] = Lval + rbase + (int64_t)gc * ldh;
+                        } else {
+                            const UBlk U = ublk[~h];
+                            const int64_t e = U.coloff + gc - U.fcol;
+                            dp[j] = Uval + ucol_voff[e] + gr - ucol_fst[e];
+                        }
                     }
                 }
-                T *dst;
-                if (h >= 0) {
-                    dst = Lval + rbase + (int64_t)gc * ldh;
+                if (ki.atomic) {
+#pragma unroll
+                    for (int j = 0; j < EB; ++j)
+                        if (dp[j]) Sx::atomic_sub(dp[j], v[j]);
                 } else {
-                    const UBlk U = ublk[~h];
-                    const int64_t e = U.coloff + gc - U.fcol;
-                    dst = Uval + ucol_voff[e] + gr - ucol_fst[e];
+                    T o[EB];
+#pragma unroll
+                    for (int j = 0; j < EB; ++j) o[j] = dp[j] ? *dp[j] : Sx::zero();
+#pragma unroll
+                    for (int j = 0; j < EB; ++j)
+                        if (dp[j]) *dp[j] = Sx::sub(o[j], v[j]);
                 }
-                if (ki.atomic) Sx::atomic_sub(dst, v);
-                else Sx::sub_to(dst, v);
             }
         }
         __syncthreads();

@@ -122,9 +122,28 @@ int main(int argc, char **argv) {
     auto *dl = (LBlk *)up(&L, sizeof L);
     auto *dmap = (int *)up(lmap.data(), m * 4);
     int tm = (m + SB_BM - 1) / SB_BM, tn = (n + SB_BN - 1) / SB_BN;
-    std::vector<TileItem> tiles;
-    for (int i = 0; i < tm; ++i)
-        for (int j = 0; j < tn; ++j) tiles.push_back(TileItem{0, i, j});
+    std::vector<TileItem> tiles0, tiles;
+    const int order = getenv("ORDER") ? atoi(getenv("ORDER")) : 0;
+    const int G = getenv("GROUP") ? atoi(getenv("GROUP")) : 8;
+    if (order == 0 || order == 2) {
+        for (int i = 0; i < tm; ++i)
+            for (int j = 0; j < tn; ++j) tiles0.push_back(TileItem{0, i, j});
+    } else { // groups of G tile rows, column-major inside a group
+        for (int i0 = 0; i0 < tm; i0 += G)
+            for (int j = 0; j < tn; ++j)
+                for (int i = i0; i < std::min(tm, i0 + G); ++i) tiles0.push_back(TileItem{0, i, j});
+    }
+    if (order == 2 || order == 3) { // XCD x takes the x-th contiguous chunk of the order
+        const size_t T = tiles0.size(), ch = (T + 7) / 8;
+        tiles.resize(T);
+        std::vector<size_t> pos;
+        for (size_t j = 0; j < ch; ++j)
+            for (size_t x = 0; x < 8; ++x) pos.push_back(x * ch + j);
+        size_t p = 0;
+        for (size_t q : pos) if (q < T) tiles[p++] = tiles0[q];
+    } else tiles = tiles0;
+    if (order == 9) // timing only: every tile reads the same A rows / B columns (L2-resident operands)
+        for (auto &t : tiles) { t.tm = 0; t.tn = 0; }
     auto *dt = (TileItem *)up(tiles.data(), tiles.size() * sizeof(TileItem));
     double fl = 2.0 * m * n * kw;
     for (int r = 0; r < reps; ++r) {
