@@ -1277,7 +1277,7 @@ struct Plan : PlanBase {
                 });
             if (R.df_n)
                 span(0, P, [&] {
-                    hipLaunchKernelGGL(k_diag_lu_blk<T>, dim3(R.df_n), dim3(256), 0, P,
+                    hipLaunchKernelGGL(k_diag_lu_f<T>, dim3(R.df_n), dim3(DF_THREADS), 0, P,
                                        d_df.p + R.df_off, thresh, opts.replace_tiny_pivot,
                                        d_counters.p, d_zpiv.p);
                 });

@@ -574,17 +574,41 @@ template <typename T> struct DiagItemF {
     int ld, w, k, fcol;
 };
 
-// Blocked right-looking LU of one <= 256 x 256 diagonal block per workgroup:
-// panels of PW columns are factored in LDS (SRC/pdgstrf2.c:213-269 semantics:
-// tiny-pivot replacement, reciprocal scaling, zero-pivot info), the U12 row
-// block is L11^{-1} A12, and the trailing block is updated with MFMA
-// (A22 -= L21 U12).  The inverses of the PW x PW diagonal blocks of L and U
-// are written to dinv for the MFMA TRSMs.
+// Wave-uniform read of lane l's value (v_readlane; l must be uniform).
+__device__ inline double rlane(double v, int l) {
+    const long long x = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)x, l);
+    const int hi = __builtin_amdgcn_readlane((int)(x >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+__device__ inline float rlane(float v, int l) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+__device__ inline zc rlane(zc v, int l) { return {rlane(v.r, l), rlane(v.i, l)}; }
+
+// Blocked right-looking LU of one <= 256 x 256 diagonal block per 512-thread
+// workgroup, built for latency (the top-of-tree levels hold one supernode
+// each, so this kernel sits on the critical path).  Per panel of PW columns:
+//   0. the panel (rows p0.., PW columns) and the U12 row block (PW rows,
+//      columns right of the panel) are staged into LDS, coalesced;
+//   1. waves 0 and 1 both factor the PW x PW block A11 in registers (lane =
+//      row, the pivot row read with v_readlane: no LDS, no barrier per
+//      column; SRC/pdgstrf2.c:213-269 semantics: tiny-pivot replacement,
+//      reciprocal scaling, a zero pivot sets info and leaves its column
+//      unscaled), then wave 0 forms U11^{-1} and wave 1 L11^{-1} (lane =
+//      column), written to LDS and to dinv for the MFMA TRSMs;
+//   2. L21 = A21 U11^{-1} and U12 = L11^{-1} A12 on MFMA (a panel with a zero
+//      pivot takes the substitution path instead, to keep the unscaled-column
+//      semantics);
+//   3. the panel and U12 go back to global memory and A22 -= L21 U12 runs on
+//      MFMA with both operands in LDS, the next batch's loads in flight.
+constexpr int DF_THREADS = 512;
 template <typename T>
-__global__ void __launch_bounds__(256)
-k_diag_lu_blk(const DiagItemF<T> *items, double thresh, int replace_tiny, int *tiny_count,
-              int *zpiv) {
+__global__ void __launch_bounds__(DF_THREADS)
+k_diag_lu_f(const DiagItemF<T> *items, double thresh, int replace_tiny, int *tiny_count,
+            int *zpiv) {
     constexpr int PW = PWOf<T>::v;
+    constexpr int NW = DF_THREADS / 64;
     using Sx = S<T>;
     using M = Mma<T>;
     const DiagItemF<T> it = items[blockIdx.x];
@@ -592,145 +616,239 @@ k_diag_lu_blk(const DiagItemF<T> *items, double thresh, int replace_tiny, int *t
     const int ld = it.ld, w = it.w, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int nb = (w + PW - 1) / PW;
     T *dinvU = it.dinv, *dinvLT = it.dinv + (int64_t)nb * PW * PW;
-    __shared__ T sP[FAST_MAXW][PW + 1];
-    __shared__ T sU12[PW][FAST_MAXW + 1];
-    __shared__ T sLinv[PW][PW + 1];
-    __shared__ T s_row[2][PW];
-    __shared__ T s_piv[2];
-    __shared__ int s_pz[2];
+    __shared__ T sP[FAST_MAXW][PW + 1];   // panel rows (row 0 = row p0), PW columns
+    __shared__ T sU[PW][FAST_MAXW + 1];   // U12: PW rows x columns right of the panel
+    __shared__ T sUi[PW][PW + 1], sLi[PW][PW + 1]; // U11^{-1}, L11^{-1}
+    __shared__ T s_rp[PW];
+    __shared__ int s_z[PW];
+    __shared__ int s_anyz;
     for (int p = 0; p < nb; ++p) {
-        const int p0 = p * PW, pw = min(PW, w - p0), nrow = w - p0;
-        // ---- unblocked LU of the nrow x pw panel: thread r keeps row r in
-        // registers; the pivot row is broadcast through LDS (double buffered,
-        // one barrier per column).
-        T xr[PW];
-        const bool own = tid < nrow;
+        const int p0 = p * PW, pw = min(PW, w - p0), nrow = w - p0, nbl = nrow - pw;
+        const int c0 = p0 + pw;
+        T *A11 = A + p0 + (int64_t)p0 * ld;
+
+        // ---- 0. stage the panel and U12 (zero outside pw)
+        for (int e = tid; e < nrow * PW; e += DF_THREADS) {
+            const int r = e % nrow, c = e / nrow;
+            sP[r][c] = c < pw ? A11[r + (int64_t)c * ld] : Sx::zero();
+        }
+        for (int e = tid; e < nbl * PW; e += DF_THREADS) {
+            const int i = e % PW, c = e / PW;
+            sU[i][c] = i < pw ? A11[i + (int64_t)(pw + c) * ld] : Sx::zero();
+        }
+        __syncthreads();
+        // ---- 1. A11 = L11 U11 in registers (wave 0); meanwhile, on the first
+        // panel, the other waves pull the trailing block into L2 (every
+        // panel's update re-reads it)
+        if (p == 0 && wid >= 1 && nbl > 0) {
+            T sink = Sx::zero();
+            for (int e = tid - 64; e < nbl * nbl; e += DF_THREADS - 64)
+                sink = Sx::sub(sink, A11[pw + e % nbl + (int64_t)(pw + e / nbl) * ld]);
+            if (Sx::abs1(sink) == -1.0) s_anyz = 0; // keeps the loads; never true
+        }
+        if (wid == 0) {
+            const int row = lane & (PW - 1);
+            T xr[PW];
 #pragma unroll
-        for (int c = 0; c < PW; ++c)
-            xr[c] = (own && c < pw) ? A[(p0 + tid) + (int64_t)(p0 + c) * ld] : Sx::zero();
+            for (int c = 0; c < PW; ++c) xr[c] = (row < pw) ? sP[row][c] : Sx::zero();
+            int anyz = 0;
 #pragma unroll
-        for (int j = 0; j < PW; ++j) {
-            if (j < pw && tid == j) { // pivot row owner
-                T piv = xr[j];
-                if (replace_tiny && Sx::abs1(piv) < thresh) {
-                    piv = Sx::thresh(piv, thresh);
-                    atomicAdd(tiny_count, 1);
+            for (int j = 0; j < PW; ++j) {
+                if (j < pw) { // uniform
+                    T piv = rlane(xr[j], j);
+                    if (replace_tiny && Sx::abs1(piv) < thresh) {
+                        piv = Sx::thresh(piv, thresh);
+                        if (lane == 0) atomicAdd(tiny_count, 1);
+                    }
+                    const int z = Sx::iszero(piv);
+                    if (z) {
+                        anyz = 1;
+                        if (lane == 0) atomicMax(&zpiv[it.k], it.fcol + p0 + j + 1);
+                    }
+                    const T rp = z ? Sx::zero() : Sx::recip(piv);
+                    // branch-free: rows below j eliminate, row j keeps the pivot
+                    const bool below = row > j;
+                    const T l = below ? (z ? xr[j] : Sx::mul(xr[j], rp)) : Sx::zero();
+                    xr[j] = below ? l : (row == j ? piv : xr[j]);
+                    __builtin_amdgcn_sched_barrier(0); // keep the readlanes next to their FMAs
+#pragma unroll
+                    for (int c = j + 1; c < PW; ++c) {
+                        xr[c] = Sx::fms(xr[c], l, rlane(xr[c], j));
+                        if ((c & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                    if (lane == 0) {
+                        s_rp[j] = rp;
+                        s_z[j] = z;
+                    }
                 }
-                xr[j] = piv;
-                const int z = Sx::iszero(piv);
-                if (z) atomicMax(&zpiv[it.k], it.fcol + p0 + j + 1);
-                s_piv[j & 1] = z ? Sx::zero() : Sx::recip(piv);
-                s_pz[j & 1] = z;
-#pragma unroll
-                for (int c = j + 1; c < PW; ++c) s_row[j & 1][c] = xr[c];
             }
-            __syncthreads();
-            if (j < pw && own && tid > j) {
-                const T rp = s_piv[j & 1];
-                const T l = s_pz[j & 1] ? xr[j] : Sx::mul(xr[j], rp);
-                xr[j] = l;
+            if (lane < pw) {
 #pragma unroll
-                for (int c = j + 1; c < PW; ++c)
-                    if (c < pw) xr[c] = Sx::fms(xr[c], l, s_row[j & 1][c]);
+                for (int c = 0; c < PW; ++c) sP[lane][c] = xr[c];
+            }
+            if (lane == 0) s_anyz = anyz;
+            if (lane >= pw && lane < PW) {
+                s_rp[lane] = Sx::zero();
+                s_z[lane] = 0;
             }
         }
-#pragma unroll
-        for (int c = 0; c < PW; ++c)
-            if (own && c < pw) {
-                sP[tid][c] = xr[c];
-                A[(p0 + tid) + (int64_t)(p0 + c) * ld] = xr[c];
-            }
         __syncthreads();
-        // inverses of the diagonal PW x PW blocks
-        if (tid < PW) { // column j of U11^{-1}
-            const int j = tid;
+        // ---- 1b. inverses from the factored A11 in LDS, lane = column j
+        // (wave 0 U11^{-1}, wave 1 L11^{-1}), column-sweep (axpy) order so the
+        // dependent chain is one multiply per row
+        if (wid < 2 && lane < PW) {
+            const int j = lane;
             T x[PW];
 #pragma unroll
-            for (int i = PW - 1; i >= 0; --i) {
-                T v = Sx::zero();
-                if (i == j) v = one_of(v);
+            for (int i = 0; i < PW; ++i) x[i] = (i == j) ? one_of(Sx::zero()) : Sx::zero();
+            if (wid == 0) { // U11 x = e_j
 #pragma unroll
-                for (int k = 0; k < PW; ++k)
-                    if (k > i && k <= j) v = Sx::fms(v, sP[i][k], x[k]);
-                x[i] = (i <= j && j < pw) ? Sx::div(v, sP[i][i]) : Sx::zero();
-            }
+                for (int i = PW - 1; i >= 0; --i) {
+                    x[i] = Sx::mul(x[i], s_rp[i]);
 #pragma unroll
-            for (int i = 0; i < PW; ++i) dinvU[(int64_t)p * PW * PW + i * PW + j] = x[i];
-        } else if (tid >= 64 && tid < 64 + PW) { // column j of L11^{-1} (unit lower)
-            const int j = tid - 64;
-            T x[PW];
+                    for (int k = 0; k < i; ++k) x[k] = Sx::fms(x[k], sP[k][i], x[i]);
+                }
 #pragma unroll
-            for (int i = 0; i < PW; ++i) {
-                T v = Sx::zero();
-                if (i == j) v = one_of(v);
+                for (int i = 0; i < PW; ++i) {
+                    const T v = (i <= j && j < pw) ? x[i] : Sx::zero();
+                    sUi[i][j] = v;
+                    dinvU[(int64_t)p * PW * PW + i * PW + j] = v;
+                }
+            } else { // L11 x = e_j (unit lower)
 #pragma unroll
-                for (int k = 0; k < PW; ++k)
-                    if (k >= j && k < i) v = Sx::fms(v, sP[i][k], x[k]);
-                x[i] = (i >= j && i < pw && j < pw) ? v : Sx::zero();
-            }
+                for (int i = 0; i < PW; ++i)
 #pragma unroll
-            for (int i = 0; i < PW; ++i) {
-                sLinv[i][j] = x[i];
-                dinvLT[(int64_t)p * PW * PW + j * PW + i] = x[i];
-            }
-        }
-        __syncthreads();
-        const int c0 = p0 + pw, ncol = w - c0;
-        if (ncol <= 0) break;
-        // U12 = L11^{-1} A12, thread per column
-        for (int c = tid; c < ncol; c += 256) {
-            T a[PW];
+                    for (int k = i + 1; k < PW; ++k) x[k] = Sx::fms(x[k], sP[k][i], x[i]);
 #pragma unroll
-            for (int k = 0; k < PW; ++k)
-                a[k] = k < pw ? A[(p0 + k) + (int64_t)(c0 + c) * ld] : Sx::zero();
-#pragma unroll
-            for (int i = 0; i < PW; ++i) {
-                T y = a[i];
-#pragma unroll
-                for (int k = 0; k < PW; ++k)
-                    if (k < i) y = Sx::fms(y, Sx::neg(sLinv[i][k]), a[k]);
-                if (i < pw) {
-                    A[(p0 + i) + (int64_t)(c0 + c) * ld] = y;
-                    sU12[i][c] = y;
+                for (int i = 0; i < PW; ++i) {
+                    const T v = (i >= j && i < pw && j < pw) ? x[i] : Sx::zero();
+                    sLi[i][j] = v;
+                    dinvLT[(int64_t)p * PW * PW + j * PW + i] = v;
                 }
             }
         }
         __syncthreads();
-        // A22 -= L21 U12 with MFMA 16x16 fragments, 4 waves; each wave takes
-        // FB fragments at a time and issues all their loads before the MFMAs
-        // (the block lives in L2: hide its latency with ILP).
-        const int nf = (ncol + 15) / 16;
-        constexpr int FB = 4;
-        for (int f0 = wid * FB; f0 < nf * nf; f0 += 4 * FB) {
-            T cv[FB][4];
+        // ---- 2. L21 = A21 U11^{-1}, U12 = L11^{-1} A12
+        if (!s_anyz) {
+            const int nfr = (nbl + 15) / 16; // L21 row fragments; U12 column fragments
+            for (int f = wid; f < 2 * nfr; f += NW) {
+                typename M::acc_t acc0 = M::zero(), acc1 = M::zero();
+                if (f < nfr) { // rows 16f.. of L21, both 16-column halves
+                    const int r = f * 16 + (lane & 15);
 #pragma unroll
-            for (int q = 0; q < FB; ++q) {
-                const int f = f0 + q, fr = f / nf, fc = f % nf;
+                    for (int ks = 0; ks < PW; ks += M::KSTEP) {
+                        const int k = ks + (lane >> 4);
+                        const T av = r < nbl ? sP[pw + r][k] : Sx::zero();
+                        M::step(acc0, av, sUi[k][lane & 15]);
+                        if (PW > 16) M::step(acc1, av, sUi[k][16 + (lane & 15)]);
+                    }
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int r = fr * 16 + M::row(lane, i), c = fc * 16 + (lane & 15);
-                    cv[q][i] = (f < nf * nf && r < ncol && c < ncol)
-                                   ? A[(c0 + r) + (int64_t)(c0 + c) * ld] : Sx::zero();
+                    for (int i = 0; i < 4; ++i) {
+                        const int rr = f * 16 + M::row(lane, i), cc = lane & 15;
+                        if (rr < nbl) {
+                            sP[pw + rr][cc] = cc < pw ? M::get(acc0, i) : Sx::zero();
+                            if (PW > 16)
+                                sP[pw + rr][16 + cc] = 16 + cc < pw ? M::get(acc1, i) : Sx::zero();
+                        }
+                    }
+                } else { // columns 16g.. of U12, both 16-row halves
+                    const int g = f - nfr, c = g * 16 + (lane & 15);
+#pragma unroll
+                    for (int ks = 0; ks < PW; ks += M::KSTEP) {
+                        const int k = ks + (lane >> 4);
+                        const T bv = c < nbl ? sU[k][c] : Sx::zero();
+                        M::step(acc0, sLi[lane & 15][k], bv);
+                        if (PW > 16) M::step(acc1, sLi[16 + (lane & 15)][k], bv);
+                    }
+                    // all waves have read their U12 columns before any is overwritten
+                    // (each fragment's columns belong to this wave only)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int ii = M::row(lane, i), cc = g * 16 + (lane & 15);
+                        if (cc < nbl) {
+                            sU[ii][cc] = ii < pw ? M::get(acc0, i) : Sx::zero();
+                            if (PW > 16) sU[16 + ii][cc] = 16 + ii < pw ? M::get(acc1, i) : Sx::zero();
+                        }
+                    }
                 }
             }
+        } else {
+            for (int t = tid; t < 2 * nbl; t += DF_THREADS) {
+                if (t < nbl) { // row t of L21: x U11 = a, column by column
+                    for (int c = 0; c < PW; ++c) {
+                        T v = sP[pw + t][c];
+                        for (int i = 0; i < c; ++i) v = Sx::fms(v, sP[pw + t][i], sP[i][c]);
+                        sP[pw + t][c] = c >= pw ? Sx::zero() : s_z[c] ? v : Sx::mul(v, s_rp[c]);
+                    }
+                } else { // column cc of U12: L11 y = a
+                    const int cc = t - nbl;
+                    for (int i = 0; i < PW; ++i) {
+                        T v = sU[i][cc];
+                        for (int k = 0; k < i; ++k) v = Sx::fms(v, sP[i][k], sU[k][cc]);
+                        sU[i][cc] = i < pw ? v : Sx::zero();
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        // ---- 3. panel and U12 back to global; A22 -= L21 U12 on MFMA
+        for (int e = tid; e < nrow * pw; e += DF_THREADS) {
+            const int r = e % nrow, c = e / nrow;
+            A11[r + (int64_t)c * ld] = sP[r][c];
+        }
+        for (int e = tid; e < nbl * pw; e += DF_THREADS) {
+            const int i = e % pw, c = e / pw;
+            A11[i + (int64_t)(pw + c) * ld] = sU[i][c];
+        }
+        if (nbl > 0) {
+            // wave wid takes fragment batches f0 = (wid + NW i) FB; the next
+            // batch's C loads are issued before this batch's MFMAs
+            const int nf = (nbl + 15) / 16, nff = nf * nf;
+            T *A22 = A + c0 + (int64_t)c0 * ld;
+            constexpr int FB = 4;
+            T cv[FB][4], cn[FB][4];
+            auto cload = [&](T (&dst)[FB][4], int f0) {
 #pragma unroll
-            for (int q = 0; q < FB; ++q) {
-                const int f = f0 + q, fr = f / nf, fc = f % nf;
-                typename M::acc_t acc = M::zero();
+                for (int q = 0; q < FB; ++q) {
+                    const int f = f0 + q, fr = f % nf, fc = f / nf;
 #pragma unroll
-                for (int ks = 0; ks < PW; ks += 4) {
-                    const int k = ks + (lane >> 4);
+                    for (int i = 0; i < 4; ++i) {
+                        const int r = fr * 16 + M::row(lane, i), c = fc * 16 + (lane & 15);
+                        dst[q][i] = (f < nff && r < nbl && c < nbl) ? A22[r + (int64_t)c * ld]
+                                                                    : Sx::zero();
+                    }
+                }
+            };
+            int f0 = wid * FB;
+            if (f0 < nff) cload(cv, f0);
+            for (; f0 < nff; f0 += NW * FB) {
+                const int f1 = f0 + NW * FB;
+                if (f1 < nff) cload(cn, f1);
+#pragma unroll
+                for (int q = 0; q < FB; ++q) {
+                    const int f = f0 + q, fr = f % nf, fc = f / nf;
+                    typename M::acc_t acc = M::zero();
                     const int r = fr * 16 + (lane & 15), c = fc * 16 + (lane & 15);
-                    T av = (k < pw && r < ncol) ? sP[pw + r][k] : Sx::zero();
-                    T bv = (k < pw && c < ncol) ? sU12[k][c] : Sx::zero();
-                    M::step(acc, av, bv);
+#pragma unroll
+                    for (int ks = 0; ks < PW; ks += M::KSTEP) {
+                        const int k = ks + (lane >> 4);
+                        const T av = (r < nbl) ? sP[pw + r][k] : Sx::zero();
+                        const T bv = (c < nbl) ? sU[k][c] : Sx::zero();
+                        M::step(acc, av, bv);
+                    }
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int rr = fr * 16 + M::row(lane, i), cc = fc * 16 + (lane & 15);
+                        if (f < nff && rr < nbl && cc < nbl)
+                            A22[rr + (int64_t)cc * ld] =
+                                Sx::fms(cv[q][i], M::get(acc, i), one_of(cv[q][i]));
+                    }
                 }
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int r = fr * 16 + M::row(lane, i), c = fc * 16 + (lane & 15);
-                    if (f < nf * nf && r < ncol && c < ncol)
-                        A[(c0 + r) + (int64_t)(c0 + c) * ld] = Sx::fms(cv[q][i], M::get(acc, i), one_of(cv[q][i]));
-                }
+                for (int q = 0; q < FB; ++q)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) cv[q][i] = cn[q][i];
             }
         }
         __syncthreads();
