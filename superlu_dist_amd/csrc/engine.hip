@@ -326,8 +326,13 @@ struct Plan : PlanBase {
                         "communicator is for a %dx%d grid rank %d, plan for %dx%d rank %d",
                         comm->nprow, comm->npcol, comm->iam, Pr, Pc, iam);
         if (comm) HIPCHK(hipSetDevice(comm->device));
-        HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
-        HIPCHK(hipStreamCreateWithFlags(&pstream, hipStreamNonBlocking));
+        // the panel stream carries the critical path (critical Schur tiles,
+        // next level's diag LU / TRSM / exchanges): higher priority, so its
+        // workgroups are dispatched ahead of the bulk Schur update's
+        int prio_lo = 0, prio_hi = 0;
+        HIPCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+        HIPCHK(hipStreamCreateWithPriority(&stream, hipStreamNonBlocking, prio_lo));
+        HIPCHK(hipStreamCreateWithPriority(&pstream, hipStreamNonBlocking, prio_hi));
         X.c = comm;
         X.s = pstream;
         int_t *hx = LU->Glu_persist->xsup;

@@ -135,6 +135,10 @@ int main(int argc, char **argv) {
     CK(hipMemcpy(A, h.data(), (size_t)m * kw * 8, hipMemcpyHostToDevice));
     CK(hipMemcpy(B, h.data(), (size_t)std::min(m, n) * kw * 8, hipMemcpyHostToDevice));
     CK(hipMemset(C, 0, (size_t)m * n * 8));
+    run<128, 128, 16, 2, 2, false, true>("128x128x16 2x2w (64x64/wave)", A, B, C, m, n, kw);
+    run<128, 128, 16, 2, 2, true, true>("128x128x16 2x2w prio", A, B, C, m, n, kw);
+    run<128, 128, 32, 2, 2, false, true>("128x128x32 2x2w", A, B, C, m, n, kw);
+    run<256, 128, 16, 4, 2, false, true>("256x128x16 4x2w (64x64/wave)", A, B, C, m, n, kw);
     run<128, 128, 16, 4, 2, false, true>("128x128x16 4x2w B-dwordx4", A, B, C, m, n, kw);
     run<128, 128, 16, 4, 2, true, true>("128x128x16 4x2w prio", A, B, C, m, n, kw);
     run<128, 128, 32, 4, 2, false, true>("128x128x32 4x2w", A, B, C, m, n, kw);
