@@ -187,6 +187,7 @@ struct LevelRange {
     int ds_off = 0, ds_n = 0;   // diag-package broadcasts
     int ps_off = 0, ps_n = 0;   // panel broadcasts
     double schur_flops = 0, big_flops = 0;
+    int atomic_tiles = 0; // tiles of supernodes whose destinations collide within the level
     bool big = false;
 };
 
@@ -795,6 +796,10 @@ struct Plan : PlanBase {
                 }
             }
             for (int key : touched) owner[key] = -1;
+            for (int i = R.big_off; i < R.big_off + R.big_n; ++i)
+                R.atomic_tiles += kinfos[R.k_off + tiles_big[i].kslot].atomic;
+            for (int i = R.tile_off; i < R.tile_off + R.tile_n; ++i)
+                R.atomic_tiles += kinfos[R.k_off + tiles[i].kslot].atomic;
         }
         khost.clear();
     }
@@ -1387,13 +1392,13 @@ struct Plan : PlanBase {
                     HIPCHK(hipEventElapsedTime(&ms, ev[s.a], ev[s.b]));
                     t[s.level][s.kind] += ms;
                 }
-                fprintf(stderr, "[slu rank %d] lvl nsup diag trsm big small  GFLOP  diag_ms trsm_ms big_ms small_ms comm_ms  TF/s\n", iam);
+                fprintf(stderr, "[slu rank %d] lvl nsup diag trsm big small atomic  GFLOP  diag_ms trsm_ms big_ms small_ms comm_ms  TF/s\n", iam);
                 for (size_t L = 0; L < levels.size(); ++L) {
                     const LevelRange &R = levels[L];
                     double sch = t[L][2] + t[L][3];
-                    fprintf(stderr, "[slu rank %d] %3zu %5zu %4d %5d %5d %5d %7.2f %8.3f %7.3f %7.3f %7.3f %7.3f %6.2f\n",
+                    fprintf(stderr, "[slu rank %d] %3zu %5zu %4d %5d %5d %5d %6d %7.2f %8.3f %7.3f %7.3f %7.3f %7.3f %6.2f\n",
                             iam, L, bylev[L].size(), R.diag_n + R.df_n, R.lf_n + R.uf_n + R.tl_n + R.tu_n,
-                            R.big_n, R.tile_n, R.schur_flops / 1e9, t[L][0], t[L][1], t[L][2], t[L][3],
+                            R.big_n, R.tile_n, R.atomic_tiles, R.schur_flops / 1e9, t[L][0], t[L][1], t[L][2], t[L][3],
                             t[L][4], sch > 0 ? R.schur_flops / sch / 1e9 : 0.0);
                 }
             }

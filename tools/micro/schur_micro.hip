@@ -107,7 +107,7 @@ int main(int argc, char **argv) {
     for (int r = 0; r < m; ++r) { rg[r] = r; lmap[r] = r; }
     auto up = [](const void *h, size_t bytes) { void *d; CK(hipMalloc(&d, bytes)); CK(hipMemcpy(d, h, bytes, hipMemcpyHostToDevice)); return d; };
     KInfo<double> ki{};
-    ki.a = dA; ki.lda = m; ki.m = m; ki.n = n; ki.kmin = 0; ki.kw = kw; ki.nub = 1; ki.atomic = 0;
+    ki.a = dA; ki.lda = m; ki.m = m; ki.n = n; ki.kmin = 0; ki.kw = kw; ki.nub = 1; ki.atomic = getenv("ATOMIC") ? 1 : 0;
     ki.ubase = dB;
     ki.cvoff = (const int64_t *)up(cvoff.data(), n * 8);
     ki.ct0 = (const int *)up(ct0.data(), n * 4);
