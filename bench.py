@@ -31,19 +31,45 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 FP64_MFMA_PEAK_TFLOPS = 78.6   # MI355X dense FP64 matrix (MI355X_MICROARCH.md / SURVEY §8d)
+FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X dense FP32 matrix (MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0
+
+# BASELINE.json configs.  The default, lap3d at nx=100, is the
+# headline metric's workload (C3 on one GPU); the others are extra
+# measurements of the same path in fp64 2D (C2), complex (C4) and fp32 (C5).
+WORKLOADS = {
+    # name: (stencil kind, dims(nx), dtype, diag, diag_im, metric, routine, dtype label, default nx)
+    "lap3d": ("3d7", lambda n: (n, n, n), 0, None, 0.0,
+              "pdgstrf fp64 GFLOP/s + factor time, 3D Laplacian n~1M", "pdgstrf", "f64", 100),
+    "lap2d": ("2d5", lambda n: (n, n, 1), 0, None, 0.0,
+              "pdgstrf fp64 GFLOP/s + factor time, 2D 5-point Laplacian", "pdgstrf", "f64", 1000),
+    "helm3d": ("3d7", lambda n: (n, n, n), 2, 6.0 - 0.25, -0.0025,
+               "pzgstrf complex fp64 GFLOP/s + factor time, 3D Helmholtz (kh=0.5)", "pzgstrf",
+               "c128", 80),
+    "st27": ("3d27", lambda n: (n, n, n), 1, None, 0.0,
+             "psgstrf fp32 GFLOP/s + factor time, 3D 27-point stencil", "psgstrf", "f32", 120),
+}
 
 
 def grid_shape(n):
     return {1: (1, 1), 2: (1, 2), 4: (2, 2), 8: (2, 4), 16: (4, 4)}.get(n, (1, n))
 
 
-def build_lu(nx, pr, pc, myrow, mycol):
-    from superlu_dist_amd.frontend import STENCIL_3D7, Csc, Symbolic, nd_order
-    A = Csc.stencil(STENCIL_3D7, nx, nx, nx)
-    S = Symbolic(A, nd_order(nx, nx, nx), 60, 256)
+def build_lu(workload, nx, pr, pc, myrow, mycol):
+    from superlu_dist_amd.frontend import STENCIL_2D5, STENCIL_3D7, STENCIL_3D27, Csc, Symbolic, nd_order
+    kind, dims, dtype, diag, diag_im = WORKLOADS[workload][:5]
+    kind = {"2d5": STENCIL_2D5, "3d7": STENCIL_3D7, "3d27": STENCIL_3D27}[kind]
+    d = dims(nx)
+    A = Csc.stencil(kind, *d, diag=diag, diag_im=diag_im, dtype=dtype)
+    S = Symbolic(A, nd_order(*d), 60, 256)
     lu = S.distribute(pr, pc, myrow, mycol)
     return A, S, lu
+
+
+def one_norm(A):
+    """||A||_1 (max column sum of |a_ij|), the anorm pdgssvx passes to pdgstrf."""
+    colptr, _, val = A.arrays()
+    return float(np.add.reduceat(np.abs(val).astype(np.float64), colptr[:-1]).max())
 
 
 def cpu_baseline(nx_sample, nranks, timeout):
@@ -78,7 +104,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--nx", type=int, default=100, help="grid points per dimension")
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="lap3d",
+                    help="lap3d = C3 (headline), lap2d = C2, helm3d = C4 (complex), st27 = C5 (fp32)")
+    ap.add_argument("--nx", type=int, default=None, help="grid points per dimension")
     ap.add_argument("--cpu-sample", type=int, default=80)
     ap.add_argument("--cpu-ranks", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
@@ -90,6 +118,11 @@ def main():
                     help="REHEARSAL ONLY: several ranks on one GPU through the host-staged "
                          "test transport (RCCL refuses duplicate devices); not a measurement")
     args = ap.parse_args()
+    W = WORKLOADS[args.workload]
+    if args.nx is None:
+        args.nx = W[8]
+    if args.workload != "lap3d":
+        args.no_cpu = True  # the CPU baseline is the reference on the headline workload
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -126,7 +159,7 @@ def main():
             dist.barrier()
 
     t0 = time.time()
-    A, S, lu = build_lu(args.nx, pr, pc, myrow, mycol)
+    A, S, lu = build_lu(args.workload, args.nx, pr, pc, myrow, mycol)
     t_front = time.time() - t0
     if world == 1:
         comm = None
@@ -141,7 +174,7 @@ def main():
     plan.upload()
     t_upload = time.time() - t0
     plan.snapshot()
-    anorm = 12.0  # ||A||_1 of the 7-point Laplacian (diag 6, six -1 neighbours)
+    anorm = one_norm(A)  # 12 for the 7-point Laplacian (diag 6, six -1 neighbours)
 
     st0 = plan.stats()
     my_flops = st0["schur_flops"] + st0["panel_flops"]
@@ -197,18 +230,31 @@ def main():
 
     if rank == 0:
         K = args.steps
-        big_s = sst["t_schur_big_ms"] / 1e3
-        launches = max(int(sst["n_schur_big_launches"]), 1)
-        achieved = sst["schur_big_flops"] / big_s / 1e12 if big_s > 0 else 0.0
+        dtype = W[2]
+        peak = FP32_MFMA_PEAK_TFLOPS if dtype == 1 else FP64_MFMA_PEAK_TFLOPS
+        if dtype == 2:
+            # complex supernodes use the 64x64 tile kernel only (4 real MFMAs per
+            # complex multiply-add); its launches are the Schur launches
+            kname = "k_schur<zc> (64x64 complex fp64 MFMA GEMM + fused scatter)"
+            ker_ms, ker_flops = sst["t_schur_ms"], sst["schur_flops"]
+            launches = max(int(sst["n_schur_launches"]), 1)
+            tkey = "k_schur<zc>"
+        else:
+            tn = "double" if dtype == 0 else "float"
+            kname = f"k_schur_big<{tn}> (128x128 {W[7]} MFMA GEMM + fused scatter)"
+            ker_ms, ker_flops = sst["t_schur_big_ms"], sst["schur_big_flops"]
+            launches = max(int(sst["n_schur_big_launches"]), 1)
+            tkey = f"k_schur_big<{tn}>"
+        achieved = ker_flops / (ker_ms / 1e3) / 1e12 if ker_ms > 0 else 0.0
         roof = {"bound": "mfma", "achieved": round(achieved, 3),
-                "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(achieved / FP64_MFMA_PEAK_TFLOPS, 4),
-                "traffic": pmc_traffic(args.nx, pr, pc),
-                "kernel": "k_schur_big<double> (128x128 fp64 MFMA GEMM + fused scatter)",
+                "peak": peak, "unit": "TFLOP/s",
+                "frac": round(achieved / peak, 4),
+                "traffic": pmc_traffic(args.workload, args.nx, pr, pc, tkey),
+                "kernel": kname,
                 "launches_per_step": launches,
-                "flops_per_launch": sst["schur_big_flops"] / launches,
-                "avg_launch_ms": round(sst["t_schur_big_ms"] / launches, 4),
-                "timer": "HIP events around each k_schur_big launch, in one extra "
+                "flops_per_launch": ker_flops / launches,
+                "avg_launch_ms": round(ker_ms / launches, 4),
+                "timer": "HIP events around each launch of the kernel, in one extra "
                          "factorization with all launches on one stream (untimed for value)",
                 "serial_factor_ms": round(sst["t_total_ms"], 3),
                 "all_schur_tflops": round(st["schur_flops"] / (acc["t_schur_ms"] / 1e3 / K) / 1e12,
@@ -217,7 +263,7 @@ def main():
         if not args.no_cpu and world == 1:
             cpu = cpu_baseline(args.cpu_sample, args.cpu_ranks, timeout=600)
         out = {
-            "metric": "pdgstrf fp64 GFLOP/s + factor time, 3D Laplacian n~1M",
+            "metric": W[5],
             "value": round(flops_all / t_step / 1e9, 2),
             "unit": "GFLOP/s",
             "n_gpus": world,
@@ -227,10 +273,10 @@ def main():
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": "f64",
-            "data": "synthetic (generated 7-point stencil, diag 6 / off -1)",
-            "config": {"workload": f"3D 7-point Laplacian {args.nx}^3 (n={args.nx**3}), nested "
-                                   f"dissection, relax 60, maxsup 256",
+            "dtype": W[7],
+            "data": f"synthetic (generated {W[0]} stencil matrix, ||A||_1 = {anorm:g})",
+            "config": {"workload": f"{args.workload}: {W[0]} stencil {'x'.join(map(str, W[1](args.nx)))} "
+                                   f"(n={A.n}), nested dissection, relax 60, maxsup 256, {W[6]}",
                        "grid": f"{pr}x{pc}", "nsupers": int(S.nsupers),
                        "flops_per_factorization": flops_all,
                        "nnz_L": S.nnzL, "parallelism": f"2D block-cyclic {pr}x{pc}",
@@ -250,17 +296,17 @@ def main():
         dist.destroy_process_group()
 
 
-def pmc_traffic(nx, pr, pc):
-    """HBM bytes per k_schur_big launch from the committed rocprofv3 PMC passes
-    (profiles/traffic.json, written by tools/pmc_traffic.py: FETCH_SIZE x2
-    gfx950 correction + WRITE_SIZE) for this exact workload, else None."""
+def pmc_traffic(workload, nx, pr, pc, kernel):
+    """HBM bytes per launch of the roofline kernel from the committed
+    rocprofv3 PMC passes (profiles/traffic.json, written by
+    tools/pmc_traffic.py: FETCH_SIZE x2 gfx950 correction + WRITE_SIZE) for
+    this exact workload, else None."""
     f = os.path.join(ROOT, "profiles", "traffic.json")
     try:
         d = json.load(open(f))
     except (OSError, ValueError):
         return None
-    e = d.get(f"lap3d_{nx}_{pr}x{pc}", {}).get("k_schur_big<double>")
-    return e
+    return d.get(f"{workload}_{nx}_{pr}x{pc}", {}).get(kernel)
 
 
 if __name__ == "__main__":
