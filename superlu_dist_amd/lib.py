@@ -10,7 +10,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libslu_mi355x.so")
+# SLU_LIB overrides the in-tree library (A/B comparisons of engine builds)
+LIB_PATH = os.environ.get("SLU_LIB") or os.path.join(_HERE, "lib", "libslu_mi355x.so")
 
 SLU_D, SLU_S, SLU_Z = 0, 1, 2
 DTYPES = {SLU_D: np.float64, SLU_S: np.float32, SLU_Z: np.complex128}
