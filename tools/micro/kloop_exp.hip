@@ -92,13 +92,14 @@ template <int V> void run(const char *name, const double *A, const double *B, do
 }
 
 int main(int argc, char **argv) {
-    const int m = 8192, n = 8192, kw = argc > 1 ? atoi(argv[1]) : 256;
+    const int kw = argc > 1 ? atoi(argv[1]) : 256, m = argc > 2 ? atoi(argv[2]) : 8192, n = argc > 3 ? atoi(argv[3]) : 8192;
     std::vector<double> h((size_t)m * kw);
     for (size_t i = 0; i < h.size(); ++i) h[i] = (double)((i * 2654435761u) % 1000) / 1000.0 - 0.5;
     double *A, *B, *C;
     CK(hipMalloc(&A, (size_t)m * kw * 8)); CK(hipMalloc(&B, (size_t)n * kw * 8)); CK(hipMalloc(&C, (size_t)m * n * 8));
     CK(hipMemcpy(A, h.data(), (size_t)m * kw * 8, hipMemcpyHostToDevice));
     CK(hipMemcpy(B, h.data(), (size_t)n * kw * 8, hipMemcpyHostToDevice));
+    if (getenv("ONLY0")) { run<0>("full K loop", A, B, C, m, n, kw); return 0; }
     run<0>("full K loop", A, B, C, m, n, kw);
     run<1>("no LDS operand reads", A, B, C, m, n, kw);
     run<2>("no barrier", A, B, C, m, n, kw);
