@@ -710,22 +710,14 @@ k_diag_lu_f(const DiagItemF<T> *items, double thresh, int replace_tiny, int *tin
                     for (int k = 0; k < i; ++k) x[k] = Sx::fms(x[k], sP[k][i], x[i]);
                 }
 #pragma unroll
-                for (int i = 0; i < PW; ++i) {
-                    const T v = (i <= j && j < pw) ? x[i] : Sx::zero();
-                    sUi[i][j] = v;
-                    dinvU[(int64_t)p * PW * PW + i * PW + j] = v;
-                }
+                for (int i = 0; i < PW; ++i) sUi[i][j] = (i <= j && j < pw) ? x[i] : Sx::zero();
             } else { // L11 x = e_j (unit lower)
 #pragma unroll
                 for (int i = 0; i < PW; ++i)
 #pragma unroll
                     for (int k = i + 1; k < PW; ++k) x[k] = Sx::fms(x[k], sP[k][i], x[i]);
 #pragma unroll
-                for (int i = 0; i < PW; ++i) {
-                    const T v = (i >= j && i < pw && j < pw) ? x[i] : Sx::zero();
-                    sLi[i][j] = v;
-                    dinvLT[(int64_t)p * PW * PW + j * PW + i] = v;
-                }
+                for (int i = 0; i < PW; ++i) sLi[i][j] = (i >= j && i < pw && j < pw) ? x[i] : Sx::zero();
             }
         }
         __syncthreads();
@@ -792,7 +784,14 @@ k_diag_lu_f(const DiagItemF<T> *items, double thresh, int replace_tiny, int *tin
             }
         }
         __syncthreads();
-        // ---- 3. panel and U12 back to global; A22 -= L21 U12 on MFMA
+        // ---- 3. panel, U12 and the dinv blocks back to global (written here
+        // so that no barrier before the trailing update waits for them);
+        // A22 -= L21 U12 on MFMA
+        for (int e = tid; e < PW * PW; e += DF_THREADS) {
+            const int i = e / PW, jj = e % PW;
+            dinvU[(int64_t)p * PW * PW + e] = sUi[i][jj];  // row-major U11^{-1}
+            dinvLT[(int64_t)p * PW * PW + e] = sLi[jj][i]; // row-major (L11^{-1})^T
+        }
         for (int e = tid; e < nrow * pw; e += DF_THREADS) {
             const int r = e % nrow, c = e / nrow;
             A11[r + (int64_t)c * ld] = sP[r][c];
