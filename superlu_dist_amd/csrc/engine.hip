@@ -1264,6 +1264,7 @@ struct Plan : PlanBase {
             if (timing) spans.push_back({a, mark_on(st), kind, cur_level});
         };
         int e_start = timing ? mark() : -1;
+        vector<int> lvl_end;
         HIPCHK(hipEventRecord(ev_start, stream));
         HIPCHK(hipStreamWaitEvent(pstream, ev_start, 0));
         X.s = opts.serial ? stream : pstream;
@@ -1343,6 +1344,7 @@ struct Plan : PlanBase {
                 stats.n_schur_launches++;
             }
             HIPCHK(hipEventRecord(ev_rest[L], stream));
+            if (opts.timing >= 2) lvl_end.push_back(mark_on(stream)); // level wall time
         }
         HIPCHK(hipEventRecord(ev_pend, pstream));
         HIPCHK(hipStreamWaitEvent(stream, ev_pend, 0));
@@ -1392,14 +1394,16 @@ struct Plan : PlanBase {
                     HIPCHK(hipEventElapsedTime(&ms, ev[s.a], ev[s.b]));
                     t[s.level][s.kind] += ms;
                 }
-                fprintf(stderr, "[slu rank %d] lvl nsup diag trsm big small atomic  GFLOP  diag_ms trsm_ms big_ms small_ms comm_ms  TF/s\n", iam);
+                fprintf(stderr, "[slu rank %d] lvl nsup diag trsm big small atomic  GFLOP  diag_ms trsm_ms big_ms small_ms comm_ms  TF/s wall_ms\n", iam);
                 for (size_t L = 0; L < levels.size(); ++L) {
                     const LevelRange &R = levels[L];
                     double sch = t[L][2] + t[L][3];
-                    fprintf(stderr, "[slu rank %d] %3zu %5zu %4d %5d %5d %5d %6d %7.2f %8.3f %7.3f %7.3f %7.3f %7.3f %6.2f\n",
+                    float wall = 0;
+                    HIPCHK(hipEventElapsedTime(&wall, ev[L ? lvl_end[L - 1] : e_start], ev[lvl_end[L]]));
+                    fprintf(stderr, "[slu rank %d] %3zu %5zu %4d %5d %5d %5d %6d %7.2f %8.3f %7.3f %7.3f %7.3f %7.3f %6.2f %7.3f\n",
                             iam, L, bylev[L].size(), R.diag_n + R.df_n, R.lf_n + R.uf_n + R.tl_n + R.tu_n,
                             R.big_n, R.tile_n, R.atomic_tiles, R.schur_flops / 1e9, t[L][0], t[L][1], t[L][2], t[L][3],
-                            t[L][4], sch > 0 ? R.schur_flops / sch / 1e9 : 0.0);
+                            t[L][4], sch > 0 ? R.schur_flops / sch / 1e9 : 0.0, (double)wall);
                 }
             }
             for (auto e : ev) (void)hipEventDestroy(e);
