@@ -148,6 +148,12 @@ int slu_plan_set_timing(slu_plan *p, int timing, int serial);
 int slu_plan_sync(slu_plan *p);
 /* Copy factors back into the host LUstruct arrays. */
 int slu_plan_download(slu_plan *p);
+/* Solve L U x = b with the device-resident factors of the last
+ * slu_plan_factor (1x1 grid; SURVEY 8(f) row 2, the supernodal solve of
+ * SRC/pdgstrs.c in the LUstruct's permuted coordinates).  b: host array of
+ * nrhs columns of n values (ld ldb, element type of the plan), overwritten
+ * with x.  t_solve_ms in the stats is the device time of the last call. */
+int slu_plan_solve(slu_plan *p, void *b, int64_t ldb, int nrhs);
 void slu_plan_destroy(slu_plan *p);
 
 /* Plan statistics (algorithmic work of one factorization on this rank). */
@@ -167,11 +173,15 @@ typedef struct {
     int64_t n_schur_launches;
     int64_t n_schur_big_launches;
     double comm_bytes;         /* bytes this rank sends + receives per factor */
+    double t_solve_ms;         /* device time of the last slu_plan_solve */
 } slu_plan_stats;
 int slu_plan_get_stats(const slu_plan *p, slu_plan_stats *st);
 
 /* Last error string of this thread (empty when none). */
 const char *slu_last_error(void);
+/* Test hook: fill the LDS of every CU of `device` with NaN, so that a
+ * kernel reading LDS it did not write fails deterministically. */
+int slu_debug_poison_lds(int device);
 
 /* ---------------- 3. front-end helpers ---------------- */
 

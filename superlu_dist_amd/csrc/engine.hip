@@ -37,6 +37,7 @@
 
 #include "common.h"
 #include "kernels.h"
+#include "solve.h"
 #include "slu_mi355x.h"
 
 using std::vector;
@@ -206,6 +207,7 @@ struct PlanBase {
     virtual void restore() = 0;
     virtual void sync() = 0;
     virtual void set_timing(int timing, int serial) = 0;
+    virtual void solve(void *b, int64_t ldb, int nrhs) = 0;
     slu_plan_stats stats{};
 };
 
@@ -1409,6 +1411,124 @@ struct Plan : PlanBase {
             for (auto e : ev) (void)hipEventDestroy(e);
         }
     }
+
+    // ------------------------------------------------------- device solve
+    // (1x1; solve.h).  Tables are built on the first call and kept.
+    bool sv_ready = false;
+    vector<int> sv_d_off, sv_l_off, sv_u_off; // per level: diag items, L chunks, U chunks
+    DevBuf<SvDiag> d_sv_diag, d_sv_lvl;       // per supernode / in level order
+    DevBuf<SvChunk> d_sv_lch, d_sv_uch;
+    DevBuf<i64> d_sv_roff, d_sv_coff;
+    DevBuf<int> d_sv_rows, d_sv_ncol, d_sv_gc;
+    DevBuf<T> d_sv_x;
+
+    void build_solve() {
+        SLU_REQUIRE(!xmode, "the device solve is implemented for 1x1 grids");
+        vector<SvDiag> dg(nsupers), lvl;
+        vector<i64> roff(nsupers), coff(nsupers, 0);
+        vector<int> rows, ncol(nsupers, 0), gc;
+        for (int k = 0; k < nsupers; ++k) {
+            SLU_REQUIRE(lval_off[k] >= 0, "supernode %d has no L column block", k);
+            SvDiag d{};
+            d.voff = lval_off[k];
+            d.ld = lval_ld[k];
+            d.w = W(k);
+            d.fst = (int)xsup[k];
+            dg[k] = d;
+            roff[k] = (i64)rows.size();
+            const int_t *ix = lidx[k];
+            i64 p = SLU_BC_HEADER;
+            for (i64 b = 0; b < ix[0]; ++b) {
+                const int gb = (int)ix[p], nr = (int)ix[p + 1];
+                if (gb != k)
+                    for (int i = 0; i < nr; ++i) rows.push_back((int)ix[p + 2 + i]);
+                p += SLU_LB_DESCRIPTOR + nr;
+            }
+            SLU_REQUIRE((i64)rows.size() - roff[k] == d.ld - d.w, "supernode %d: panel rows", k);
+            if (uval_off[k] >= 0 && urow_nblk[k] > 0) {
+                coff[k] = ublk[urow_first[k]].coloff;
+                for (int b = urow_first[k]; b < urow_first[k] + urow_nblk[k]; ++b) ncol[k] += W(ublk_jb[b]);
+            }
+        }
+        gc.resize(ucol_voff.size());
+        for (size_t b = 0; b < ublk.size(); ++b)
+            for (int c = 0; c < W(ublk_jb[b]); ++c) gc[ublk[b].coloff + c] = ublk[b].fcol + c;
+        vector<SvChunk> lch, uch;
+        const int nl = (int)bylev.size();
+        sv_d_off.assign(nl + 1, 0);
+        sv_l_off.assign(nl + 1, 0);
+        sv_u_off.assign(nl + 1, 0);
+        for (int L = 0; L < nl; ++L) {
+            sv_d_off[L] = (int)lvl.size();
+            sv_l_off[L] = (int)lch.size();
+            sv_u_off[L] = (int)uch.size();
+            for (int k : bylev[L]) {
+                lvl.push_back(dg[k]);
+                for (int r0 = 0; r0 < dg[k].ld - dg[k].w; r0 += SV_THREADS) lch.push_back({k, r0});
+                for (int c0 = 0; c0 < ncol[k]; c0 += SV_THREADS) uch.push_back({k, c0});
+            }
+        }
+        sv_d_off[nl] = (int)lvl.size();
+        sv_l_off[nl] = (int)lch.size();
+        sv_u_off[nl] = (int)uch.size();
+        d_sv_diag.upload(dg);
+        d_sv_lvl.upload(lvl);
+        d_sv_lch.upload(lch);
+        d_sv_uch.upload(uch);
+        d_sv_roff.upload(roff);
+        d_sv_coff.upload(coff);
+        d_sv_rows.upload(rows.empty() ? vector<int>(1, 0) : rows);
+        d_sv_ncol.upload(ncol);
+        d_sv_gc.upload(gc.empty() ? vector<int>(1, 0) : gc);
+        d_sv_x.alloc(std::max(n, 1));
+        sv_ready = true;
+    }
+
+    void solve(void *b, int64_t ldb, int nrhs) override {
+        if (!sv_ready) build_solve();
+        SLU_REQUIRE(ldb >= n && nrhs >= 0, "solve: ldb %lld < n %d", (long long)ldb, n);
+        hipEvent_t e0, e1;
+        HIPCHK(hipEventCreate(&e0));
+        HIPCHK(hipEventCreate(&e1));
+        float total = 0;
+        const int nl = (int)bylev.size();
+        for (int r = 0; r < nrhs; ++r) {
+            HT *hb = (HT *)b + (i64)r * ldb;
+            HIPCHK(hipMemcpyAsync(d_sv_x.p, hb, (size_t)n * sizeof(T), hipMemcpyHostToDevice, stream));
+            HIPCHK(hipEventRecord(e0, stream));
+            for (int L = 0; L < nl; ++L) { // L y = b
+                const int nd = sv_d_off[L + 1] - sv_d_off[L], nc = sv_l_off[L + 1] - sv_l_off[L];
+                if (nd)
+                    hipLaunchKernelGGL(k_sv_ldiag<T>, dim3(nd), dim3(SVD_THREADS), 0, stream,
+                                       d_sv_lvl.p + sv_d_off[L], d_L.p, d_sv_x.p);
+                if (nc)
+                    hipLaunchKernelGGL(k_sv_lpanel<T>, dim3(nc), dim3(SV_THREADS), 0, stream,
+                                       d_sv_lch.p + sv_l_off[L], d_sv_diag.p, d_sv_roff.p,
+                                       d_sv_rows.p, d_L.p, d_sv_x.p);
+            }
+            for (int L = nl - 1; L >= 0; --L) { // U x = y
+                const int nd = sv_d_off[L + 1] - sv_d_off[L], nc = sv_u_off[L + 1] - sv_u_off[L];
+                if (nc)
+                    hipLaunchKernelGGL(k_sv_upanel<T>, dim3(nc), dim3(SV_THREADS), 0, stream,
+                                       d_sv_uch.p + sv_u_off[L], d_sv_diag.p, d_sv_coff.p,
+                                       d_sv_ncol.p, d_ucol_voff.p, d_ucol_fst.p, d_sv_gc.p,
+                                       d_U.p, d_sv_x.p);
+                if (nd)
+                    hipLaunchKernelGGL(k_sv_udiag<T>, dim3(nd), dim3(SVD_THREADS), 0, stream,
+                                       d_sv_lvl.p + sv_d_off[L], d_L.p, d_sv_x.p);
+            }
+            HIPCHK(hipGetLastError());
+            HIPCHK(hipEventRecord(e1, stream));
+            HIPCHK(hipMemcpyAsync(hb, d_sv_x.p, (size_t)n * sizeof(T), hipMemcpyDeviceToHost, stream));
+            HIPCHK(hipStreamSynchronize(stream));
+            float ms = 0;
+            HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+            total += ms;
+        }
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+        stats.t_solve_ms = total;
+    }
 };
 
 template <typename P> PlanBase *make_plan(void *LU, int n, int pr, int pc, int iam, slu_comm *c,
@@ -1425,7 +1545,39 @@ struct slu_plan {
 
 using namespace slu;
 
+// Fills the whole LDS of every CU with NaN (test hook: a kernel that reads
+// LDS it did not write, even to multiply it by zero, then fails every time
+// instead of depending on what the previous kernel left there).
+__global__ void __launch_bounds__(1024) k_poison_lds(double v, int bytes) {
+    extern __shared__ double s_poison[];
+    const int n = bytes / (int)sizeof(double);
+    for (int i = threadIdx.x; i < n; i += blockDim.x) s_poison[i] = v;
+    __syncthreads();
+    if (s_poison[(threadIdx.x * 7) % n] != s_poison[(threadIdx.x * 7) % n] && threadIdx.x == 1u << 30)
+        s_poison[0] = 0; // never true; keeps the stores
+}
+
 extern "C" {
+
+int slu_debug_poison_lds(int device) {
+    try {
+        HIPCHK(hipSetDevice(device));
+        // the whole 160 KB per workgroup where the runtime allows it, else 64 KB
+        int bytes = 160 * 1024;
+        if (hipFuncSetAttribute((const void *)k_poison_lds,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, bytes) != hipSuccess) {
+            (void)hipGetLastError();
+            bytes = 64 * 1024;
+        }
+        hipLaunchKernelGGL(k_poison_lds, dim3(4096), dim3(1024), bytes, 0, __builtin_nan(""), bytes);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipDeviceSynchronize());
+        return 0;
+    } catch (const std::exception &e) {
+        set_last_error(e.what());
+        return -1;
+    }
+}
 
 const char *slu_last_error(void) { return g_last_error.c_str(); }
 
@@ -1537,6 +1689,16 @@ int slu_plan_factor(slu_plan *p, double anorm, int *info, int *tiny) {
         p->impl->factor(anorm, &i, &t);
         if (info) *info = i;
         if (tiny) *tiny = t;
+        return 0;
+    } catch (const std::exception &e) {
+        set_last_error(e.what());
+        return -1;
+    }
+}
+
+int slu_plan_solve(slu_plan *p, void *b, int64_t ldb, int nrhs) {
+    try {
+        p->impl->solve(b, ldb, nrhs);
         return 0;
     } catch (const std::exception &e) {
         set_last_error(e.what());

@@ -627,10 +627,14 @@ k_diag_lu_f(const DiagItemF<T> *items, double thresh, int replace_tiny, int *tin
         const int c0 = p0 + pw;
         T *A11 = A + p0 + (int64_t)p0 * ld;
 
-        // ---- 0. stage the panel and U12 (zero outside pw)
-        for (int e = tid; e < nrow * PW; e += DF_THREADS) {
-            const int r = e % nrow, c = e / nrow;
-            sP[r][c] = c < pw ? A11[r + (int64_t)c * ld] : Sx::zero();
+        // ---- 0. stage the panel and U12 (zero outside pw; a last panel with
+        // nrow < PW zero-fills rows nrow..PW-1, which the inverse sweeps in
+        // 1b multiply by zero: stale LDS there could be NaN, and 0 * NaN
+        // would reach the stored U11^{-1})
+        const int nrs = max(nrow, PW);
+        for (int e = tid; e < nrs * PW; e += DF_THREADS) {
+            const int r = e % nrs, c = e / nrs;
+            sP[r][c] = (c < pw && r < nrow) ? A11[r + (int64_t)c * ld] : Sx::zero();
         }
         for (int e = tid; e < nbl * PW; e += DF_THREADS) {
             const int i = e % PW, c = e / PW;

@@ -115,6 +115,16 @@ class Plan:
     def download(self):
         self._chk(lib().slu_plan_download(self.ptr))
 
+    def solve(self, b):
+        """Solve L U x = b with the device-resident factors (1x1 grid, the
+        LUstruct's permuted coordinates); b: (n,) or (n, nrhs).  Returns x."""
+        dt = self.lu.Lval.dtype
+        x = np.array(b, dtype=dt, order="F", copy=True)
+        nrhs = 1 if x.ndim == 1 else x.shape[1]
+        n = x.shape[0]
+        self._chk(lib().slu_plan_solve(self.ptr, x.ctypes.data_as(C.c_void_p), n, nrhs))
+        return x
+
     def stats(self):
         st = PlanStats()
         lib().slu_plan_get_stats(self.ptr, C.byref(st))

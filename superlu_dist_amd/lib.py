@@ -56,7 +56,8 @@ class PlanStats(C.Structure):
                 ("t_trsm_ms", C.c_double), ("t_schur_ms", C.c_double),
                 ("t_comm_ms", C.c_double), ("t_schur_big_ms", C.c_double),
                 ("schur_big_flops", C.c_double), ("n_schur_launches", C.c_int64),
-                ("n_schur_big_launches", C.c_int64), ("comm_bytes", C.c_double)]
+                ("n_schur_big_launches", C.c_int64), ("comm_bytes", C.c_double),
+                ("t_solve_ms", C.c_double)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -100,6 +101,7 @@ def lib():
         "slu_plan_upload": (C.c_int, [P]),
         "slu_plan_factor": (C.c_int, [P, C.c_double, c_intp, c_intp]),
         "slu_plan_download": (C.c_int, [P]),
+        "slu_plan_solve": (C.c_int, [P, P, C.c_int64, C.c_int]),
         "slu_plan_snapshot": (C.c_int, [P]),
         "slu_plan_restore": (C.c_int, [P]),
         "slu_plan_sync": (C.c_int, [P]),
@@ -107,6 +109,7 @@ def lib():
         "slu_plan_destroy": (None, [P]),
         "slu_plan_get_stats": (C.c_int, [P, C.POINTER(PlanStats)]),
         "slu_last_error": (C.c_char_p, []),
+        "slu_debug_poison_lds": (C.c_int, [C.c_int]),
     }
     for name, (res, args) in sig.items():
         if not hasattr(L, name):

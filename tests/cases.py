@@ -116,6 +116,8 @@ def factor_error(lus, ref):
         for mine, r in ((lu.Lval, Lr), (lu.Uval, Ur)):
             if len(r) == 0:
                 continue
+            if not np.isfinite(mine).all():
+                return float("inf")  # max() below would drop a NaN
             d = np.abs(mine.astype(np.complex128) - r.astype(np.complex128)).max()
             worst = max(worst, d / max(np.abs(r).max(), 1e-300))
     return worst

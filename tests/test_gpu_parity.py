@@ -100,3 +100,31 @@ def test_gpu_refactor_same_plan_is_reproducible_without_atomics():
         outs.append((lu.Lval.copy(), lu.Uval.copy()))
     assert np.allclose(outs[0][0], outs[1][0], rtol=0, atol=1e-13)
     assert np.allclose(outs[0][1], outs[1][1], rtol=0, atol=1e-13)
+
+
+@pytest.mark.parametrize("kind,dims,dtype", [
+    (STENCIL_3D7, (10, 10, 10), 0),
+    (STENCIL_3D7, (10, 10, 10), 1),
+    (STENCIL_3D27, (10, 10, 10), 1),
+    (STENCIL_3D7, (8, 8, 8), 2),
+    (STENCIL_2D5, (30, 30, 1), 1),
+])
+def test_gpu_factors_finite_with_poisoned_lds(kind, dims, dtype):
+    """Every kernel must only read LDS it wrote: with the LDS of every CU
+    filled with NaN before the factorization, the factors still match the
+    oracle (a stale-LDS read, even one multiplied by zero, gives NaN)."""
+    from superlu_dist_amd.lib import lib
+    kw = dict(diag=6 - 0.25, diag_im=-0.0025) if dtype == 2 else {}
+    A = Csc.stencil(kind, *dims, dtype=dtype, **kw)
+    S = Symbolic(A, nd_order(*dims), 60, 256)
+    gpu, ref = S.distribute(), S.distribute()
+    an = cases.anorm(A)
+    p = Plan(gpu)
+    p.upload()
+    assert lib().slu_debug_poison_lds(0) == 0
+    assert p.factor(an) == (0, 0)
+    p.download()
+    assert np.isfinite(gpu.Lval).all() and np.isfinite(gpu.Uval).all()
+    pyoracle.oracle_factor([ref], 1, 1, A.n, False, an)
+    err = cases.factor_error([gpu], [(ref.Lval, ref.Uval)])
+    assert err < TOL[dtype], err
