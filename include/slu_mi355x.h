@@ -154,6 +154,20 @@ int slu_plan_download(slu_plan *p);
  * nrhs columns of n values (ld ldb, element type of the plan), overwritten
  * with x.  t_solve_ms in the stats is the device time of the last call. */
 int slu_plan_solve(slu_plan *p, void *b, int64_t ldb, int nrhs);
+/* Device-side refill of the factor storage from new values of A with the
+ * same pattern (replaces the options->Fact ==
+ * SamePattern_SameRowPerm branch of pddistribute, SRC/pddistribute.c:545-672).
+ * set_a_pattern: A in the LUstruct's permuted coordinates (what
+ * dReDistribute_A hands pddistribute, SRC/pddistribute.c:536), CSC with
+ * column pointers xa[ncol+1] and row indices asub[xa[ncol]]; entries of
+ * other process rows / columns are ignored, so every rank may pass the
+ * whole matrix.  Fails (-1) if an entry lies outside the L/U structure.
+ * fill_a: zero this rank's L and U values and store a[e] (nnz values of the
+ * plan's element type, host pointer or, with on_device = 1, device pointer)
+ * at their positions; a duplicated (row, column) keeps the last value.
+ * t_fill_ms in the stats is the device time of the zero + scatter. */
+int slu_plan_set_a_pattern(slu_plan *p, int64_t ncol, const int64_t *xa, const int64_t *asub);
+int slu_plan_fill_a(slu_plan *p, const void *a, int on_device);
 void slu_plan_destroy(slu_plan *p);
 
 /* Plan statistics (algorithmic work of one factorization on this rank). */
@@ -174,6 +188,7 @@ typedef struct {
     int64_t n_schur_big_launches;
     double comm_bytes;         /* bytes this rank sends + receives per factor */
     double t_solve_ms;         /* device time of the last slu_plan_solve */
+    double t_fill_ms;          /* device time of the last slu_plan_fill_a */
 } slu_plan_stats;
 int slu_plan_get_stats(const slu_plan *p, slu_plan_stats *st);
 

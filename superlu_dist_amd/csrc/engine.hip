@@ -37,6 +37,7 @@
 
 #include "common.h"
 #include "kernels.h"
+#include "fill.h"
 #include "solve.h"
 #include "slu_mi355x.h"
 
@@ -208,6 +209,8 @@ struct PlanBase {
     virtual void sync() = 0;
     virtual void set_timing(int timing, int serial) = 0;
     virtual void solve(void *b, int64_t ldb, int nrhs) = 0;
+    virtual void set_a_pattern(int64_t ncol, const int64_t *xa, const int64_t *asub) = 0;
+    virtual void fill_a(const void *a, int on_device) = 0;
     slu_plan_stats stats{};
 };
 
@@ -1529,6 +1532,91 @@ struct Plan : PlanBase {
         (void)hipEventDestroy(e1);
         stats.t_solve_ms = total;
     }
+
+    // ------------------------------------------------------- values of A
+    // SamePattern_SameRowPerm refill (SRC/pddistribute.c:545-672) on the
+    // device: the destination of every nonzero of A in this rank's L/U
+    // storage is resolved once per pattern, with the reference's rules --
+    // row block gb < column block jb goes to U(gb,jb) at the segment offset of
+    // column j (:598-618), otherwise to L(:,jb) at the row's position in the
+    // block column (:619-656); entries of other process rows / columns are
+    // skipped (:587,596).
+    DevBuf<i64> d_amap;
+    DevBuf<T> d_aval;
+    i64 a_nnz = -1;
+
+    void set_a_pattern(int64_t ncol, const int64_t *xa, const int64_t *asub) override {
+        SLU_REQUIRE(ncol == n, "A has %lld columns, the LU structure %d", (long long)ncol, n);
+        SLU_REQUIRE(xa[0] == 0 && xa[n] >= 0, "A: bad column pointers");
+        const int_t *supno = LU->Glu_persist->supno;
+        const i64 nnz = xa[n];
+        vector<i64> map((size_t)nnz, -1);
+        vector<std::pair<i64, i64>> col; // (destination, nonzero) of one column
+        for (int j = 0; j < n; ++j) {
+            const int jb = (int)supno[j];
+            SLU_REQUIRE(xa[j + 1] >= xa[j], "A: column pointers decrease at %d", j);
+            if (jb % Pc != mycol) continue;
+            const int jc = (int)(j - xsup[jb]);
+            col.clear();
+            for (i64 e = xa[j]; e < xa[j + 1]; ++e) {
+                const i64 irow = asub[e];
+                SLU_REQUIRE(irow >= 0 && irow < n, "A(%lld,%d): row out of range", (long long)irow, j);
+                const int gb = (int)supno[irow];
+                if (gb % Pr != myrow) continue;
+                i64 m;
+                if (gb < jb) {
+                    const UBlk &B = ublk[find_ublk(gb, jb)];
+                    const i64 c = B.coloff + jc;
+                    SLU_REQUIRE(irow >= ucol_fst[c], "A(%lld,%d) is outside the U structure",
+                                (long long)irow, j);
+                    m = 2 * (ucol_voff[c] + irow - ucol_fst[c]) + 1;
+                } else {
+                    const LBlk &B = lblk[find_lblk(gb, jb)];
+                    const int pos = lmap[B.mapoff + irow - xsup[gb]];
+                    SLU_REQUIRE(pos >= 0, "A(%lld,%d) is outside the L structure", (long long)irow, j);
+                    m = 2 * (B.colvoff + (i64)jc * B.ld + pos);
+                }
+                col.push_back({m, e});
+            }
+            // a duplicated (row, column): the later entry wins, as in the SPA
+            std::sort(col.begin(), col.end());
+            for (size_t i = 0; i < col.size(); ++i)
+                if (i + 1 == col.size() || col[i + 1].first != col[i].first)
+                    map[col[i].second] = col[i].first;
+        }
+        d_amap.upload(map.empty() ? vector<i64>(1, -1) : map);
+        d_aval.alloc(std::max<i64>(nnz, 1));
+        a_nnz = nnz;
+    }
+
+    void fill_a(const void *a, int on_device) override {
+        SLU_REQUIRE(a_nnz >= 0, "fill_a before set_a_pattern");
+        const T *src = (const T *)a;
+        if (!on_device && a_nnz) {
+            HIPCHK(hipMemcpyAsync(d_aval.p, a, (size_t)a_nnz * sizeof(T), hipMemcpyHostToDevice, stream));
+            src = d_aval.p;
+        }
+        hipEvent_t e0, e1;
+        HIPCHK(hipEventCreate(&e0));
+        HIPCHK(hipEventCreate(&e1));
+        HIPCHK(hipStreamSynchronize(pstream));
+        HIPCHK(hipEventRecord(e0, stream));
+        if (d_L.n) HIPCHK(hipMemsetAsync(d_L.p, 0, d_L.bytes(), stream));
+        if (d_U.n) HIPCHK(hipMemsetAsync(d_U.p, 0, d_U.bytes(), stream));
+        if (a_nnz) {
+            const i64 blocks = std::min<i64>((a_nnz + FILL_THREADS - 1) / FILL_THREADS, 65536);
+            hipLaunchKernelGGL(k_fill_a<T>, dim3((unsigned)blocks), dim3(FILL_THREADS), 0, stream,
+                               d_amap.p, src, a_nnz, d_L.p, d_U.p);
+            HIPCHK(hipGetLastError());
+        }
+        HIPCHK(hipEventRecord(e1, stream));
+        HIPCHK(hipStreamSynchronize(stream));
+        float ms = 0;
+        HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+        stats.t_fill_ms = ms;
+    }
 };
 
 template <typename P> PlanBase *make_plan(void *LU, int n, int pr, int pc, int iam, slu_comm *c,
@@ -1699,6 +1787,26 @@ int slu_plan_factor(slu_plan *p, double anorm, int *info, int *tiny) {
 int slu_plan_solve(slu_plan *p, void *b, int64_t ldb, int nrhs) {
     try {
         p->impl->solve(b, ldb, nrhs);
+        return 0;
+    } catch (const std::exception &e) {
+        set_last_error(e.what());
+        return -1;
+    }
+}
+
+int slu_plan_set_a_pattern(slu_plan *p, int64_t ncol, const int64_t *xa, const int64_t *asub) {
+    try {
+        p->impl->set_a_pattern(ncol, xa, asub);
+        return 0;
+    } catch (const std::exception &e) {
+        set_last_error(e.what());
+        return -1;
+    }
+}
+
+int slu_plan_fill_a(slu_plan *p, const void *a, int on_device) {
+    try {
+        p->impl->fill_a(a, on_device);
         return 0;
     } catch (const std::exception &e) {
         set_last_error(e.what());

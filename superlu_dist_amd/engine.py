@@ -10,7 +10,7 @@ import ctypes as C
 
 import numpy as np
 
-from .lib import HOST_BCAST_FN, EngineOpts, PlanStats, lib
+from .lib import HOST_BCAST_FN, EngineOpts, PlanStats, as_i64p, lib
 
 SMACH_EPS = 5.9604644775390625e-08  # smach_dist("Epsilon"), SRC/smach_dist.c:64
 
@@ -124,6 +124,21 @@ class Plan:
         n = x.shape[0]
         self._chk(lib().slu_plan_solve(self.ptr, x.ctypes.data_as(C.c_void_p), n, nrhs))
         return x
+
+    def set_a_pattern(self, colptr, rowind):
+        """Pattern of A in the LUstruct's permuted coordinates (CSC)."""
+        self._xa = np.ascontiguousarray(colptr, dtype=np.int64)
+        self._asub = np.ascontiguousarray(rowind, dtype=np.int64)
+        self._chk(lib().slu_plan_set_a_pattern(self.ptr, len(self._xa) - 1,
+                                               as_i64p(self._xa), as_i64p(self._asub)))
+
+    def fill_a(self, values):
+        """Refill the device factor storage from A's values (host array in the
+        order of the pattern), SamePattern_SameRowPerm; no LU upload."""
+        v = np.ascontiguousarray(values, dtype=self.lu.Lval.dtype)
+        if len(v) != len(self._asub):
+            raise ValueError(f"{len(v)} values for a pattern of {len(self._asub)} nonzeros")
+        self._chk(lib().slu_plan_fill_a(self.ptr, v.ctypes.data_as(C.c_void_p), 0))
 
     def stats(self):
         st = PlanStats()

@@ -49,7 +49,7 @@ class GlooGrid:
         self.dist.broadcast(t, src=self.global_root(group, root), group=g)
 
 
-def _worker(rank, world, port, recipe, out_dir, device):
+def _worker(rank, world, port, recipe, out_dir, device, fill=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     try:
         import torch.distributed as dist
@@ -65,7 +65,12 @@ def _worker(rank, world, port, recipe, out_dir, device):
         if device is not None:
             comm = Comm.host(pr, pc, rank, device, gg.bcast)
             p = Plan(lu, comm=comm, replace_tiny=tiny)
-            p.upload()
+            if fill:  # values from A on the device (no LU upload), SamePattern refill
+                cp, ri, v = A.permuted(S.perm_c).arrays()
+                p.set_a_pattern(cp, ri)
+                p.fill_a(v)
+            else:
+                p.upload()
             info, ntiny = p.factor(cases.anorm(A))
             p.download()
             st = p.stats()
@@ -89,7 +94,7 @@ def _worker(rank, world, port, recipe, out_dir, device):
         raise
 
 
-def run_grid(recipe, pr, pc, out_dir, device=0, timeout=240):
+def run_grid(recipe, pr, pc, out_dir, device=0, timeout=240, fill=False):
     """Run ``recipe`` (picklable callable returning cases.build()-style
     tuples) on a pr x pc grid; returns the per-rank result dicts.
 
@@ -100,7 +105,7 @@ def run_grid(recipe, pr, pc, out_dir, device=0, timeout=240):
     ctx = mp.get_context("spawn")
     world = pr * pc
     port = free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, recipe, str(out_dir), device))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, recipe, str(out_dir), device, fill))
              for r in range(world)]
     for p in procs:
         p.start()

@@ -33,11 +33,14 @@ def test_gloo_grid_groups_cpu(tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", GRID_CASES)
-def test_grid_matches_reference_fixture(name, tmp_path):
+@pytest.mark.parametrize("name,fill", [(n, False) for n in GRID_CASES] +
+                         [("lap3d_10_2x4_small_d", True), ("cg20_2x2_small_z", True)])
+def test_grid_matches_reference_fixture(name, fill, tmp_path):
+    """fill: every rank loads its values from A on the device (slu_plan_fill_a,
+    the SamePattern_SameRowPerm refill) instead of uploading its LUstruct."""
     meta, ref = load_golden(name)
     pr, pc = meta["grid"]
-    out = run_grid(functools.partial(cases.build, name), pr, pc, tmp_path, device=0)
+    out = run_grid(functools.partial(cases.build, name), pr, pc, tmp_path, device=0, fill=fill)
     assert all(int(o["info"]) == meta["ref_info"] for o in out)
     assert sum(int(o["tiny"]) for o in out) == meta["ref_tiny"]
     worst = 0.0
