@@ -66,6 +66,43 @@ def build_lu(workload, nx, pr, pc, myrow, mycol):
     return A, S, lu
 
 
+def next_rows(plan, A, S, anorm, one_step):
+    """SURVEY 8(f) rows 1-2 on the same workload, untimed for value:
+    device refill of the factor storage from A (SamePattern_SameRowPerm,
+    instead of the PCIe upload of L and U) and the triangular solve on the
+    device-resident factors, with the solve's backward error."""
+    import scipy.sparse as sp
+    cp, ri, v = A.permuted(S.perm_c).arrays()
+    t0 = time.time()
+    plan.set_a_pattern(cp, ri)
+    t_pat = time.time() - t0
+    fills = []
+    for _ in range(3):
+        plan.fill_a(v)
+        fills.append(plan.stats()["t_fill_ms"])
+    st = plan.stats()
+    lu_bytes = st["lu_bytes"]
+    info, _ = plan.factor(anorm)
+    plan.sync()
+    B = sp.csc_matrix((v, ri, cp), shape=(A.n, A.n))
+    xt = np.random.default_rng(1).standard_normal(A.n).astype(v.dtype)
+    b = B @ xt
+    solves = []
+    for _ in range(3):
+        x = plan.solve(b)
+        solves.append(plan.stats()["t_solve_ms"])
+    r = B @ x - b
+    berr = float(np.abs(r).max() / (abs(B).sum(axis=1).max() * np.abs(x).max()))
+    fill_ms = min(fills)
+    return {"fill": {"kernel": "memset L/U + k_fill_a (nnz(A) scatter)",
+                     "device_ms": round(fill_ms, 3),
+                     "hbm_gbps": round((lu_bytes + len(v) * (8 + v.itemsize * 2)) / fill_ms / 1e6, 1),
+                     "pattern_setup_s": round(t_pat, 3), "nnz_A": int(len(v)),
+                     "lu_bytes": lu_bytes, "factor_info_after_fill": int(info)},
+            "solve": {"device_ms": round(min(solves), 3), "nrhs": 1, "berr": berr,
+                      "fwd_err": float(np.abs(x - xt).max() / np.abs(xt).max())}}
+
+
 def one_norm(A):
     """||A||_1 (max column sum of |a_ij|), the anorm pdgssvx passes to pdgstrf."""
     colptr, _, val = A.arrays()
@@ -110,6 +147,8 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=80)
     ap.add_argument("--cpu-ranks", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-next", action="store_true",
+                    help="skip the device fill / solve measurements (SURVEY 8(f) rows 1-2)")
     ap.add_argument("--level-log", action="store_true",
                     help="per-level phase breakdown of the last step on stderr")
     ap.add_argument("--roofline-only", action="store_true",
@@ -211,6 +250,9 @@ def main():
     sst = plan.stats()
     plan.set_timing(2 if args.level_log else 1, serial=False)
     st = plan.stats()
+    nxt = None
+    if world == 1 and not args.no_next and not args.roofline_only:
+        nxt = next_rows(plan, A, S, anorm, one_step)
     if args.roofline_only:
         if rank == 0:
             print(json.dumps({"roofline_only": True, "t_schur_big_ms": sst["t_schur_big_ms"],
@@ -285,6 +327,7 @@ def main():
                                      ("rccl" if world > 1 else "none"))},
             "roofline": roof,
             "cpu_baseline": cpu,
+            "next_rows": nxt,
             "phases_ms_per_step_rank0": {k[2:-3]: round(v / K, 3) for k, v in acc.items()},
             "setup_s": {"frontend": round(t_front, 2), "plan": round(t_plan, 2),
                         "h2d_upload_pcie": round(t_upload, 2)},

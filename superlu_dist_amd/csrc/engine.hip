@@ -1545,6 +1545,13 @@ struct Plan : PlanBase {
     DevBuf<T> d_aval;
     i64 a_nnz = -1;
 
+    bool has_block(int gb, int jb) const { // this rank holds L(gb,jb) (gb >= jb) or U(gb,jb)
+        const vector<int> &ids = gb < jb ? ublk_jb : lblk_ib;
+        const int f = gb < jb ? urow_first[gb / Pr] : lcol_first[jb / Pc];
+        const int nb = gb < jb ? urow_nblk[gb / Pr] : lcol_nblk[jb / Pc];
+        return std::binary_search(ids.begin() + f, ids.begin() + f + nb, gb < jb ? jb : gb);
+    }
+
     void set_a_pattern(int64_t ncol, const int64_t *xa, const int64_t *asub) override {
         SLU_REQUIRE(ncol == n, "A has %lld columns, the LU structure %d", (long long)ncol, n);
         SLU_REQUIRE(xa[0] == 0 && xa[n] >= 0, "A: bad column pointers");
@@ -1564,6 +1571,9 @@ struct Plan : PlanBase {
                 const int gb = (int)supno[irow];
                 if (gb % Pr != myrow) continue;
                 i64 m;
+                if (!has_block(gb, jb))
+                    throw Error(fmt("A(%lld,%d) is outside the %c structure (no block (%d,%d))",
+                                    (long long)irow, j, gb < jb ? 'U' : 'L', gb, jb));
                 if (gb < jb) {
                     const UBlk &B = ublk[find_ublk(gb, jb)];
                     const i64 c = B.coloff + jc;

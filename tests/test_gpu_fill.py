@@ -56,20 +56,28 @@ def test_fill_then_factor_matches_reference(name):
 
 def test_refill_new_values_same_pattern():
     """Refactor with new values of the same pattern (the reference's
-    SamePattern_SameRowPerm use): scale A by 2, refill, factor; L is
-    unchanged and U doubles (up to the order of atomic additions, which
-    may differ between two factorizations)."""
+    SamePattern_SameRowPerm use): after one factorization, refill the same
+    plan with A' = 2A + I and factor again; the factors equal those of a fresh
+    plan filled with A' (up to the order of atomic additions)."""
     A = Csc.stencil(STENCIL_3D7, 12, 12, 12)
     S = Symbolic(A, nd_order(12, 12, 12), 60, 256)
     p, lu, (cp, ri, v) = _filled_plan(A, S)
     assert p.factor(12.0) == (0, 0)
+    v2 = 2.0 * v
+    for j in range(A.n):
+        sl = slice(cp[j], cp[j + 1])
+        v2[sl][ri[sl] == j] += 1.0
+    p.fill_a(v2)
+    assert p.factor(25.0) == (0, 0)
     p.download()
-    L1, U1 = lu.Lval.copy(), lu.Uval.copy()
-    p.fill_a(2.0 * v)
-    assert p.factor(24.0) == (0, 0)
-    p.download()
-    assert np.abs(lu.Uval - 2.0 * U1).max() <= 1e-13 * np.abs(2.0 * U1).max()
-    assert np.abs(lu.Lval - L1).max() <= 1e-13 * np.abs(L1).max()
+    lu2 = S.distribute()
+    q = Plan(lu2)
+    q.set_a_pattern(cp, ri)
+    q.fill_a(v2)
+    assert q.factor(25.0) == (0, 0)
+    q.download()
+    for a, b in ((lu.Lval, lu2.Lval), (lu.Uval, lu2.Uval)):
+        assert np.abs(a - b).max() <= 1e-13 * np.abs(b).max()
 
 
 def test_fill_duplicate_entry_keeps_last():
