@@ -1468,7 +1468,7 @@ struct Plan : PlanBase {
             for (int k : bylev[L]) {
                 lvl.push_back(dg[k]);
                 for (int r0 = 0; r0 < dg[k].ld - dg[k].w; r0 += SV_THREADS) lch.push_back({k, r0});
-                for (int c0 = 0; c0 < ncol[k]; c0 += SV_THREADS) uch.push_back({k, c0});
+                for (int c0 = 0; c0 < ncol[k]; c0 += SVU_COLS) uch.push_back({k, c0});
             }
         }
         sv_d_off[nl] = (int)lvl.size();

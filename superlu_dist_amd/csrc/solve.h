@@ -31,48 +31,91 @@ struct SvChunk {    // 256 panel rows (forward) or 256 U columns (backward)
 constexpr int SV_THREADS = 256;  // panel chunks
 constexpr int SVD_THREADS = 512; // diagonal solves: one thread per row, w <= MAX_SUPER_SIZE
 
-// L_kk y_k = b_k, unit lower; thread t owns row t, column j is read one step
-// ahead (coalesced along the column), y_j is broadcast through LDS.
+__device__ inline double sv_shfl(double v, int src) { return __shfl(v, src, 64); }
+__device__ inline float sv_shfl(float v, int src) { return __shfl(v, src, 64); }
+__device__ inline zc sv_shfl(zc v, int src) { return {__shfl(v.r, src, 64), __shfl(v.i, src, 64)}; }
+
+// columns per panel of the diagonal solves: 32 (16 complex, to keep the
+// thread's panel row in registers); divides the 64-wide wavefront, so a
+// panel's rows always sit in one wavefront
+template <typename T> struct SvPanel { static constexpr int v = sizeof(T) == 16 ? 16 : 32; };
+
+// L_kk y_k = b_k, unit lower, blocked by SVP-column panels.  Thread t owns
+// row t and holds its SVP panel entries in registers (one coalesced batch of
+// loads per panel).  The panel's own rows are solved inside their wavefront
+// (y_j passed by lane shuffle, no barrier per column); one barrier publishes
+// the panel's y through LDS, then every row below subtracts L(t, panel) y.
 template <typename T>
 __global__ void __launch_bounds__(SVD_THREADS) k_sv_ldiag(const SvDiag *items, const T *Lval, T *x) {
     using Sx = S<T>;
+    constexpr int SVP = SvPanel<T>::v;
     const SvDiag it = items[blockIdx.x];
     const T *L = Lval + it.voff;
     const int t = threadIdx.x, w = it.w, ld = it.ld;
-    __shared__ T s_y[2];
+    __shared__ T s_y[2][SVP];
     T yi = t < w ? x[it.fst + t] : Sx::zero();
-    T lc = (t < w && t > 0) ? L[t] : Sx::zero();
-    for (int j = 0; j < w; ++j) {
-        if (t == j) s_y[j & 1] = yi;
+    for (int j0 = 0, buf = 0; j0 < w; j0 += SVP, buf ^= 1) {
+        const int nj = min(SVP, w - j0);
+        T l[SVP];
+#pragma unroll
+        for (int j = 0; j < SVP; ++j)
+            l[j] = (j < nj && t > j0 + j && t < w) ? L[t + (int64_t)(j0 + j) * ld] : Sx::zero();
+        if ((t >> 6) == (j0 >> 6)) {
+            const int base = j0 & 63;
+#pragma unroll
+            for (int j = 0; j < SVP; ++j) {
+                const T yj = sv_shfl(yi, base + j);
+                if (t > j0 + j && t < j0 + nj) yi = Sx::fms(yi, l[j], yj);
+            }
+            if (t >= j0 && t < j0 + nj) s_y[buf][t - j0] = yi;
+        }
         __syncthreads();
-        const T yj = s_y[j & 1];
-        const T ln = (t < w && t > j + 1) ? L[t + (int64_t)(j + 1) * ld] : Sx::zero();
-        if (t > j && t < w) yi = Sx::fms(yi, lc, yj);
-        lc = ln;
+        if (t >= j0 + nj && t < w) { // only for full panels (a partial one is the last)
+#pragma unroll
+            for (int j = 0; j < SVP; ++j) yi = Sx::fms(yi, l[j], s_y[buf][j]);
+        }
     }
     if (t < w) x[it.fst + t] = yi;
 }
 
-// U_kk x_k = y_k (upper, non-unit), column sweep from the last column.
+// U_kk x_k = y_k (upper, non-unit), blocked like k_sv_ldiag from the last
+// panel up: in-panel back substitution by lane shuffles, then every row above
+// the panel subtracts U(t, panel) x_panel.
 template <typename T>
 __global__ void __launch_bounds__(SVD_THREADS) k_sv_udiag(const SvDiag *items, const T *Lval, T *x) {
     using Sx = S<T>;
+    constexpr int SVP = SvPanel<T>::v;
     const SvDiag it = items[blockIdx.x];
     const T *L = Lval + it.voff;
     const int t = threadIdx.x, w = it.w, ld = it.ld;
-    __shared__ T s_x[2];
+    __shared__ T s_x[2][SVP];
     T yi = t < w ? x[it.fst + t] : Sx::zero();
-    T uc = (t < w - 1) ? L[t + (int64_t)(w - 1) * ld] : Sx::zero(); // column w-1, rows < w-1
-    for (int j = w - 1; j >= 0; --j) {
-        if (t == j) {
-            yi = Sx::div(yi, L[j + (int64_t)j * ld]);
-            s_x[j & 1] = yi;
+    for (int j0 = ((w - 1) / SVP) * SVP, buf = 0; j0 >= 0; j0 -= SVP, buf ^= 1) {
+        const int nj = min(SVP, w - j0);
+        T u[SVP];
+#pragma unroll
+        for (int j = 0; j < SVP; ++j)
+            u[j] = (j < nj && t < j0 + j) ? L[t + (int64_t)(j0 + j) * ld] : Sx::zero();
+        const bool mine = t >= j0 && t < j0 + nj;
+        const T d = mine ? L[t + (int64_t)t * ld] : Sx::zero();
+        if ((t >> 6) == (j0 >> 6)) {
+            const int base = j0 & 63;
+#pragma unroll
+            for (int j = SVP - 1; j >= 0; --j) {
+                if (j < nj) {
+                    if (t == j0 + j) yi = Sx::div(yi, d);
+                    const T xj = sv_shfl(yi, base + j);
+                    if (t >= j0 && t < j0 + j) yi = Sx::fms(yi, u[j], xj);
+                }
+            }
+            if (mine) s_x[buf][t - j0] = yi;
         }
         __syncthreads();
-        const T xj = s_x[j & 1];
-        const T un = (j > 0 && t < j - 1) ? L[t + (int64_t)(j - 1) * ld] : Sx::zero();
-        if (t < j) yi = Sx::fms(yi, uc, xj);
-        uc = un;
+        if (t < j0) { // the first (last-column) panel may be partial: no stale LDS
+#pragma unroll
+            for (int j = 0; j < SVP; ++j)
+                if (j < nj) yi = Sx::fms(yi, u[j], s_x[buf][j]);
+        }
     }
     if (t < w) x[it.fst + t] = yi;
 }
@@ -93,38 +136,57 @@ k_sv_lpanel(const SvChunk *chunks, const SvDiag *diag, const int64_t *roff, cons
     if (r >= nb) return;
     const T *L = Lval + it.voff + w + r;
     T acc = Sx::zero();
-    for (int j = 0; j < w; ++j) acc = Sx::fms(acc, L[(int64_t)j * it.ld], s_y[j]);
+    constexpr int UN = 16; // columns of loads in flight per thread
+    for (int j0 = 0; j0 < w; j0 += UN) {
+        T v[UN];
+#pragma unroll
+        for (int u = 0; u < UN; ++u) v[u] = j0 + u < w ? L[(int64_t)(j0 + u) * it.ld] : Sx::zero();
+#pragma unroll
+        for (int u = 0; u < UN; ++u)
+            if (j0 + u < w) acc = Sx::fms(acc, v[u], s_y[j0 + u]);
+    }
     // acc = -(L_r . y)
     Sx::atomic_sub(x + rows[roff[ch.sn] + r], Sx::neg(acc));
 }
 
-// y_k -= U(k, chunk of 256 columns) x: thread t owns rows t, t + 256 of the supernode;
-// each U column is a segment of rows fst..w-1 stored contiguously.
+// y_k -= U(k, chunk of SVU_COLS columns) x: thread t owns rows t, t + 256 of
+// the supernode; each U column is a segment of rows fst..w-1 stored
+// contiguously (coalesced along t).  Short chunks (many workgroups per
+// supernode at the chain-bound top of the tree) and 16 columns of loads in
+// flight per thread; partial sums meet in x through atomics.
+constexpr int SVU_COLS = 64;
 template <typename T>
 __global__ void __launch_bounds__(SV_THREADS)
 k_sv_upanel(const SvChunk *chunks, const SvDiag *diag, const int64_t *coff, const int *ncol,
             const int64_t *ucol_voff, const int *ucol_fst, const int *ucol_gc, const T *Uval,
             T *x) {
     using Sx = S<T>;
+    constexpr int UN = 16;
     const SvChunk ch = chunks[blockIdx.x];
     const SvDiag it = diag[ch.sn];
     const int t = threadIdx.x, w = it.w;
-    const int nc = min(SV_THREADS, ncol[ch.sn] - ch.c0);
-    __shared__ int64_t s_v[SV_THREADS];
-    __shared__ int s_f[SV_THREADS];
-    __shared__ T s_x[SV_THREADS];
-    if (t < nc) {
+    const int nc = min(SVU_COLS, ncol[ch.sn] - ch.c0);
+    __shared__ int64_t s_v[SVU_COLS];
+    __shared__ int s_f[SVU_COLS];
+    __shared__ T s_x[SVU_COLS];
+    if (t < SVU_COLS) {
         const int64_t e = coff[ch.sn] + ch.c0 + t;
-        s_v[t] = ucol_voff[e];
-        s_f[t] = ucol_fst[e] - it.fst; // first row of the segment, relative
-        s_x[t] = x[ucol_gc[e]];
+        s_v[t] = t < nc ? ucol_voff[e] : 0;
+        s_f[t] = t < nc ? ucol_fst[e] - it.fst : w; // first row of the segment, relative
+        s_x[t] = t < nc ? x[ucol_gc[e]] : Sx::zero();
     }
     __syncthreads();
     for (int i = t; i < w; i += SV_THREADS) { // w <= MAX_SUPER_SIZE = 2 x SV_THREADS
         T acc = Sx::zero();
-        for (int c = 0; c < nc; ++c) {
-            const int rf = s_f[c];
-            if (i >= rf) acc = Sx::fms(acc, Uval[s_v[c] + i - rf], s_x[c]);
+        for (int c0 = 0; c0 < nc; c0 += UN) {
+            T v[UN];
+#pragma unroll
+            for (int u = 0; u < UN; ++u) {
+                const int rf = s_f[c0 + u]; // w (no load) past the chunk's last column
+                v[u] = i >= rf ? Uval[s_v[c0 + u] + i - rf] : Sx::zero();
+            }
+#pragma unroll
+            for (int u = 0; u < UN; ++u) acc = Sx::fms(acc, v[u], s_x[c0 + u]);
         }
         Sx::atomic_sub(x + it.fst + i, Sx::neg(acc));
     }
