@@ -168,6 +168,18 @@ int slu_plan_solve(slu_plan *p, void *b, int64_t ldb, int nrhs);
  * t_fill_ms in the stats is the device time of the zero + scatter. */
 int slu_plan_set_a_pattern(slu_plan *p, int64_t ncol, const int64_t *xa, const int64_t *asub);
 int slu_plan_fill_a(slu_plan *p, const void *a, int on_device);
+/* Iterative refinement on the device (SRC/pdgsrfs.c:197-253; 1x1 grid, the
+ * LUstruct's permuted coordinates): for each of the nrhs columns of b / x
+ * (ld ld, host arrays of the plan's element type), repeat R = b - A x,
+ * berr = max_i |R_i| / (|A||x| + |b|)_i (SAFE1/SAFE2 guards), and while
+ * berr > eps, berr <= lstres / 2 and fewer than 20 steps, x += solve(R) with
+ * the device factors.  A = the values of the last slu_plan_fill_a (a device
+ * pointer passed there must stay valid).  x: in = initial solution (e.g.
+ * from slu_plan_solve), out = refined.  berr[nrhs], steps[nrhs] (may be
+ * NULL) receive the final backward error and the number of steps
+ * (stat->RefineSteps).  t_refine_ms in the stats = device time of the call. */
+int slu_plan_refine(slu_plan *p, const void *b, void *x, int64_t ld, int nrhs, double *berr,
+                    int *steps);
 void slu_plan_destroy(slu_plan *p);
 
 /* Plan statistics (algorithmic work of one factorization on this rank). */
@@ -189,6 +201,7 @@ typedef struct {
     double comm_bytes;         /* bytes this rank sends + receives per factor */
     double t_solve_ms;         /* device time of the last slu_plan_solve */
     double t_fill_ms;          /* device time of the last slu_plan_fill_a */
+    double t_refine_ms;        /* device time of the last slu_plan_refine */
 } slu_plan_stats;
 int slu_plan_get_stats(const slu_plan *p, slu_plan_stats *st);
 

@@ -33,6 +33,7 @@
 #include <memory>
 #include <numeric>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "common.h"
@@ -211,6 +212,7 @@ struct PlanBase {
     virtual void solve(void *b, int64_t ldb, int nrhs) = 0;
     virtual void set_a_pattern(int64_t ncol, const int64_t *xa, const int64_t *asub) = 0;
     virtual void fill_a(const void *a, int on_device) = 0;
+    virtual void refine(const void *b, void *x, int64_t ld, int nrhs, double *berr, int *steps) = 0;
     slu_plan_stats stats{};
 };
 
@@ -1487,6 +1489,33 @@ struct Plan : PlanBase {
         sv_ready = true;
     }
 
+    // L and U sweeps over the device vector xv (in place), on `stream`
+    void sweep(T *xv) {
+        const int nl = (int)bylev.size();
+        for (int L = 0; L < nl; ++L) { // L y = b
+            const int nd = sv_d_off[L + 1] - sv_d_off[L], nc = sv_l_off[L + 1] - sv_l_off[L];
+            if (nd)
+                hipLaunchKernelGGL(k_sv_ldiag<T>, dim3(nd), dim3(SVD_THREADS), 0, stream,
+                                   d_sv_lvl.p + sv_d_off[L], d_L.p, xv);
+            if (nc)
+                hipLaunchKernelGGL(k_sv_lpanel<T>, dim3(nc), dim3(SV_THREADS), 0, stream,
+                                   d_sv_lch.p + sv_l_off[L], d_sv_diag.p, d_sv_roff.p,
+                                   d_sv_rows.p, d_L.p, xv);
+        }
+        for (int L = nl - 1; L >= 0; --L) { // U x = y
+            const int nd = sv_d_off[L + 1] - sv_d_off[L], nc = sv_u_off[L + 1] - sv_u_off[L];
+            if (nc)
+                hipLaunchKernelGGL(k_sv_upanel<T>, dim3(nc), dim3(SV_THREADS), 0, stream,
+                                   d_sv_uch.p + sv_u_off[L], d_sv_diag.p, d_sv_coff.p,
+                                   d_sv_ncol.p, d_ucol_voff.p, d_ucol_fst.p, d_sv_gc.p,
+                                   d_U.p, xv);
+            if (nd)
+                hipLaunchKernelGGL(k_sv_udiag<T>, dim3(nd), dim3(SVD_THREADS), 0, stream,
+                                   d_sv_lvl.p + sv_d_off[L], d_L.p, xv);
+        }
+        HIPCHK(hipGetLastError());
+    }
+
     void solve(void *b, int64_t ldb, int nrhs) override {
         if (!sv_ready) build_solve();
         SLU_REQUIRE(ldb >= n && nrhs >= 0, "solve: ldb %lld < n %d", (long long)ldb, n);
@@ -1494,33 +1523,11 @@ struct Plan : PlanBase {
         HIPCHK(hipEventCreate(&e0));
         HIPCHK(hipEventCreate(&e1));
         float total = 0;
-        const int nl = (int)bylev.size();
         for (int r = 0; r < nrhs; ++r) {
             HT *hb = (HT *)b + (i64)r * ldb;
             HIPCHK(hipMemcpyAsync(d_sv_x.p, hb, (size_t)n * sizeof(T), hipMemcpyHostToDevice, stream));
             HIPCHK(hipEventRecord(e0, stream));
-            for (int L = 0; L < nl; ++L) { // L y = b
-                const int nd = sv_d_off[L + 1] - sv_d_off[L], nc = sv_l_off[L + 1] - sv_l_off[L];
-                if (nd)
-                    hipLaunchKernelGGL(k_sv_ldiag<T>, dim3(nd), dim3(SVD_THREADS), 0, stream,
-                                       d_sv_lvl.p + sv_d_off[L], d_L.p, d_sv_x.p);
-                if (nc)
-                    hipLaunchKernelGGL(k_sv_lpanel<T>, dim3(nc), dim3(SV_THREADS), 0, stream,
-                                       d_sv_lch.p + sv_l_off[L], d_sv_diag.p, d_sv_roff.p,
-                                       d_sv_rows.p, d_L.p, d_sv_x.p);
-            }
-            for (int L = nl - 1; L >= 0; --L) { // U x = y
-                const int nd = sv_d_off[L + 1] - sv_d_off[L], nc = sv_u_off[L + 1] - sv_u_off[L];
-                if (nc)
-                    hipLaunchKernelGGL(k_sv_upanel<T>, dim3(nc), dim3(SV_THREADS), 0, stream,
-                                       d_sv_uch.p + sv_u_off[L], d_sv_diag.p, d_sv_coff.p,
-                                       d_sv_ncol.p, d_ucol_voff.p, d_ucol_fst.p, d_sv_gc.p,
-                                       d_U.p, d_sv_x.p);
-                if (nd)
-                    hipLaunchKernelGGL(k_sv_udiag<T>, dim3(nd), dim3(SVD_THREADS), 0, stream,
-                                       d_sv_lvl.p + sv_d_off[L], d_L.p, d_sv_x.p);
-            }
-            HIPCHK(hipGetLastError());
+            sweep(d_sv_x.p);
             HIPCHK(hipEventRecord(e1, stream));
             HIPCHK(hipMemcpyAsync(hb, d_sv_x.p, (size_t)n * sizeof(T), hipMemcpyDeviceToHost, stream));
             HIPCHK(hipStreamSynchronize(stream));
@@ -1531,6 +1538,74 @@ struct Plan : PlanBase {
         (void)hipEventDestroy(e0);
         (void)hipEventDestroy(e1);
         stats.t_solve_ms = total;
+    }
+
+    // Iterative refinement on the device (SRC/pdgsrfs.c:197-253, 1x1 grid,
+    // permuted coordinates): R = B - A X and S = |A||X| + |B| by rows of A
+    // (k_resid), componentwise backward error berr = max |R_i| / S_i with the
+    // SAFE1/SAFE2 guards (:219-230); while berr > eps, berr halves and fewer
+    // than ITMAX = 20 steps: solve A dx = R with the device factors, X += dx.
+    // A is the matrix of the last slu_plan_fill_a.
+    DevBuf<i64> d_rp;
+    DevBuf<int> d_rc;
+    DevBuf<i64> d_re;
+    const T *d_acur = nullptr;
+    DevBuf<T> d_rf_b, d_rf_x, d_rf_r;
+    DevBuf<unsigned long long> d_rf_berr;
+
+    void refine(const void *b, void *x, int64_t ld, int nrhs, double *berr, int *steps) override {
+        SLU_REQUIRE(Pr * Pc == 1, "refine: 1x1 grids only");
+        SLU_REQUIRE(d_acur != nullptr, "refine needs the values of A (slu_plan_fill_a)");
+        SLU_REQUIRE(ld >= n && nrhs >= 0, "refine: ld %lld < n %d", (long long)ld, n);
+        if (!sv_ready) build_solve();
+        const bool dbl = !std::is_same<T, float>::value;
+        const double eps = dbl ? 0.5 * 2.220446049250313e-16 : 0.5 * 1.1920928955078125e-07;
+        const double safmin = dbl ? 2.2250738585072014e-308 : 1.1754943508222875e-38;
+        const double safe1 = (double)(n + 1) * safmin, safe2 = safe1 / eps;
+        d_rf_b.alloc(std::max(n, 1));
+        d_rf_x.alloc(std::max(n, 1));
+        d_rf_r.alloc(std::max(n, 1));
+        d_rf_berr.alloc(1);
+        const unsigned rb = (unsigned)((n + 255) / 256);
+        hipEvent_t e0, e1;
+        HIPCHK(hipEventCreate(&e0));
+        HIPCHK(hipEventCreate(&e1));
+        HIPCHK(hipStreamSynchronize(pstream));
+        HIPCHK(hipEventRecord(e0, stream));
+        for (int j = 0; j < nrhs; ++j) {
+            const HT *hb = (const HT *)b + (i64)j * ld;
+            HT *hx = (HT *)x + (i64)j * ld;
+            HIPCHK(hipMemcpyAsync(d_rf_b.p, hb, (size_t)n * sizeof(T), hipMemcpyHostToDevice, stream));
+            HIPCHK(hipMemcpyAsync(d_rf_x.p, hx, (size_t)n * sizeof(T), hipMemcpyHostToDevice, stream));
+            int count = 0;
+            double lstres = 3.0, be = 0.0;
+            while (true) {
+                HIPCHK(hipMemsetAsync(d_rf_berr.p, 0, sizeof(unsigned long long), stream));
+                hipLaunchKernelGGL(k_resid<T>, dim3(rb), dim3(256), 0, stream, d_rp.p, d_rc.p, d_re.p,
+                                   d_acur, d_rf_x.p, d_rf_b.p, d_rf_r.p, n, safe1, safe2, d_rf_berr.p);
+                HIPCHK(hipGetLastError());
+                unsigned long long bits = 0;
+                HIPCHK(hipMemcpyAsync(&bits, d_rf_berr.p, sizeof bits, hipMemcpyDeviceToHost, stream));
+                HIPCHK(hipStreamSynchronize(stream));
+                memcpy(&be, &bits, sizeof be);
+                if (!(be > eps && be * 2 <= lstres && count < 20)) break;
+                sweep(d_rf_r.p);
+                hipLaunchKernelGGL(k_axpy1<T>, dim3(rb), dim3(256), 0, stream, d_rf_x.p, d_rf_r.p, n);
+                lstres = be;
+                ++count;
+            }
+            HIPCHK(hipMemcpyAsync(hx, d_rf_x.p, (size_t)n * sizeof(T), hipMemcpyDeviceToHost, stream));
+            HIPCHK(hipStreamSynchronize(stream));
+            if (berr) berr[j] = be;
+            if (steps) steps[j] = count;
+        }
+        HIPCHK(hipEventRecord(e1, stream));
+        HIPCHK(hipStreamSynchronize(stream));
+        float ms = 0;
+        HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+        stats.t_refine_ms = ms;
     }
 
     // ------------------------------------------------------- values of A
@@ -1597,15 +1672,34 @@ struct Plan : PlanBase {
         d_amap.upload(map.empty() ? vector<i64>(1, -1) : map);
         d_aval.alloc(std::max<i64>(nnz, 1));
         a_nnz = nnz;
+        d_acur = nullptr;
+        if (Pr * Pc == 1) { // rows of A for the refinement's residual (k_resid)
+            vector<i64> rp(n + 1, 0), re((size_t)nnz);
+            vector<int> rc((size_t)nnz);
+            for (i64 e = 0; e < nnz; ++e) ++rp[asub[e] + 1];
+            for (int i = 0; i < n; ++i) rp[i + 1] += rp[i];
+            vector<i64> nx(rp.begin(), rp.end() - 1);
+            for (int j = 0; j < n; ++j)
+                for (i64 e = xa[j]; e < xa[j + 1]; ++e) {
+                    const i64 q = nx[asub[e]]++;
+                    rc[q] = j;
+                    re[q] = e;
+                }
+            d_rp.upload(rp);
+            d_rc.upload(rc.empty() ? vector<int>(1, 0) : rc);
+            d_re.upload(re.empty() ? vector<i64>(1, 0) : re);
+        }
     }
 
     void fill_a(const void *a, int on_device) override {
         SLU_REQUIRE(a_nnz >= 0, "fill_a before set_a_pattern");
         const T *src = (const T *)a;
-        if (!on_device && a_nnz) {
-            HIPCHK(hipMemcpyAsync(d_aval.p, a, (size_t)a_nnz * sizeof(T), hipMemcpyHostToDevice, stream));
+        if (!on_device) {
+            if (a_nnz)
+                HIPCHK(hipMemcpyAsync(d_aval.p, a, (size_t)a_nnz * sizeof(T), hipMemcpyHostToDevice, stream));
             src = d_aval.p;
         }
+        d_acur = src;
         hipEvent_t e0, e1;
         HIPCHK(hipEventCreate(&e0));
         HIPCHK(hipEventCreate(&e1));
@@ -1817,6 +1911,17 @@ int slu_plan_set_a_pattern(slu_plan *p, int64_t ncol, const int64_t *xa, const i
 int slu_plan_fill_a(slu_plan *p, const void *a, int on_device) {
     try {
         p->impl->fill_a(a, on_device);
+        return 0;
+    } catch (const std::exception &e) {
+        set_last_error(e.what());
+        return -1;
+    }
+}
+
+int slu_plan_refine(slu_plan *p, const void *b, void *x, int64_t ld, int nrhs, double *berr,
+                    int *steps) {
+    try {
+        p->impl->refine(b, x, ld, nrhs, berr, steps);
         return 0;
     } catch (const std::exception &e) {
         set_last_error(e.what());

@@ -192,4 +192,39 @@ k_sv_upanel(const SvChunk *chunks, const SvDiag *diag, const int64_t *coff, cons
     }
 }
 
+// Residual of the iterative refinement (SRC/pdgsrfs.c:209-230) by rows of A
+// (CSR index over the CSC values): r = b - A x, s = |A||x| + |b| (abs1 for
+// complex, as pzgsrfs), berr = max_i |r_i| / s_i with the SAFE1 / SAFE2
+// guards; the max over rows goes through the bit pattern of non-negative
+// doubles (monotone as unsigned integers).
+template <typename T>
+__global__ void __launch_bounds__(256)
+k_resid(const int64_t *rp, const int *rc, const int64_t *re, const T *a, const T *x, const T *b,
+        T *r, int n, double safe1, double safe2, unsigned long long *berr) {
+    using Sx = S<T>;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    double s = 0.0;
+    if (i < n) {
+        T acc = b[i];
+        double tmp = Sx::abs1(b[i]);
+        for (int64_t e = rp[i]; e < rp[i + 1]; ++e) {
+            const T av = a[re[e]], xv = x[rc[e]];
+            acc = Sx::fms(acc, av, xv);
+            tmp += Sx::abs1(av) * Sx::abs1(xv);
+        }
+        r[i] = acc;
+        const double ra = Sx::abs1(acc);
+        if (tmp > safe2) s = ra / tmp;
+        else if (tmp != 0.0) s = (safe1 + ra) / tmp;
+    }
+    for (int off = 32; off > 0; off >>= 1) s = fmax(s, __shfl_xor(s, off, 64));
+    if ((threadIdx.x & 63) == 0 && s > 0.0)
+        atomicMax(berr, (unsigned long long)__double_as_longlong(s));
+}
+
+template <typename T> __global__ void __launch_bounds__(256) k_axpy1(T *x, const T *dx, int n) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < n) x[i] = S<T>::sub(x[i], S<T>::neg(dx[i]));
+}
+
 } // namespace slu

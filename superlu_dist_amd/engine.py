@@ -140,6 +140,23 @@ class Plan:
             raise ValueError(f"{len(v)} values for a pattern of {len(self._asub)} nonzeros")
         self._chk(lib().slu_plan_fill_a(self.ptr, v.ctypes.data_as(C.c_void_p), 0))
 
+    def refine(self, b, x):
+        """Iterative refinement of x for A x = b on the device (pdgsrfs), A =
+        the values of the last fill_a; returns (x, berr, steps) per column."""
+        dt = self.lu.Lval.dtype
+        bb = np.array(b, dtype=dt, order="F", copy=True)
+        xx = np.array(x, dtype=dt, order="F", copy=True)
+        if bb.shape != xx.shape:
+            raise ValueError("b and x differ in shape")
+        nrhs = 1 if bb.ndim == 1 else bb.shape[1]
+        berr = np.zeros(max(nrhs, 1))
+        steps = np.zeros(max(nrhs, 1), dtype=np.int32)
+        self._chk(lib().slu_plan_refine(self.ptr, bb.ctypes.data_as(C.c_void_p),
+                                        xx.ctypes.data_as(C.c_void_p), bb.shape[0], nrhs,
+                                        berr.ctypes.data_as(C.POINTER(C.c_double)),
+                                        steps.ctypes.data_as(C.POINTER(C.c_int))))
+        return xx, berr[:nrhs], steps[:nrhs]
+
     def stats(self):
         st = PlanStats()
         lib().slu_plan_get_stats(self.ptr, C.byref(st))

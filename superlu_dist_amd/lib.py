@@ -57,7 +57,8 @@ class PlanStats(C.Structure):
                 ("t_comm_ms", C.c_double), ("t_schur_big_ms", C.c_double),
                 ("schur_big_flops", C.c_double), ("n_schur_launches", C.c_int64),
                 ("n_schur_big_launches", C.c_int64), ("comm_bytes", C.c_double),
-                ("t_solve_ms", C.c_double), ("t_fill_ms", C.c_double)]
+                ("t_solve_ms", C.c_double), ("t_fill_ms", C.c_double),
+                ("t_refine_ms", C.c_double)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -104,6 +105,7 @@ def lib():
         "slu_plan_solve": (C.c_int, [P, P, C.c_int64, C.c_int]),
         "slu_plan_set_a_pattern": (C.c_int, [P, C.c_int64, c_i64p, c_i64p]),
         "slu_plan_fill_a": (C.c_int, [P, P, C.c_int]),
+        "slu_plan_refine": (C.c_int, [P, P, P, C.c_int64, C.c_int, C.POINTER(C.c_double), c_intp]),
         "slu_plan_snapshot": (C.c_int, [P]),
         "slu_plan_restore": (C.c_int, [P]),
         "slu_plan_sync": (C.c_int, [P]),
