@@ -69,8 +69,9 @@ def build_lu(workload, nx, pr, pc, myrow, mycol):
 def next_rows(plan, A, S, anorm, one_step):
     """SURVEY 8(f) rows 1-2 on the same workload, untimed for value:
     device refill of the factor storage from A (SamePattern_SameRowPerm,
-    instead of the PCIe upload of L and U) and the triangular solve on the
-    device-resident factors, with the solve's backward error."""
+    instead of the PCIe upload of L and U), the triangular solve on the
+    device-resident factors with its backward error, and the iterative
+    refinement (pdgsrfs) of that solution."""
     import scipy.sparse as sp
     cp, ri, v = A.permuted(S.perm_c).arrays()
     t0 = time.time()
@@ -93,6 +94,8 @@ def next_rows(plan, A, S, anorm, one_step):
         solves.append(plan.stats()["t_solve_ms"])
     r = B @ x - b
     berr = float(np.abs(r).max() / (abs(B).sum(axis=1).max() * np.abs(x).max()))
+    xr, rberr, rsteps = plan.refine(b, x)
+    t_ref = plan.stats()["t_refine_ms"]
     fill_ms = min(fills)
     return {"fill": {"kernel": "memset L/U + k_fill_a (nnz(A) scatter)",
                      "device_ms": round(fill_ms, 3),
@@ -100,7 +103,10 @@ def next_rows(plan, A, S, anorm, one_step):
                      "pattern_setup_s": round(t_pat, 3), "nnz_A": int(len(v)),
                      "lu_bytes": lu_bytes, "factor_info_after_fill": int(info)},
             "solve": {"device_ms": round(min(solves), 3), "nrhs": 1, "berr": berr,
-                      "fwd_err": float(np.abs(x - xt).max() / np.abs(xt).max())}}
+                      "fwd_err": float(np.abs(x - xt).max() / np.abs(xt).max())},
+            "refine": {"device_ms": round(t_ref, 3), "steps": int(rsteps[0]),
+                       "berr_componentwise": float(rberr[0]),
+                       "fwd_err": float(np.abs(xr - xt).max() / np.abs(xt).max())}}
 
 
 def one_norm(A):
