@@ -1489,47 +1489,59 @@ struct Plan : PlanBase {
         sv_ready = true;
     }
 
-    // L and U sweeps over the device vector xv (in place), on `stream`
-    void sweep(T *xv) {
+    // L and U sweeps over nr <= SV_NR device vectors xv (ld ldx, in place), on `stream`
+    template <int NR> void sweep_nr(T *xv, i64 ldx, int nr) {
         const int nl = (int)bylev.size();
         for (int L = 0; L < nl; ++L) { // L y = b
             const int nd = sv_d_off[L + 1] - sv_d_off[L], nc = sv_l_off[L + 1] - sv_l_off[L];
             if (nd)
-                hipLaunchKernelGGL(k_sv_ldiag<T>, dim3(nd), dim3(SVD_THREADS), 0, stream,
-                                   d_sv_lvl.p + sv_d_off[L], d_L.p, xv);
+                hipLaunchKernelGGL((k_sv_ldiag<T, NR>), dim3(nd), dim3(SVD_THREADS), 0, stream,
+                                   d_sv_lvl.p + sv_d_off[L], d_L.p, xv, ldx, nr);
             if (nc)
-                hipLaunchKernelGGL(k_sv_lpanel<T>, dim3(nc), dim3(SV_THREADS), 0, stream,
+                hipLaunchKernelGGL((k_sv_lpanel<T, NR>), dim3(nc), dim3(SV_THREADS), 0, stream,
                                    d_sv_lch.p + sv_l_off[L], d_sv_diag.p, d_sv_roff.p,
-                                   d_sv_rows.p, d_L.p, xv);
+                                   d_sv_rows.p, d_L.p, xv, ldx, nr);
         }
         for (int L = nl - 1; L >= 0; --L) { // U x = y
             const int nd = sv_d_off[L + 1] - sv_d_off[L], nc = sv_u_off[L + 1] - sv_u_off[L];
             if (nc)
-                hipLaunchKernelGGL(k_sv_upanel<T>, dim3(nc), dim3(SV_THREADS), 0, stream,
+                hipLaunchKernelGGL((k_sv_upanel<T, NR>), dim3(nc), dim3(SV_THREADS), 0, stream,
                                    d_sv_uch.p + sv_u_off[L], d_sv_diag.p, d_sv_coff.p,
                                    d_sv_ncol.p, d_ucol_voff.p, d_ucol_fst.p, d_sv_gc.p,
-                                   d_U.p, xv);
+                                   d_U.p, xv, ldx, nr);
             if (nd)
-                hipLaunchKernelGGL(k_sv_udiag<T>, dim3(nd), dim3(SVD_THREADS), 0, stream,
-                                   d_sv_lvl.p + sv_d_off[L], d_L.p, xv);
+                hipLaunchKernelGGL((k_sv_udiag<T, NR>), dim3(nd), dim3(SVD_THREADS), 0, stream,
+                                   d_sv_lvl.p + sv_d_off[L], d_L.p, xv, ldx, nr);
         }
         HIPCHK(hipGetLastError());
     }
+    void sweep(T *xv, i64 ldx = 0, int nr = 1) {
+        if (nr == 1) sweep_nr<1>(xv, ldx, 1);
+        else sweep_nr<SvNr<T>::v>(xv, ldx, nr);
+    }
 
+    // right-hand sides in batches of SvNr<T>: every factor element is read once
+    // per batch and sweep
     void solve(void *b, int64_t ldb, int nrhs) override {
         if (!sv_ready) build_solve();
         SLU_REQUIRE(ldb >= n && nrhs >= 0, "solve: ldb %lld < n %d", (long long)ldb, n);
+        constexpr int NB = SvNr<T>::v;
+        if (nrhs > 1 && d_sv_x.n < (size_t)n * NB) d_sv_x.alloc((size_t)std::max(n, 1) * NB);
         hipEvent_t e0, e1;
         HIPCHK(hipEventCreate(&e0));
         HIPCHK(hipEventCreate(&e1));
         float total = 0;
-        for (int r = 0; r < nrhs; ++r) {
-            HT *hb = (HT *)b + (i64)r * ldb;
-            HIPCHK(hipMemcpyAsync(d_sv_x.p, hb, (size_t)n * sizeof(T), hipMemcpyHostToDevice, stream));
+        for (int r0 = 0; r0 < nrhs; r0 += NB) {
+            const int nr = std::min(NB, nrhs - r0);
+            for (int q = 0; q < nr; ++q)
+                HIPCHK(hipMemcpyAsync(d_sv_x.p + (i64)q * n, (HT *)b + (i64)(r0 + q) * ldb,
+                                      (size_t)n * sizeof(T), hipMemcpyHostToDevice, stream));
             HIPCHK(hipEventRecord(e0, stream));
-            sweep(d_sv_x.p);
+            sweep(d_sv_x.p, n, nr);
             HIPCHK(hipEventRecord(e1, stream));
-            HIPCHK(hipMemcpyAsync(hb, d_sv_x.p, (size_t)n * sizeof(T), hipMemcpyDeviceToHost, stream));
+            for (int q = 0; q < nr; ++q)
+                HIPCHK(hipMemcpyAsync((HT *)b + (i64)(r0 + q) * ldb, d_sv_x.p + (i64)q * n,
+                                      (size_t)n * sizeof(T), hipMemcpyDeviceToHost, stream));
             HIPCHK(hipStreamSynchronize(stream));
             float ms = 0;
             HIPCHK(hipEventElapsedTime(&ms, e0, e1));

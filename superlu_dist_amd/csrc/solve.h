@@ -40,20 +40,29 @@ __device__ inline zc sv_shfl(zc v, int src) { return {__shfl(v.r, src, 64), __sh
 // panel's rows always sit in one wavefront
 template <typename T> struct SvPanel { static constexpr int v = sizeof(T) == 16 ? 16 : 32; };
 
+// Right-hand sides: NR (compile-time, 1 or SV_NR) columns of x with leading
+// dimension ldx, of which the first nr (<= NR, uniform) are live; every
+// factor element is read once per sweep for all of them.
+constexpr int SV_NR = 8;
+template <typename T> struct SvNr { static constexpr int v = sizeof(T) == 16 ? 2 : SV_NR; }; // no spills
+
 // L_kk y_k = b_k, unit lower, blocked by SVP-column panels.  Thread t owns
 // row t and holds its SVP panel entries in registers (one coalesced batch of
 // loads per panel).  The panel's own rows are solved inside their wavefront
 // (y_j passed by lane shuffle, no barrier per column); one barrier publishes
 // the panel's y through LDS, then every row below subtracts L(t, panel) y.
-template <typename T>
-__global__ void __launch_bounds__(SVD_THREADS) k_sv_ldiag(const SvDiag *items, const T *Lval, T *x) {
+template <typename T, int NR>
+__global__ void __launch_bounds__(SVD_THREADS)
+k_sv_ldiag(const SvDiag *items, const T *Lval, T *x, int64_t ldx, int nr) {
     using Sx = S<T>;
     constexpr int SVP = SvPanel<T>::v;
     const SvDiag it = items[blockIdx.x];
     const T *L = Lval + it.voff;
     const int t = threadIdx.x, w = it.w, ld = it.ld;
-    __shared__ T s_y[2][SVP];
-    T yi = t < w ? x[it.fst + t] : Sx::zero();
+    __shared__ T s_y[2][NR][SVP];
+    T yi[NR];
+#pragma unroll
+    for (int q = 0; q < NR; ++q) yi[q] = (q < nr && t < w) ? x[it.fst + t + q * ldx] : Sx::zero();
     for (int j0 = 0, buf = 0; j0 < w; j0 += SVP, buf ^= 1) {
         const int nj = min(SVP, w - j0);
         T l[SVP];
@@ -64,32 +73,48 @@ __global__ void __launch_bounds__(SVD_THREADS) k_sv_ldiag(const SvDiag *items, c
             const int base = j0 & 63;
 #pragma unroll
             for (int j = 0; j < SVP; ++j) {
-                const T yj = sv_shfl(yi, base + j);
-                if (t > j0 + j && t < j0 + nj) yi = Sx::fms(yi, l[j], yj);
+                const bool upd = t > j0 + j && t < j0 + nj;
+#pragma unroll
+                for (int q = 0; q < NR; ++q) {
+                    if (q >= nr) break;
+                    const T yj = sv_shfl(yi[q], base + j);
+                    if (upd) yi[q] = Sx::fms(yi[q], l[j], yj);
+                }
             }
-            if (t >= j0 && t < j0 + nj) s_y[buf][t - j0] = yi;
+            if (t >= j0 && t < j0 + nj)
+#pragma unroll
+                for (int q = 0; q < NR; ++q) s_y[buf][q][t - j0] = yi[q];
         }
         __syncthreads();
         if (t >= j0 + nj && t < w) { // only for full panels (a partial one is the last)
 #pragma unroll
-            for (int j = 0; j < SVP; ++j) yi = Sx::fms(yi, l[j], s_y[buf][j]);
+            for (int q = 0; q < NR; ++q) {
+                if (q >= nr) break;
+#pragma unroll
+                for (int j = 0; j < SVP; ++j) yi[q] = Sx::fms(yi[q], l[j], s_y[buf][q][j]);
+            }
         }
     }
-    if (t < w) x[it.fst + t] = yi;
+#pragma unroll
+    for (int q = 0; q < NR; ++q)
+        if (q < nr && t < w) x[it.fst + t + q * ldx] = yi[q];
 }
 
 // U_kk x_k = y_k (upper, non-unit), blocked like k_sv_ldiag from the last
 // panel up: in-panel back substitution by lane shuffles, then every row above
 // the panel subtracts U(t, panel) x_panel.
-template <typename T>
-__global__ void __launch_bounds__(SVD_THREADS) k_sv_udiag(const SvDiag *items, const T *Lval, T *x) {
+template <typename T, int NR>
+__global__ void __launch_bounds__(SVD_THREADS)
+k_sv_udiag(const SvDiag *items, const T *Lval, T *x, int64_t ldx, int nr) {
     using Sx = S<T>;
     constexpr int SVP = SvPanel<T>::v;
     const SvDiag it = items[blockIdx.x];
     const T *L = Lval + it.voff;
     const int t = threadIdx.x, w = it.w, ld = it.ld;
-    __shared__ T s_x[2][SVP];
-    T yi = t < w ? x[it.fst + t] : Sx::zero();
+    __shared__ T s_x[2][NR][SVP];
+    T yi[NR];
+#pragma unroll
+    for (int q = 0; q < NR; ++q) yi[q] = (q < nr && t < w) ? x[it.fst + t + q * ldx] : Sx::zero();
     for (int j0 = ((w - 1) / SVP) * SVP, buf = 0; j0 >= 0; j0 -= SVP, buf ^= 1) {
         const int nj = min(SVP, w - j0);
         T u[SVP];
@@ -103,50 +128,73 @@ __global__ void __launch_bounds__(SVD_THREADS) k_sv_udiag(const SvDiag *items, c
 #pragma unroll
             for (int j = SVP - 1; j >= 0; --j) {
                 if (j < nj) {
-                    if (t == j0 + j) yi = Sx::div(yi, d);
-                    const T xj = sv_shfl(yi, base + j);
-                    if (t >= j0 && t < j0 + j) yi = Sx::fms(yi, u[j], xj);
+                    const bool upd = t >= j0 && t < j0 + j;
+#pragma unroll
+                    for (int q = 0; q < NR; ++q) {
+                        if (q >= nr) break;
+                        if (t == j0 + j) yi[q] = Sx::div(yi[q], d);
+                        const T xj = sv_shfl(yi[q], base + j);
+                        if (upd) yi[q] = Sx::fms(yi[q], u[j], xj);
+                    }
                 }
             }
-            if (mine) s_x[buf][t - j0] = yi;
+            if (mine)
+#pragma unroll
+                for (int q = 0; q < NR; ++q) s_x[buf][q][t - j0] = yi[q];
         }
         __syncthreads();
         if (t < j0) { // the first (last-column) panel may be partial: no stale LDS
 #pragma unroll
-            for (int j = 0; j < SVP; ++j)
-                if (j < nj) yi = Sx::fms(yi, u[j], s_x[buf][j]);
+            for (int q = 0; q < NR; ++q) {
+                if (q >= nr) break;
+#pragma unroll
+                for (int j = 0; j < SVP; ++j)
+                    if (j < nj) yi[q] = Sx::fms(yi[q], u[j], s_x[buf][q][j]);
+            }
         }
     }
-    if (t < w) x[it.fst + t] = yi;
+#pragma unroll
+    for (int q = 0; q < NR; ++q)
+        if (q < nr && t < w) x[it.fst + t + q * ldx] = yi[q];
 }
 
 // x[rows below] -= L_panel(256-row chunk) * y_k.
-template <typename T>
+template <typename T, int NR>
 __global__ void __launch_bounds__(SV_THREADS)
 k_sv_lpanel(const SvChunk *chunks, const SvDiag *diag, const int64_t *roff, const int *rows,
-            const T *Lval, T *x) {
+            const T *Lval, T *x, int64_t ldx, int nr) {
     using Sx = S<T>;
     const SvChunk ch = chunks[blockIdx.x];
     const SvDiag it = diag[ch.sn];
     const int t = threadIdx.x, w = it.w, nb = it.ld - it.w;
-    __shared__ T s_y[FAST_MAXW * 2];
-    for (int j = t; j < w; j += SV_THREADS) s_y[j] = x[it.fst + j];
+    __shared__ T s_y[NR][FAST_MAXW * 2];
+    for (int q = 0; q < nr; ++q)
+        for (int j = t; j < w; j += SV_THREADS) s_y[q][j] = x[it.fst + j + q * ldx];
     __syncthreads();
     const int r = ch.c0 + t;
     if (r >= nb) return;
     const T *L = Lval + it.voff + w + r;
-    T acc = Sx::zero();
+    T acc[NR];
+#pragma unroll
+    for (int q = 0; q < NR; ++q) acc[q] = Sx::zero();
     constexpr int UN = 16; // columns of loads in flight per thread
     for (int j0 = 0; j0 < w; j0 += UN) {
         T v[UN];
 #pragma unroll
         for (int u = 0; u < UN; ++u) v[u] = j0 + u < w ? L[(int64_t)(j0 + u) * it.ld] : Sx::zero();
 #pragma unroll
-        for (int u = 0; u < UN; ++u)
-            if (j0 + u < w) acc = Sx::fms(acc, v[u], s_y[j0 + u]);
+        for (int q = 0; q < NR; ++q) {
+            if (q >= nr) break;
+#pragma unroll
+            for (int u = 0; u < UN; ++u)
+                if (j0 + u < w) acc[q] = Sx::fms(acc[q], v[u], s_y[q][j0 + u]);
+        }
     }
     // acc = -(L_r . y)
-    Sx::atomic_sub(x + rows[roff[ch.sn] + r], Sx::neg(acc));
+    const int64_t gr = rows[roff[ch.sn] + r];
+#pragma unroll
+    for (int q = 0; q < NR; ++q)
+        if (q < nr) Sx::atomic_sub(x + gr + q * ldx, Sx::neg(acc[q]));
 }
 
 // y_k -= U(k, chunk of SVU_COLS columns) x: thread t owns rows t, t + 256 of
@@ -155,11 +203,11 @@ k_sv_lpanel(const SvChunk *chunks, const SvDiag *diag, const int64_t *roff, cons
 // supernode at the chain-bound top of the tree) and 16 columns of loads in
 // flight per thread; partial sums meet in x through atomics.
 constexpr int SVU_COLS = 64;
-template <typename T>
+template <typename T, int NR>
 __global__ void __launch_bounds__(SV_THREADS)
 k_sv_upanel(const SvChunk *chunks, const SvDiag *diag, const int64_t *coff, const int *ncol,
             const int64_t *ucol_voff, const int *ucol_fst, const int *ucol_gc, const T *Uval,
-            T *x) {
+            T *x, int64_t ldx, int nr) {
     using Sx = S<T>;
     constexpr int UN = 16;
     const SvChunk ch = chunks[blockIdx.x];
@@ -168,16 +216,20 @@ k_sv_upanel(const SvChunk *chunks, const SvDiag *diag, const int64_t *coff, cons
     const int nc = min(SVU_COLS, ncol[ch.sn] - ch.c0);
     __shared__ int64_t s_v[SVU_COLS];
     __shared__ int s_f[SVU_COLS];
-    __shared__ T s_x[SVU_COLS];
+    __shared__ T s_x[NR][SVU_COLS];
     if (t < SVU_COLS) {
         const int64_t e = coff[ch.sn] + ch.c0 + t;
         s_v[t] = t < nc ? ucol_voff[e] : 0;
         s_f[t] = t < nc ? ucol_fst[e] - it.fst : w; // first row of the segment, relative
-        s_x[t] = t < nc ? x[ucol_gc[e]] : Sx::zero();
+        const int64_t gc = t < nc ? ucol_gc[e] : 0;
+#pragma unroll
+        for (int q = 0; q < NR; ++q) s_x[q][t] = (t < nc && q < nr) ? x[gc + q * ldx] : Sx::zero();
     }
     __syncthreads();
     for (int i = t; i < w; i += SV_THREADS) { // w <= MAX_SUPER_SIZE = 2 x SV_THREADS
-        T acc = Sx::zero();
+        T acc[NR];
+#pragma unroll
+        for (int q = 0; q < NR; ++q) acc[q] = Sx::zero();
         for (int c0 = 0; c0 < nc; c0 += UN) {
             T v[UN];
 #pragma unroll
@@ -186,9 +238,15 @@ k_sv_upanel(const SvChunk *chunks, const SvDiag *diag, const int64_t *coff, cons
                 v[u] = i >= rf ? Uval[s_v[c0 + u] + i - rf] : Sx::zero();
             }
 #pragma unroll
-            for (int u = 0; u < UN; ++u) acc = Sx::fms(acc, v[u], s_x[c0 + u]);
+            for (int q = 0; q < NR; ++q) {
+                if (q >= nr) break;
+#pragma unroll
+                for (int u = 0; u < UN; ++u) acc[q] = Sx::fms(acc[q], v[u], s_x[q][c0 + u]);
+            }
         }
-        Sx::atomic_sub(x + it.fst + i, Sx::neg(acc));
+#pragma unroll
+        for (int q = 0; q < NR; ++q)
+            if (q < nr) Sx::atomic_sub(x + it.fst + i + q * ldx, Sx::neg(acc[q]));
     }
 }
 

@@ -37,6 +37,9 @@ def _rhs(A, perm, xt):
     (STENCIL_2D5, (40, 40, 1), 0, 60, 256, 1),
     (STENCIL_3D27, (10, 10, 10), 1, 60, 256, 2),
     (STENCIL_3D7, (10, 10, 10), 2, 60, 256, 2),
+    (STENCIL_3D7, (12, 12, 12), 0, 60, 256, 10),  # batches of 8 + 2 right-hand sides
+    (STENCIL_3D27, (8, 8, 8), 1, 60, 256, 9),
+    (STENCIL_3D7, (8, 8, 8), 2, 60, 256, 5),      # complex: batches of 2
 ])
 def test_device_solve_matches_host_solve(kind, dims, dtype, relax, maxsup, nrhs):
     kw = dict(diag=6 - 0.25, diag_im=-0.0025) if dtype == 2 else {}

@@ -18,6 +18,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--nx", type=int, default=100)
     ap.add_argument("--solves", type=int, default=3)
+    ap.add_argument("--nrhs", type=int, default=1)
     a = ap.parse_args()
     A = Csc.stencil(STENCIL_3D7, a.nx, a.nx, a.nx)
     S = Symbolic(A, nd_order(a.nx, a.nx, a.nx), 60, 256)
@@ -35,11 +36,11 @@ def main():
     ts = []
     for _ in range(a.solves):
         t0 = time.perf_counter()
-        x = p.solve(b)
+        x = p.solve(b) if a.nrhs == 1 else p.solve(np.repeat(b[:, None], a.nrhs, axis=1))[:, 0]
         ts.append((time.perf_counter() - t0) * 1e3, )
         dev = p.stats()["t_solve_ms"]
     berr = float(np.abs(B @ x - b).max() / (abs(B).sum(axis=1).max() * np.abs(x).max()))
-    print(json.dumps({"nx": a.nx, "fill_ms": fill, "solve_ms_device": dev,
+    print(json.dumps({"nx": a.nx, "nrhs": a.nrhs, "fill_ms": fill, "solve_ms_device": dev,
                       "solve_ms_wall": min(ts), "berr": berr,
                       "fwd_err": float(np.abs(x - xt).max())}), flush=True)
 
