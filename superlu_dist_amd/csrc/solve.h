@@ -42,7 +42,9 @@ template <typename T> struct SvPanel { static constexpr int v = sizeof(T) == 16 
 
 // Right-hand sides: NR (compile-time, 1 or SV_NR) columns of x with leading
 // dimension ldx, of which the first nr (<= NR, uniform) are live; every
-// factor element is read once per sweep for all of them.
+// factor element is read once per sweep for all of them.  Dead columns are
+// carried as zeros through the arithmetic (never loaded or stored), so the
+// NR independent chains stay branch-free and interleave.
 constexpr int SV_NR = 8;
 template <typename T> struct SvNr { static constexpr int v = sizeof(T) == 16 ? 2 : SV_NR; }; // no spills
 
@@ -76,7 +78,6 @@ k_sv_ldiag(const SvDiag *items, const T *Lval, T *x, int64_t ldx, int nr) {
                 const bool upd = t > j0 + j && t < j0 + nj;
 #pragma unroll
                 for (int q = 0; q < NR; ++q) {
-                    if (q >= nr) break;
                     const T yj = sv_shfl(yi[q], base + j);
                     if (upd) yi[q] = Sx::fms(yi[q], l[j], yj);
                 }
@@ -89,7 +90,6 @@ k_sv_ldiag(const SvDiag *items, const T *Lval, T *x, int64_t ldx, int nr) {
         if (t >= j0 + nj && t < w) { // only for full panels (a partial one is the last)
 #pragma unroll
             for (int q = 0; q < NR; ++q) {
-                if (q >= nr) break;
 #pragma unroll
                 for (int j = 0; j < SVP; ++j) yi[q] = Sx::fms(yi[q], l[j], s_y[buf][q][j]);
             }
@@ -131,7 +131,6 @@ k_sv_udiag(const SvDiag *items, const T *Lval, T *x, int64_t ldx, int nr) {
                     const bool upd = t >= j0 && t < j0 + j;
 #pragma unroll
                     for (int q = 0; q < NR; ++q) {
-                        if (q >= nr) break;
                         if (t == j0 + j) yi[q] = Sx::div(yi[q], d);
                         const T xj = sv_shfl(yi[q], base + j);
                         if (upd) yi[q] = Sx::fms(yi[q], u[j], xj);
@@ -146,7 +145,6 @@ k_sv_udiag(const SvDiag *items, const T *Lval, T *x, int64_t ldx, int nr) {
         if (t < j0) { // the first (last-column) panel may be partial: no stale LDS
 #pragma unroll
             for (int q = 0; q < NR; ++q) {
-                if (q >= nr) break;
 #pragma unroll
                 for (int j = 0; j < SVP; ++j)
                     if (j < nj) yi[q] = Sx::fms(yi[q], u[j], s_x[buf][q][j]);
@@ -184,7 +182,6 @@ k_sv_lpanel(const SvChunk *chunks, const SvDiag *diag, const int64_t *roff, cons
         for (int u = 0; u < UN; ++u) v[u] = j0 + u < w ? L[(int64_t)(j0 + u) * it.ld] : Sx::zero();
 #pragma unroll
         for (int q = 0; q < NR; ++q) {
-            if (q >= nr) break;
 #pragma unroll
             for (int u = 0; u < UN; ++u)
                 if (j0 + u < w) acc[q] = Sx::fms(acc[q], v[u], s_y[q][j0 + u]);
@@ -239,7 +236,6 @@ k_sv_upanel(const SvChunk *chunks, const SvDiag *diag, const int64_t *coff, cons
             }
 #pragma unroll
             for (int q = 0; q < NR; ++q) {
-                if (q >= nr) break;
 #pragma unroll
                 for (int u = 0; u < UN; ++u) acc[q] = Sx::fms(acc[q], v[u], s_x[q][c0 + u]);
             }
