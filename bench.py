@@ -96,7 +96,8 @@ def next_rows(plan, A, S, anorm, one_step):
     berr = float(np.abs(r).max() / (abs(B).sum(axis=1).max() * np.abs(x).max()))
     xb = plan.solve(np.repeat(b[:, None], 8, axis=1))
     t8 = plan.stats()["t_solve_ms"]
-    assert np.abs(xb - x[:, None]).max() <= 1e-12 * np.abs(x).max()
+    # the panel sums meet through atomics: batch and single solves agree to rounding
+    assert np.abs(xb - x[:, None]).max() <= (1e-4 if x.dtype == np.float32 else 1e-12) * np.abs(x).max()
     xr, rberr, rsteps = plan.refine(b, x)
     t_ref = plan.stats()["t_refine_ms"]
     fill_ms = min(fills)
