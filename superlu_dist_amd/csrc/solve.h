@@ -31,9 +31,19 @@ struct SvChunk {    // 256 panel rows (forward) or 256 U columns (backward)
 constexpr int SV_THREADS = 256;  // panel chunks
 constexpr int SVD_THREADS = 512; // diagonal solves: one thread per row, w <= MAX_SUPER_SIZE
 
-__device__ inline double sv_shfl(double v, int src) { return __shfl(v, src, 64); }
-__device__ inline float sv_shfl(float v, int src) { return __shfl(v, src, 64); }
-__device__ inline zc sv_shfl(zc v, int src) { return {__shfl(v.r, src, 64), __shfl(v.i, src, 64)}; }
+// value of lane `src` (wavefront-uniform) for every lane: v_readlane into a
+// scalar register, no LDS round trip (tools/micro/lat_micro.hip: readlane +
+// FMA 56 cycles against 92 for an LDS load)
+__device__ inline float sv_shfl(float v, int src) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), src));
+}
+__device__ inline double sv_shfl(double v, int src) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)b, src);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), src);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+__device__ inline zc sv_shfl(zc v, int src) { return {sv_shfl(v.r, src), sv_shfl(v.i, src)}; }
 
 // columns per panel of the diagonal solves: 32 (16 complex, to keep the
 // thread's panel row in registers); divides the 64-wide wavefront, so a
