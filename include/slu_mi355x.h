@@ -258,6 +258,19 @@ void slu_symb_struct_sizes(const slu_symb *s, int64_t *sizes);
 void *slu_distribute(const slu_symb *s, const slu_csc *A, int nprow,
                      int npcol, int myrow, int mycol);
 void slu_lustruct_free(void *LUstruct, int dtype);
+/* An LUstruct (freed by slu_lustruct_free) holding given arrays in the layout
+ * pddistribute leaves (SRC/pddistribute.c:1283-1340, 1465-1493): flat index /
+ * value arrays with offsets per local block column (Loff/Lvoff, nlc entries)
+ * and block row (Uoff/Uvoff, nlr entries), -1 where the block column / row
+ * is empty; ToSendR flattened nlc x npcol.  Used to feed the engine
+ * LUstructs made by the reference's own front-end (tests/golden/refdump_*). */
+void *slu_lustruct_build(int dtype, int64_t n, int64_t nsupers, const int_t *xsup,
+                         const int_t *supno, int nprow, int npcol, const int_t *Lidx,
+                         int64_t Lidx_cnt, const int64_t *Loff, const void *Lval,
+                         int64_t Lval_cnt, const int64_t *Lvoff, const int_t *Uidx,
+                         int64_t Uidx_cnt, const int64_t *Uoff, const void *Uval,
+                         int64_t Uval_cnt, const int64_t *Uvoff, const int *ToRecv,
+                         const int *ToSendD, const int *ToSendR, const int_t *bufmax);
 
 /* Permuted-matrix helpers for tests: B = P*A*P^T in CSC. */
 slu_csc *slu_permute(const slu_csc *A, const int64_t *perm_c);

@@ -1,0 +1,134 @@
+"""ctypes mirror of the reference types that cross the pdgstrf boundary
+(include/slu_abi.h: superlu_dist_options_t SRC/superlu_defs.h:716-755,
+gridinfo_t :385-399, SuperLUStat_t SRC/util_dist.h:101-134) and a caller of
+the drop-in entry points pdgstrf / psgstrf / pzgstrf exactly as pdgssvx calls
+them (SRC/pdgssvx.c:1174-1180).
+
+Used by the tests to exercise the exported symbols themselves (argument
+checks, in-place factors, stat side effects, info) on a 1x1 grid, where the
+entry points touch no MPI.  Multi-rank grids go through the reference's own
+drivers linked against libslu_mi355x.so (oracle/_ref/p?drive_mi355x).
+"""
+import ctypes as C
+
+import numpy as np
+
+from .lib import SLU_D, SLU_S, SLU_Z, lib
+
+MPI_Comm = C.c_int  # conda MPICH: MPI_Comm is an int (SURVEY 8b ABI layout)
+NPHASES = 22        # PhaseType (SRC/superlu_enum_consts.h)
+FACT = 7
+YES, NO = 1, 0
+
+
+class ScopeT(C.Structure):
+    _fields_ = [("comm", MPI_Comm), ("Np", C.c_int), ("Iam", C.c_int)]
+
+
+class GridInfo(C.Structure):
+    _fields_ = [("comm", MPI_Comm), ("rscp", ScopeT), ("cscp", ScopeT), ("iam", C.c_int),
+                ("nprow", C.c_int64), ("npcol", C.c_int64)]
+
+
+class Options(C.Structure):
+    _fields_ = [(nm, C.c_int) for nm in ("Fact", "Equil", "DiagInv", "ColPerm", "Trans",
+                                         "IterRefine")] + \
+               [("DiagPivotThresh", C.c_double)] + \
+               [(nm, C.c_int) for nm in ("SymmetricMode", "PivotGrowth", "ConditionNumber",
+                                         "RowPerm", "ILU_DropRule")] + \
+               [("ILU_DropTol", C.c_double), ("ILU_FillFactor", C.c_double),
+                ("ILU_Norm", C.c_int), ("ILU_FillTol", C.c_double), ("ILU_MILU", C.c_int),
+                ("ILU_MILU_Dim", C.c_double)] + \
+               [(nm, C.c_int) for nm in ("ParSymbFact", "ReplaceTinyPivot", "SolveInitialized",
+                                         "RefineInitialized", "PrintStat", "lookahead_etree",
+                                         "num_lookaheads", "superlu_relax", "superlu_maxsup")] + \
+               [("superlu_rankorder", C.c_char * 4), ("superlu_lbs", C.c_char * 4)] + \
+               [(nm, C.c_int) for nm in ("superlu_n_gemm", "superlu_max_buffer_size",
+                                         "superlu_num_gpu_streams", "superlu_acc_offload",
+                                         "SymPattern", "Use_TensorCore", "Algo3d")]
+
+
+class Stat(C.Structure):
+    _fields_ = [("panel_histo", C.POINTER(C.c_int)), ("utime", C.POINTER(C.c_double)),
+                ("ops", C.POINTER(C.c_float)), ("TinyPivots", C.c_int), ("RefineSteps", C.c_int),
+                ("num_look_aheads", C.c_int), ("current_buffer", C.c_float),
+                ("peak_buffer", C.c_float), ("gpu_buffer", C.c_float),
+                ("MaxActiveBTrees", C.c_int64), ("MaxActiveRTrees", C.c_int64)]
+
+
+def default_options():
+    """set_default_options_dist (SRC/util.c:203-238), the fields pdgstrf reads."""
+    o = Options()
+    o.Equil = YES
+    o.ColPerm = 2          # MMD_AT_PLUS_A (no METIS in the image)
+    o.IterRefine = 2       # SLU_DOUBLE
+    o.RowPerm = 1          # LargeDiag_MC64
+    o.ReplaceTinyPivot = NO
+    o.PrintStat = YES
+    o.num_lookaheads = 10
+    o.superlu_relax = 60
+    o.superlu_maxsup = 256
+    o.superlu_rankorder = b"ROW"
+    o.superlu_lbs = b"GD"
+    o.superlu_n_gemm = 5000
+    o.superlu_max_buffer_size = 256000000
+    o.superlu_num_gpu_streams = 8
+    o.superlu_acc_offload = 1
+    o.SymPattern = NO
+    return o
+
+
+def grid_1x1(comm=0x44000000):
+    """A 1x1 gridinfo_t (MPICH's MPI_COMM_WORLD handle by default; a 1x1
+    pdgstrf never calls MPI)."""
+    g = GridInfo()
+    g.comm = comm
+    g.rscp.comm = g.cscp.comm = comm
+    g.rscp.Np = g.cscp.Np = 1
+    g.iam = 0
+    g.nprow = g.npcol = 1
+    return g
+
+
+def pxgstrf(lu, anorm, options=None, grid=None, m=None, n=None):
+    """Call pdgstrf / psgstrf / pzgstrf on the LUStruct ``lu`` in place, as
+    pdgssvx does.  Returns (return value, info, stat dict)."""
+    L = lib()
+    fn = {SLU_D: L.pdgstrf, SLU_S: L.psgstrf, SLU_Z: L.pzgstrf}[lu.dtype]
+    fn.restype = C.c_int64
+    anorm_t = C.c_float if lu.dtype == SLU_S else C.c_double
+    fn.argtypes = [C.POINTER(Options), C.c_int, C.c_int, anorm_t, C.c_void_p,
+                   C.POINTER(GridInfo), C.POINTER(Stat), C.POINTER(C.c_int)]
+    o = options if options is not None else default_options()
+    g = grid if grid is not None else grid_1x1()
+    utime = (C.c_double * NPHASES)()
+    ops = (C.c_float * NPHASES)()
+    st = Stat()
+    st.utime = C.cast(utime, C.POINTER(C.c_double))
+    st.ops = C.cast(ops, C.POINTER(C.c_float))
+    info = C.c_int(-999)
+    n = lu.n if n is None else n
+    m = n if m is None else m
+    rv = fn(C.byref(o), m, n, anorm, C.c_void_p(lu.ptr), C.byref(g), C.byref(st), C.byref(info))
+    return int(rv), info.value, {"ops_fact": float(ops[FACT]), "TinyPivots": st.TinyPivots,
+                                 "num_look_aheads": st.num_look_aheads,
+                                 "gpu_buffer": float(st.gpu_buffer)}
+
+
+def layout():
+    """Sizes / offsets of the mirror, in the keys of tests/golden/abi_layout.json."""
+    return {"sizeof(gridinfo_t)": C.sizeof(GridInfo), "sizeof(superlu_scope_t)": C.sizeof(ScopeT),
+            "sizeof(superlu_dist_options_t)": C.sizeof(Options),
+            "sizeof(SuperLUStat_t)": C.sizeof(Stat),
+            "gridinfo_t.nprow": GridInfo.nprow.offset, "gridinfo_t.iam": GridInfo.iam.offset,
+            "superlu_dist_options_t.ReplaceTinyPivot": Options.ReplaceTinyPivot.offset,
+            "superlu_dist_options_t.num_lookaheads": Options.num_lookaheads.offset,
+            "superlu_dist_options_t.superlu_maxsup": Options.superlu_maxsup.offset,
+            "superlu_dist_options_t.SymPattern": Options.SymPattern.offset,
+            "superlu_dist_options_t.Algo3d": Options.Algo3d.offset,
+            "SuperLUStat_t.ops": Stat.ops.offset, "SuperLUStat_t.TinyPivots": Stat.TinyPivots.offset,
+            "SuperLUStat_t.num_look_aheads": Stat.num_look_aheads.offset}
+
+
+__all__ = ["Options", "GridInfo", "Stat", "default_options", "grid_1x1", "pxgstrf", "layout",
+           "np"]

@@ -9,9 +9,11 @@
 //   * stat->ops[FACT] = algorithmic flops, stat->TinyPivots += replacements,
 //     stat->num_look_aheads = clamp(options->num_lookaheads, 0, 49);
 //   * *info = MIN over ranks of the rank's zero-pivot column (0 if none).
-// It must be called by every rank of grid->comm.  MPI is used only to
-// bootstrap RCCL for multi-rank grids; its symbols are looked up in the host
-// process at run time (this library has no link-time MPI dependency).
+// It must be called by every rank of grid->comm.  On multi-rank grids MPI
+// bootstraps RCCL (or, with several ranks per GPU, carries the host-staged
+// panel broadcasts) and reduces info; its symbols are looked up in the host
+// process at run time (this library has no link-time MPI dependency).  A 1x1
+// grid makes no MPI call.
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 
@@ -28,13 +30,34 @@
 
 namespace {
 
-typedef int (*mpi_bcast_t)(void *, int, MPI_Datatype, int, MPI_Comm);
-typedef int (*mpi_allreduce_t)(const void *, void *, int, MPI_Datatype, MPI_Op, MPI_Comm);
+// MPI is resolved from the host process at run time (no link-time MPI).
+struct Mpi {
+    int (*bcast)(void *, int, MPI_Datatype, int, MPI_Comm) = nullptr;
+    int (*allreduce)(const void *, void *, int, MPI_Datatype, MPI_Op, MPI_Comm) = nullptr;
+    int (*allgather)(const void *, int, MPI_Datatype, void *, int, MPI_Datatype, MPI_Comm) = nullptr;
+    int (*create_keyval)(MPI_Comm_copy_attr_function *, MPI_Comm_delete_attr_function *, int *,
+                         void *) = nullptr;
+    int (*set_attr)(MPI_Comm, int, void *) = nullptr;
+    int (*get_attr)(MPI_Comm, int, void *, int *) = nullptr;
+};
 
-template <typename F> F mpi_sym(const char *name) {
-    void *p = dlsym(RTLD_DEFAULT, name);
-    if (!p) throw slu::Error(slu::fmt("MPI symbol %s not found in the process", name));
-    return (F)p;
+template <typename F> void mpi_sym(F &f, const char *name) {
+    f = (F)dlsym(RTLD_DEFAULT, name);
+    if (!f) throw slu::Error(slu::fmt("MPI symbol %s not found in the process", name));
+}
+
+const Mpi &mpi() {
+    static Mpi m = [] {
+        Mpi x;
+        mpi_sym(x.bcast, "MPI_Bcast");
+        mpi_sym(x.allreduce, "MPI_Allreduce");
+        mpi_sym(x.allgather, "MPI_Allgather");
+        mpi_sym(x.create_keyval, "MPI_Comm_create_keyval");
+        mpi_sym(x.set_attr, "MPI_Comm_set_attr");
+        mpi_sym(x.get_attr, "MPI_Comm_get_attr");
+        return x;
+    }();
+    return m;
 }
 
 int pick_device(int iam) {
@@ -50,27 +73,94 @@ int pick_device(int iam) {
     return r % nd;
 }
 
+// The engine's communicators for one gridinfo_t, cached on grid->comm as an
+// MPI attribute: the delete callback runs when superlu_gridexit frees the
+// communicator, so a later grid can never pick up a stale entry (MPICH
+// reuses freed handle values).  Transport: RCCL when every rank drives its
+// own GPU; MPI broadcasts of host-staged buffers on grid->comm / rscp / cscp
+// (SRC/superlu_grid.c:158-172) when several ranks share one (RCCL refuses
+// duplicate devices) or SUPERLU_MI355X_TRANSPORT=mpi.
+struct GridComm {
+    slu_comm *c = nullptr;
+    int nprow = 0, npcol = 0, iam = -1;
+    MPI_Comm comms[3]; // grid, process row, process column
+    bool host = false;
+};
+
+int mpi_host_bcast(void *ctx, int group, int root, void *buf, int64_t bytes) {
+    GridComm *g = (GridComm *)ctx;
+    char *p = (char *)buf;
+    while (bytes > 0) {
+        const int n = (int)std::min<int64_t>(bytes, 1 << 30);
+        if (mpi().bcast(p, n, MPI_BYTE, root, g->comms[group]) != MPI_SUCCESS) return 1;
+        p += n;
+        bytes -= n;
+    }
+    return 0;
+}
+
+int grid_attr_delete(MPI_Comm, int, void *val, void *) {
+    GridComm *g = (GridComm *)val;
+    slu_comm_destroy(g->c);
+    delete g;
+    return MPI_SUCCESS;
+}
+
 std::mutex g_mu;
-std::map<long, slu_comm *> g_comms; // keyed by the grid's MPI communicator
+int g_keyval = MPI_KEYVAL_INVALID;
+std::map<int, slu_comm *> g_single; // 1x1 grids (no MPI at all), per device
 
 slu_comm *comm_for_grid(gridinfo_t *grid) {
     std::lock_guard<std::mutex> lk(g_mu);
-    long key = (long)(intptr_t)grid->comm;
-    auto it = g_comms.find(key);
-    if (it != g_comms.end()) return it->second;
-    int nprow = (int)grid->nprow, npcol = (int)grid->npcol;
-    unsigned char uid[128] = {0};
-    if (nprow * npcol > 1) {
-        if (grid->iam == 0 && slu_comm_unique_id(uid) != 0)
-            throw slu::Error(slu_last_error());
-        auto bcast = mpi_sym<mpi_bcast_t>("MPI_Bcast");
-        bcast(uid, 128, MPI_BYTE, 0, grid->comm);
+    const int nprow = (int)grid->nprow, npcol = (int)grid->npcol;
+    if (nprow * npcol == 1) {
+        const int dev = pick_device(0);
+        auto it = g_single.find(dev);
+        if (it != g_single.end()) return it->second;
+        slu_comm *c = slu_comm_create(nullptr, 1, 1, 0, dev);
+        if (!c) throw slu::Error(slu_last_error());
+        return g_single[dev] = c;
     }
-    slu_comm *c = slu_comm_create(nprow * npcol > 1 ? uid : nullptr, nprow, npcol, grid->iam,
-                                  pick_device(grid->iam));
-    if (!c) throw slu::Error(slu_last_error());
-    g_comms[key] = c;
-    return c;
+    const Mpi &M = mpi();
+    if (g_keyval == MPI_KEYVAL_INVALID)
+        M.create_keyval(MPI_COMM_NULL_COPY_FN, grid_attr_delete, &g_keyval, nullptr);
+    void *val = nullptr;
+    int flag = 0;
+    M.get_attr(grid->comm, g_keyval, &val, &flag);
+    if (flag) {
+        GridComm *g = (GridComm *)val;
+        if (g->nprow == nprow && g->npcol == npcol && g->iam == grid->iam) return g->c;
+    }
+    // collective from here on: every rank of grid->comm takes the same path
+    const int dev = pick_device(grid->iam), P = nprow * npcol;
+    std::vector<int> devs(P, -1);
+    M.allgather(&dev, 1, MPI_INT, devs.data(), 1, MPI_INT, grid->comm);
+    std::vector<int> sorted(devs);
+    std::sort(sorted.begin(), sorted.end());
+    bool host = std::adjacent_find(sorted.begin(), sorted.end()) != sorted.end();
+    if (const char *t = getenv("SUPERLU_MI355X_TRANSPORT")) host = !strcmp(t, "mpi");
+    auto *g = new GridComm;
+    g->nprow = nprow;
+    g->npcol = npcol;
+    g->iam = grid->iam;
+    g->comms[0] = grid->comm;
+    g->comms[1] = grid->rscp.comm;
+    g->comms[2] = grid->cscp.comm;
+    g->host = host;
+    if (host) {
+        g->c = slu_comm_create_host(mpi_host_bcast, g, nprow, npcol, grid->iam, dev);
+    } else {
+        unsigned char uid[128] = {0};
+        if (grid->iam == 0 && slu_comm_unique_id(uid) != 0) throw slu::Error(slu_last_error());
+        M.bcast(uid, 128, MPI_BYTE, 0, grid->comm);
+        g->c = slu_comm_create(uid, nprow, npcol, grid->iam, dev);
+    }
+    if (!g->c) {
+        delete g;
+        throw slu::Error(slu_last_error());
+    }
+    M.set_attr(grid->comm, g_keyval, g); // replaces (and deletes) a stale entry
+    return g->c;
 }
 
 template <typename LUS>
@@ -111,9 +201,8 @@ int_t pxgstrf(int dtype, const char *name, superlu_dist_options_t *options, int 
         plan = nullptr;
         int gi = myinfo ? myinfo : n + 1;
         if (grid->nprow * grid->npcol > 1) {
-            auto allreduce = mpi_sym<mpi_allreduce_t>("MPI_Allreduce");
             int in = gi;
-            allreduce(&in, &gi, 1, MPI_INT, MPI_MIN, grid->comm);
+            mpi().allreduce(&in, &gi, 1, MPI_INT, MPI_MIN, grid->comm);
         }
         *info = gi == n + 1 ? 0 : gi;
         return 0;

@@ -681,6 +681,74 @@ void *distribute_t(const slu_symb *S, const slu_csc *A, int Pr, int Pc,
     return LU;
 }
 
+// An LUstruct holding arrays made elsewhere (e.g. dumped from the reference's
+// own pddistribute, tests/golden/refdump_*): the flat index / value arrays
+// with per local block column / row offsets (-1 = empty), laid out as
+// SRC/pddistribute.c:1283-1340, 1465-1493 lays out its *_dat arrays.
+template <typename T, typename LocalLU, typename LUstruct>
+void *build_t(int64_t n, int64_t ns, const int_t *xsup, const int_t *supno, int Pr, int Pc,
+              const int_t *Lidx, int64_t Lidx_cnt, const int64_t *Loff, const void *Lval,
+              int64_t Lval_cnt, const int64_t *Lvoff, const int_t *Uidx, int64_t Uidx_cnt,
+              const int64_t *Uoff, const void *Uval, int64_t Uval_cnt, const int64_t *Uvoff,
+              const int *ToRecv, const int *ToSendD, const int *ToSendR, const int_t *bufmax) {
+    LUstruct *LU = (LUstruct *)calloc(1, sizeof(LUstruct));
+    LU->Glu_persist = (Glu_persist_t *)calloc(1, sizeof(Glu_persist_t));
+    LU->Glu_persist->xsup = (int_t *)malloc((ns + 1) * sizeof(int_t));
+    LU->Glu_persist->supno = (int_t *)malloc(n * sizeof(int_t));
+    std::copy(xsup, xsup + ns + 1, LU->Glu_persist->xsup);
+    std::copy(supno, supno + n, LU->Glu_persist->supno);
+    LocalLU *Llu = (LocalLU *)calloc(1, sizeof(LocalLU));
+    LU->Llu = Llu;
+    LU->dt = sizeof(T) == 4 ? 's' : sizeof(T) == 8 ? 'd' : 'z';
+    const int64_t nlc = (ns + Pc - 1) / Pc, nlr = (ns + Pr - 1) / Pr;
+    for (int i = 0; i < SLU_NBUFFERS; ++i) Llu->bufmax[i] = bufmax[i];
+    Llu->Lrowind_bc_dat = (int_t *)calloc(Lidx_cnt + 1, sizeof(int_t));
+    Llu->Lnzval_bc_dat = (T *)calloc(Lval_cnt + 1, sizeof(T));
+    Llu->Lrowind_bc_cnt = Lidx_cnt + 1;
+    Llu->Lnzval_bc_cnt = Lval_cnt + 1;
+    if (Lidx_cnt) memcpy(Llu->Lrowind_bc_dat, Lidx, Lidx_cnt * sizeof(int_t));
+    if (Lval_cnt) memcpy(Llu->Lnzval_bc_dat, Lval, Lval_cnt * sizeof(T));
+    Llu->Lrowind_bc_ptr = (int_t **)calloc(std::max<int64_t>(nlc, 1), sizeof(int_t *));
+    Llu->Lnzval_bc_ptr = (T **)calloc(std::max<int64_t>(nlc, 1), sizeof(T *));
+    Llu->Lrowind_bc_offset = (long *)malloc(std::max<int64_t>(nlc, 1) * sizeof(long));
+    Llu->Lnzval_bc_offset = (long *)malloc(std::max<int64_t>(nlc, 1) * sizeof(long));
+    for (int64_t j = 0; j < nlc; ++j) {
+        Llu->Lrowind_bc_offset[j] = Loff[j];
+        Llu->Lnzval_bc_offset[j] = Lvoff[j];
+        if (Loff[j] >= 0) {
+            Llu->Lrowind_bc_ptr[j] = Llu->Lrowind_bc_dat + Loff[j];
+            Llu->Lnzval_bc_ptr[j] = Llu->Lnzval_bc_dat + Lvoff[j];
+        }
+    }
+    Llu->Ufstnz_br_dat = (int_t *)calloc(Uidx_cnt + 1, sizeof(int_t));
+    Llu->Unzval_br_dat = (T *)calloc(Uval_cnt + 1, sizeof(T));
+    Llu->Ufstnz_br_cnt = Uidx_cnt + 1;
+    Llu->Unzval_br_cnt = Uval_cnt + 1;
+    if (Uidx_cnt) memcpy(Llu->Ufstnz_br_dat, Uidx, Uidx_cnt * sizeof(int_t));
+    if (Uval_cnt) memcpy(Llu->Unzval_br_dat, Uval, Uval_cnt * sizeof(T));
+    Llu->Ufstnz_br_ptr = (int_t **)calloc(std::max<int64_t>(nlr, 1), sizeof(int_t *));
+    Llu->Unzval_br_ptr = (T **)calloc(std::max<int64_t>(nlr, 1), sizeof(T *));
+    Llu->Ufstnz_br_offset = (long *)malloc(std::max<int64_t>(nlr, 1) * sizeof(long));
+    Llu->Unzval_br_offset = (long *)malloc(std::max<int64_t>(nlr, 1) * sizeof(long));
+    for (int64_t j = 0; j < nlr; ++j) {
+        Llu->Ufstnz_br_offset[j] = Uoff[j];
+        Llu->Unzval_br_offset[j] = Uvoff[j];
+        if (Uoff[j] >= 0) {
+            Llu->Ufstnz_br_ptr[j] = Llu->Ufstnz_br_dat + Uoff[j];
+            Llu->Unzval_br_ptr[j] = Llu->Unzval_br_dat + Uvoff[j];
+        }
+    }
+    Llu->ToRecv = (int *)calloc(std::max<int64_t>(ns, 1), sizeof(int));
+    Llu->ToSendD = (int *)calloc(std::max<int64_t>(nlr, 1), sizeof(int));
+    Llu->ToSendR = (int **)malloc(std::max<int64_t>(nlc, 1) * sizeof(int *));
+    int *tsr = (int *)malloc(std::max<int64_t>(nlc * Pc, 1) * sizeof(int));
+    if (ToRecv) memcpy(Llu->ToRecv, ToRecv, ns * sizeof(int));
+    if (ToSendD) memcpy(Llu->ToSendD, ToSendD, nlr * sizeof(int));
+    for (int64_t i = 0; i < nlc * Pc; ++i) tsr[i] = ToSendR ? ToSendR[i] : SLU_EMPTY;
+    for (int64_t i = 0; i < nlc; ++i) Llu->ToSendR[i] = tsr + i * Pc;
+    return LU;
+}
+
 template <typename LocalLU, typename LUstruct>
 void free_t(void *p) {
     LUstruct *LU = (LUstruct *)p;
@@ -743,6 +811,25 @@ void *slu_distribute(const slu_symb *s, const slu_csc *A, int nprow,
     case SLU_S: return distribute_t<float, sLocalLU_t, sLUstruct_t>(s, A, nprow, npcol, myrow, mycol);
     case SLU_Z: return distribute_t<doublecomplex, zLocalLU_t, zLUstruct_t>(s, A, nprow, npcol, myrow, mycol);
     }
+    return nullptr;
+}
+
+void *slu_lustruct_build(int dtype, int64_t n, int64_t nsupers, const int_t *xsup,
+                         const int_t *supno, int nprow, int npcol, const int_t *Lidx,
+                         int64_t Lidx_cnt, const int64_t *Loff, const void *Lval, int64_t Lval_cnt,
+                         const int64_t *Lvoff, const int_t *Uidx, int64_t Uidx_cnt,
+                         const int64_t *Uoff, const void *Uval, int64_t Uval_cnt,
+                         const int64_t *Uvoff, const int *ToRecv, const int *ToSendD,
+                         const int *ToSendR, const int_t *bufmax) {
+#define SLU_BUILD_ARGS                                                                             \
+    n, nsupers, xsup, supno, nprow, npcol, Lidx, Lidx_cnt, Loff, Lval, Lval_cnt, Lvoff, Uidx,      \
+        Uidx_cnt, Uoff, Uval, Uval_cnt, Uvoff, ToRecv, ToSendD, ToSendR, bufmax
+    switch (dtype) {
+    case SLU_D: return build_t<double, dLocalLU_t, dLUstruct_t>(SLU_BUILD_ARGS);
+    case SLU_S: return build_t<float, sLocalLU_t, sLUstruct_t>(SLU_BUILD_ARGS);
+    case SLU_Z: return build_t<doublecomplex, zLocalLU_t, zLUstruct_t>(SLU_BUILD_ARGS);
+    }
+#undef SLU_BUILD_ARGS
     return nullptr;
 }
 

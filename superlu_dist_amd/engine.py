@@ -77,7 +77,7 @@ class Plan:
         err = C.create_string_buffer(1024)
         iam = lu.myrow * lu.npcol + lu.mycol
         self.comm = comm
-        self.ptr = lib().slu_plan_create(lu.dtype, lu.ptr, lu.symb.n, lu.nprow, lu.npcol, iam,
+        self.ptr = lib().slu_plan_create(lu.dtype, lu.ptr, lu.n, lu.nprow, lu.npcol, iam,
                                          comm.ptr if comm is not None else None, C.byref(o),
                                          err, len(err))
         if not self.ptr:

@@ -118,16 +118,52 @@ class Symbolic:
 
 
 class LUStruct:
-    """One rank's LUstruct (dLUstruct_t / sLUstruct_t / zLUstruct_t) built by
-    the library; exposes its flat arrays as numpy views."""
+    """One rank's LUstruct (dLUstruct_t / sLUstruct_t / zLUstruct_t) owned by
+    the library; exposes its flat arrays as numpy views.  Built either by our
+    front-end (``Symbolic.distribute``) or from given arrays (``from_arrays``,
+    e.g. the reference's own pddistribute output in tests/golden/refdump_*)."""
 
     def __init__(self, symb, nprow, npcol, myrow, mycol):
         self.symb = symb
-        self.dtype = symb.A.dtype
-        self.nprow, self.npcol, self.myrow, self.mycol = nprow, npcol, myrow, mycol
-        self.ptr = lib().slu_distribute(symb.ptr, symb.A.ptr, nprow, npcol, myrow, mycol)
-        if not self.ptr:
+        ptr = lib().slu_distribute(symb.ptr, symb.A.ptr, nprow, npcol, myrow, mycol)
+        if not ptr:
             raise RuntimeError("slu_distribute failed")
+        self._wrap(ptr, symb.A.dtype, symb.n, symb.nsupers, nprow, npcol, myrow, mycol)
+
+    @classmethod
+    def from_arrays(cls, dtype, n, xsup, supno, nprow, npcol, myrow, mycol, Lidx, Loff, Lval,
+                    Lvoff, Uidx, Uoff, Uval, Uvoff, ToRecv=None, ToSendD=None, ToSendR=None,
+                    bufmax=None):
+        self = cls.__new__(cls)
+        self.symb = None
+        npt = DTYPES[dtype]
+        i64 = lambda a: np.ascontiguousarray(a, dtype=np.int64)  # noqa: E731
+        i32 = lambda a: None if a is None else np.ascontiguousarray(a, dtype=np.int32)  # noqa: E731
+        xsup, supno = i64(xsup), i64(supno)
+        Lidx, Loff, Lvoff, Uidx, Uoff, Uvoff = map(i64, (Lidx, Loff, Lvoff, Uidx, Uoff, Uvoff))
+        Lval = np.ascontiguousarray(Lval, dtype=npt)
+        Uval = np.ascontiguousarray(Uval, dtype=npt)
+        ToRecv, ToSendD, ToSendR = i32(ToRecv), i32(ToSendD), i32(ToSendR)
+        bufmax = i64(bufmax if bufmax is not None else np.zeros(5))
+        ns = len(xsup) - 1
+        ip = lambda a: None if a is None else a.ctypes.data_as(C.POINTER(C.c_int))  # noqa: E731
+        ptr = lib().slu_lustruct_build(dtype, n, ns, as_i64p(xsup), as_i64p(supno), nprow, npcol,
+                                       as_i64p(Lidx), len(Lidx), as_i64p(Loff),
+                                       Lval.ctypes.data_as(C.c_void_p), len(Lval), as_i64p(Lvoff),
+                                       as_i64p(Uidx), len(Uidx), as_i64p(Uoff),
+                                       Uval.ctypes.data_as(C.c_void_p), len(Uval), as_i64p(Uvoff),
+                                       ip(ToRecv), ip(ToSendD), ip(ToSendR), as_i64p(bufmax))
+        if not ptr:
+            raise RuntimeError("slu_lustruct_build failed")
+        self._wrap(ptr, dtype, n, ns, nprow, npcol, myrow, mycol)
+        return self
+
+    def _wrap(self, ptr, dtype, n, nsupers, nprow, npcol, myrow, mycol):
+        self.ptr = ptr
+        self.dtype = dtype
+        self.n = n
+        self.nsupers = nsupers
+        self.nprow, self.npcol, self.myrow, self.mycol = nprow, npcol, myrow, mycol
         v = SluLuView()
         lib().slu_lu_get_view(self.ptr, self.dtype, C.byref(v))
         self.view = v
@@ -137,7 +173,7 @@ class LUStruct:
         self.Uidx = np.ctypeslib.as_array(v.Uidx, shape=(v.Uidx_cnt,))
         self.Lval = np.frombuffer((C.c_char * (v.Lval_cnt * isz)).from_address(v.Lval), dtype=npt)
         self.Uval = np.frombuffer((C.c_char * (v.Uval_cnt * isz)).from_address(v.Uval), dtype=npt)
-        ns = symb.nsupers
+        ns = nsupers
         self.nlc = (ns + npcol - 1) // npcol
         self.nlr = (ns + nprow - 1) // nprow
         self.Loff = np.ctypeslib.as_array(v.Lidx_off, shape=(self.nlc,))

@@ -116,6 +116,7 @@ def factor_error(lus, ref):
         for mine, r in ((lu.Lval, Lr), (lu.Uval, Ur)):
             if len(r) == 0:
                 continue
+            mine = mine[:len(r)]  # library-built *_dat arrays carry one spare element
             if not np.isfinite(mine).all():
                 return float("inf")  # max() below would drop a NaN
             d = np.abs(mine.astype(np.complex128) - r.astype(np.complex128)).max()

@@ -57,10 +57,19 @@ def _worker(rank, world, port, recipe, out_dir, device, fill=False):
         import cases
         from superlu_dist_amd.engine import Comm, Plan
         from superlu_dist_amd.frontend import Symbolic
-        A, perm, dtype, (pr, pc), relax, maxsup, tiny = recipe()
-        gg = GlooGrid(rank, pr, pc)
-        S = Symbolic(A, perm, relax, maxsup)
-        lu = S.distribute(pr, pc, rank // pc, rank % pc)
+        if isinstance(recipe, str):  # "refdump:<case>": the reference's own LUstruct
+            from refdump import Fixture
+            fx = Fixture(recipe.split(":", 1)[1])
+            pr, pc, tiny, anorm = fx.pr, fx.pc, fx.replace_tiny, fx.anorm
+            gg = GlooGrid(rank, pr, pc)
+            lu = fx.lu(rank)
+            A = S = None
+        else:
+            A, perm, dtype, (pr, pc), relax, maxsup, tiny = recipe()
+            anorm = cases.anorm(A)
+            gg = GlooGrid(rank, pr, pc)
+            S = Symbolic(A, perm, relax, maxsup)
+            lu = S.distribute(pr, pc, rank // pc, rank % pc)
         res = {}
         if device is not None:
             comm = Comm.host(pr, pc, rank, device, gg.bcast)
@@ -71,7 +80,7 @@ def _worker(rank, world, port, recipe, out_dir, device, fill=False):
                 p.fill_a(v)
             else:
                 p.upload()
-            info, ntiny = p.factor(cases.anorm(A))
+            info, ntiny = p.factor(anorm)
             p.download()
             st = p.stats()
             res = dict(info=info, tiny=ntiny, flops=st["schur_flops"] + st["panel_flops"],
@@ -96,7 +105,8 @@ def _worker(rank, world, port, recipe, out_dir, device, fill=False):
 
 def run_grid(recipe, pr, pc, out_dir, device=0, timeout=240, fill=False):
     """Run ``recipe`` (picklable callable returning cases.build()-style
-    tuples) on a pr x pc grid; returns the per-rank result dicts.
+    tuples, or "refdump:<case>" for the per-rank LUstructs of a reference
+    dump fixture) on a pr x pc grid; returns the per-rank result dicts.
 
     The parent never imports torch: torch bundles its own ROCm runtime, and a
     process that loads libslu_mi355x.so (system ROCm) before torch ends up

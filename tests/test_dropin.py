@@ -1,0 +1,79 @@
+"""The drop-in promise end to end: the reference's own drivers
+EXAMPLE/p[dsz]drive.c, linked against libslu_mi355x.so FIRST and then the
+reference library with pdgstrf.o / psgstrf.o / pzgstrf.o removed
+(oracle/_ref/p?drive_mi355x, built by `make -C oracle dropin`), run the
+reference's whole pipeline -- matrix read, equilibration, MC64, MMD, symbfact,
+pddistribute, OUR p?gstrf, the reference pdgstrs / pdgsrfs -- and must solve
+as accurately as the same drivers linked with the reference factorization
+(oracle/_ref/p?drive_ref).
+
+GPU: 1 rank (1x1 grid), and 4 ranks on a 2x2 grid sharing the box's one GPU
+(the library then carries the panel broadcasts over MPI instead of RCCL).
+CPU: the link itself (our pdgstrf is the one the binary binds).
+"""
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+from conftest import ROOT
+
+REF = os.path.join(ROOT, "oracle", "_ref")
+MPIEXEC = "/opt/conda/bin/mpiexec"
+MAT = os.path.join(ROOT, "tests", "golden", "matrices")
+
+
+def _have(*names):
+    return all(os.path.exists(os.path.join(REF, n)) for n in names) and os.path.exists(MPIEXEC)
+
+
+def _run(exe, nprocs, args, matrix, timeout=240):
+    env = dict(os.environ)
+    env.update({"OMP_NUM_THREADS": "1", "MKL_NUM_THREADS": "1", "MKL_THREADING_LAYER": "SEQUENTIAL",
+                "HSA_ENABLE_IPC_MODE_LEGACY": "0"})
+    cmd = [MPIEXEC, "-n", str(nprocs), os.path.join(REF, exe)] + args + [os.path.join(MAT, matrix)]
+    r = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=timeout)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, f"{exe} failed ({r.returncode}):\n{out[-3000:]}"
+    assert "ERROR: INFO" not in out, out[-2000:]
+    errs = [float(x) for x in re.findall(r"\|\|X-Xtrue\|\|/\|\|X\|\| = ([0-9.eE+-]+)", out)]
+    assert errs, out[-2000:]
+    m = re.search(r"FACTOR time\s+([0-9.]+)", out)
+    return max(errs), (float(m.group(1)) if m else None), out
+
+
+@pytest.mark.skipif(not _have("pddrive_mi355x"), reason="drop-in drivers not built")
+def test_dropin_driver_binds_our_pdgstrf():
+    exe = os.path.join(REF, "pddrive_mi355x")
+    dyn = subprocess.run(["readelf", "-d", exe], capture_output=True, text=True).stdout
+    assert "libslu_mi355x.so" in dyn
+    und = subprocess.run(["nm", "-D", "--undefined-only", exe], capture_output=True,
+                         text=True).stdout.split()
+    assert "pdgstrf" in und            # resolved at load time from libslu_mi355x.so
+    defined = subprocess.run(["nm", "--defined-only", exe], capture_output=True, text=True).stdout
+    assert not re.search(r"\bT pdgstrf\b", defined)   # no reference pdgstrf inside
+
+
+CASES = [
+    # driver, matrix, extra args
+    ("pddrive", "g20.rua", []),
+    ("pddrive", "big.rua", []),
+    ("psdrive", "g20.rua", []),
+    ("pzdrive", "cg20.cua", []),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not _have("pddrive_mi355x", "pddrive_ref"), reason="drivers not built")
+@pytest.mark.parametrize("nprocs,grid", [(1, ["-r", "1", "-c", "1"]), (4, ["-r", "2", "-c", "2"])])
+@pytest.mark.parametrize("drv,matrix,extra", CASES)
+def test_reference_driver_with_our_factorization(drv, matrix, extra, nprocs, grid):
+    args = grid + ["-q", "2"] + extra      # MMD_AT_PLUS_A: METIS is not in the image
+    ref_err, ref_t, _ = _run(f"{drv}_ref", nprocs, args, matrix)
+    my_err, my_t, out = _run(f"{drv}_mi355x", nprocs, args, matrix)
+    tol = 1e-4 if drv == "psdrive" else 1e-12
+    print(f"{drv} {matrix} {nprocs} ranks: ||x-xtrue||/||x|| ref {ref_err:.3e} mi355x {my_err:.3e}; "
+          f"FACTOR time ref {ref_t} s, mi355x {my_t} s")
+    assert my_err <= max(10 * ref_err, tol), (my_err, ref_err)
