@@ -114,6 +114,58 @@ def next_rows(plan, A, S, anorm, one_step):
                        "fwd_err": float(np.abs(xr - xt).max() / np.abs(xt).max())}}
 
 
+def abi_leg(lu, anorm, factor_ms):
+    """utime[FACT] of the drop-in path: pdgstrf called through the C ABI the
+    way pdgssvx calls it (SRC/pdgssvx.c:1174-1180) -- plan build, H2D of the
+    host LUstruct's values, factorization and D2H of the factors into the
+    same host arrays, wall-clocked around the call -- and the same sequence
+    through the engine API for the breakdown.  The H2D overlaps the plan
+    build and each level's factors go back while later levels run."""
+    from superlu_dist_amd import capi
+    from superlu_dist_amd.engine import Plan
+    L0, U0 = lu.Lval.copy(), lu.Uval.copy()
+    walls = []
+    for _ in range(2):  # first call of the process (HIP / pinned-pool set-up), then warm
+        lu.Lval[:] = L0
+        lu.Uval[:] = U0
+        t = time.perf_counter()
+        rv, info, st = capi.pxgstrf(lu, anorm)
+        walls.append((time.perf_counter() - t) * 1e3)
+        assert rv == 0 and info == 0, (rv, info)
+    Lf = lu.Lval.copy()
+    lu.Lval[:] = L0
+    lu.Uval[:] = U0
+    t = time.perf_counter()
+    p = Plan(lu, overlap_upload=True, overlap_download=True)
+    p.upload()
+    t_fact = time.perf_counter()
+    p.factor(anorm)
+    t_end = time.perf_counter()
+    p.download()
+    st = p.stats()
+    del p
+    same = bool(np.array_equal(Lf[:-1], lu.Lval[:-1]))
+    lu.Lval[:] = L0
+    lu.Uval[:] = U0
+    h2d = st["t_upload_ms"]
+    pcie = 56.0  # GB/s, registered H2D / D2H on the box (profiles/r02_pcie_micro.json)
+    return {"utime_fact_ms": round(walls[1], 1), "utime_fact_ms_first_call": round(walls[0], 1),
+            "bar_ms": round(1.2 * (h2d + factor_ms), 1),
+            "breakdown_ms": {"plan_build": round(st["t_plan_ms"], 1),
+                             "h2d_values": round(h2d, 1),
+                             "h2d_wait_after_plan": round(st["t_upload_wait_ms"], 1),
+                             "factor_with_overlapped_d2h": round((t_end - t_fact) * 1e3, 1),
+                             "d2h_span": round(st["t_d2h_ms"], 1),
+                             "d2h_after_factor": round(st["t_d2h_tail_ms"], 1),
+                             "total": round((t_end - t) * 1e3, 1)},
+            "h2d_gbs": round(st["h2d_bytes"] / h2d / 1e6, 1) if h2d else None,
+            "d2h_copies": int(st["n_d2h_copies"]),
+            "pcie_floor_ms": round((st["h2d_bytes"] + st["d2h_bytes"]) / pcie / 1e6, 1),
+            "factors_identical_abi_vs_engine": same,
+            "note": "factor_ms in bar_ms = ms_per_step (HBM-resident); h2d = staged H2D of the "
+                    "L/U values (hostio.h); D2H rides under the factorization"}
+
+
 def one_norm(A):
     """||A||_1 (max column sum of |a_ij|), the anorm pdgssvx passes to pdgstrf."""
     colptr, _, val = A.arrays()
@@ -160,6 +212,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-next", action="store_true",
                     help="skip the device fill / solve measurements (SURVEY 8(f) rows 1-2)")
+    ap.add_argument("--no-abi", action="store_true",
+                    help="skip the drop-in pdgstrf leg (utime[FACT] incl. host copies)")
     ap.add_argument("--level-log", action="store_true",
                     help="per-level phase breakdown of the last step on stderr")
     ap.add_argument("--roofline-only", action="store_true",
@@ -264,6 +318,11 @@ def main():
     nxt = None
     if world == 1 and not args.no_next and not args.roofline_only:
         nxt = next_rows(plan, A, S, anorm, one_step)
+    abi = None
+    if world == 1 and not args.no_abi and not args.roofline_only:
+        t_step_local = float(np.mean(times)) * 1e3
+        del plan
+        abi = abi_leg(lu, anorm, t_step_local)
     if args.roofline_only:
         if rank == 0:
             print(json.dumps({"roofline_only": True, "t_schur_big_ms": sst["t_schur_big_ms"],
@@ -339,6 +398,7 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
             "next_rows": nxt,
+            "abi_pdgstrf": abi,
             "phases_ms_per_step_rank0": {k[2:-3]: round(v / K, 3) for k, v in acc.items()},
             "setup_s": {"frontend": round(t_front, 2), "plan": round(t_plan, 2),
                         "h2d_upload_pcie": round(t_upload, 2)},

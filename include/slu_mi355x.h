@@ -8,13 +8,17 @@
  *      pdgstrf  -- SRC/superlu_ddefs.h:530-531, implemented at SRC/pdgstrf.c:242
  *      psgstrf  -- SRC/superlu_sdefs.h:507,     implemented at SRC/psgstrf.c
  *      pzgstrf  -- SRC/superlu_zdefs.h:507,     implemented at SRC/pzgstrf.c
- *      dscatter_l / dscatter_l_1 / dscatter_u   SRC/superlu_ddefs.h:519-528 (+ s/z),
+ *      dscatter_l / dscatter_u   SRC/superlu_ddefs.h:519-528 (+ s/z),
+ *      dscatter_l_1              SRC/dscatter.c:29-43 (no header prototype; its
+ *                                usub / lsub are int *, not int_t *),
  *        exported because the reference's pdgstrf.c.o defines them
  *        (SRC/pdgstrf.c:171 #includes SRC/dscatter.c) and dscatter3d.c.o
  *        still references them after pdgstrf.c.o is removed.
- *    pdgstrf reads the MPI communicators in gridinfo_t only to bootstrap RCCL
- *    (the MPI symbols are resolved from the host process at run time, so this
- *    library has no link-time MPI dependency).
+ *    On multi-rank grids pdgstrf uses the MPI communicators in gridinfo_t to
+ *    bootstrap RCCL (or, when ranks share a GPU, to carry the host-staged
+ *    panel broadcasts) and for the final info reduction; the MPI symbols are
+ *    resolved from the host process at run time, so this library has no
+ *    link-time MPI dependency.
  *
  * 2. Engine API (no MPI): the same factorization driven by a caller that
  *    bootstraps RCCL itself (bench.py / tests through torch.distributed).
@@ -48,7 +52,7 @@ int_t pzgstrf(superlu_dist_options_t *options, int m, int n, double anorm,
 
 void dscatter_l_1(int ib, int ljb, int nsupc, int_t iukp, int_t *xsup,
                   int klst, int nbrow, int_t lptr, int temp_nbrow,
-                  int_t *usub, int_t *lsub, double *tempv,
+                  int *usub, int *lsub, double *tempv,
                   int *indirect_thread, int_t **Lrowind_bc_ptr,
                   double **Lnzval_bc_ptr, gridinfo_t *grid);
 void dscatter_l(int ib, int ljb, int nsupc, int_t iukp, int_t *xsup,
@@ -64,7 +68,7 @@ void dscatter_u(int ib, int jb, int nsupc, int_t iukp, int_t *xsup,
                 gridinfo_t *grid);
 void sscatter_l_1(int ib, int ljb, int nsupc, int_t iukp, int_t *xsup,
                   int klst, int nbrow, int_t lptr, int temp_nbrow,
-                  int_t *usub, int_t *lsub, float *tempv,
+                  int *usub, int *lsub, float *tempv,
                   int *indirect_thread, int_t **Lrowind_bc_ptr,
                   float **Lnzval_bc_ptr, gridinfo_t *grid);
 void sscatter_l(int ib, int ljb, int nsupc, int_t iukp, int_t *xsup,
@@ -80,7 +84,7 @@ void sscatter_u(int ib, int jb, int nsupc, int_t iukp, int_t *xsup,
                 gridinfo_t *grid);
 void zscatter_l_1(int ib, int ljb, int nsupc, int_t iukp, int_t *xsup,
                   int klst, int nbrow, int_t lptr, int temp_nbrow,
-                  int_t *usub, int_t *lsub, doublecomplex *tempv,
+                  int *usub, int *lsub, doublecomplex *tempv,
                   int *indirect_thread, int_t **Lrowind_bc_ptr,
                   doublecomplex **Lnzval_bc_ptr, gridinfo_t *grid);
 void zscatter_l(int ib, int ljb, int nsupc, int_t iukp, int_t *xsup,
@@ -124,7 +128,16 @@ typedef struct {
     int replace_tiny_pivot; /* options->ReplaceTinyPivot */
     int timing;             /* 1: per-phase HIP events; 2: + per-level log on stderr */
     int serial;             /* 1: one stream, no look-ahead overlap (kernel profiling) */
-    int reserved[5];
+    int overlap_upload;     /* 1: slu_plan_create starts the H2D copy of the L/U
+                               values as soon as their HBM is allocated and
+                               builds the rest of the plan meanwhile;
+                               slu_plan_upload then waits for it */
+    int overlap_download;   /* 1: slu_plan_factor copies each finished level's
+                               L columns / U rows back into the host LUstruct
+                               while later levels are factored (the
+                               factors are final once their level's panels
+                               are done); slu_plan_download is then a no-op */
+    int reserved[3];
 } slu_engine_opts;
 
 /* A plan = device-resident factors + every index table the kernels use.
@@ -202,6 +215,16 @@ typedef struct {
     double t_solve_ms;         /* device time of the last slu_plan_solve */
     double t_fill_ms;          /* device time of the last slu_plan_fill_a */
     double t_refine_ms;        /* device time of the last slu_plan_refine */
+    /* host wall times of the drop-in path (ms) */
+    double t_plan_ms;          /* slu_plan_create */
+    double t_upload_ms;        /* H2D of the L/U values (overlapped with the
+                                  plan build when opts.overlap_upload) */
+    double t_upload_wait_ms;   /* of which slu_plan_upload still waited */
+    double t_d2h_ms;           /* D2H of the factors (overlap_download: the
+                                  helper thread's whole span) */
+    double t_d2h_tail_ms;      /* D2H after the device finished the factorization */
+    double h2d_bytes, d2h_bytes;
+    int64_t n_d2h_copies;
 } slu_plan_stats;
 int slu_plan_get_stats(const slu_plan *p, slu_plan_stats *st);
 

@@ -184,6 +184,12 @@ int_t pxgstrf(int dtype, const char *name, superlu_dist_options_t *options, int 
         slu_comm *c = comm_for_grid(grid);
         slu_engine_opts eo{};
         eo.replace_tiny_pivot = options->ReplaceTinyPivot == SLU_YES;
+        // utime[FACT] (SRC/pdgssvx.c:1174-1180) covers the copies too: the
+        // H2D of the values runs beside the plan build, and each level's
+        // finished factors go back to the host arrays while later levels
+        // are factored (SUPERLU_MI355X_OVERLAP=0 turns both off)
+        const char *ov = getenv("SUPERLU_MI355X_OVERLAP");
+        eo.overlap_upload = eo.overlap_download = !(ov && !strcmp(ov, "0"));
         char err[512] = {0};
         plan = slu_plan_create(dtype, LUstruct, n, (int)grid->nprow, (int)grid->npcol, grid->iam,
                                c, &eo, err, sizeof err);
@@ -220,9 +226,11 @@ int_t pxgstrf(int dtype, const char *name, superlu_dist_options_t *options, int 
 template <typename T> inline void vsub(T &a, const T &b) { a -= b; }
 inline void vsub(doublecomplex &a, const doublecomplex &b) { a.r -= b.r; a.i -= b.i; }
 
+// dscatter_l_1 is defined with 32-bit usub / lsub (SRC/dscatter.c:29-43; it
+// has no prototype in the headers), unlike dscatter_l / dscatter_u.
 template <typename T>
 void scatter_l_1(int ib, int ljb, int nsupc, int_t iukp, int_t *xsup, int klst, int nbrow,
-                 int_t lptr, int temp_nbrow, int_t *usub, int_t *lsub, T *tempv,
+                 int_t lptr, int temp_nbrow, int *usub, int *lsub, T *tempv,
                  int *indirect_thread, int_t **Lrowind_bc_ptr, T **Lnzval_bc_ptr) {
     int_t *index = Lrowind_bc_ptr[ljb];
     int_t ldv = index[1], lptrj = SLU_BC_HEADER, luptrj = 0;
@@ -313,7 +321,7 @@ int_t pzgstrf(superlu_dist_options_t *options, int m, int n, double anorm,
 
 #define SLU_SCATTER_EXPORTS(P, T)                                                              \
     void P##scatter_l_1(int ib, int ljb, int nsupc, int_t iukp, int_t *xsup, int klst,          \
-                        int nbrow, int_t lptr, int temp_nbrow, int_t *usub, int_t *lsub,        \
+                        int nbrow, int_t lptr, int temp_nbrow, int *usub, int *lsub,            \
                         T *tempv, int *indirect_thread, int_t **Lrowind_bc_ptr,                 \
                         T **Lnzval_bc_ptr, gridinfo_t *) {                                      \
         scatter_l_1<T>(ib, ljb, nsupc, iukp, xsup, klst, nbrow, lptr, temp_nbrow, usub, lsub,   \

@@ -34,12 +34,14 @@
 #include <numeric>
 #include <string>
 #include <type_traits>
+#include <thread>
 #include <vector>
 
 #include "common.h"
 #include "kernels.h"
 #include "fill.h"
 #include "solve.h"
+#include "hostio.h"
 #include "slu_mi355x.h"
 
 using std::vector;
@@ -350,15 +352,43 @@ struct Plan : PlanBase {
         nlr = (nsupers + Pr - 1) / Pr;
         for (int k = 0; k < nsupers; ++k)
             SLU_REQUIRE(W(k) <= 512, "supernode %d has %d columns (> MAX_SUPER_SIZE 512)", k, W(k));
+        const auto t0 = std::chrono::steady_clock::now();
         build_local();
-        exchange_index();
-        compute_levels();
-        layout_values();
-        build_schedule();
-        build_device();
+        d_L.alloc(std::max<i64>(lval_total, 1));
+        d_U.alloc(std::max<i64>(uval_total, 1));
+        if (opts.overlap_upload) {
+            // the H2D copy of the values runs beside the rest of the plan
+            // build (index exchange, levels, schedule, device tables)
+            up_thread = std::thread([this] {
+                try {
+                    HIPCHK(hipSetDevice(comm ? comm->device : 0));
+                    upload_values();
+                } catch (const std::exception &e) {
+                    up_err = e.what();
+                }
+            });
+        }
+        try {
+            exchange_index();
+            compute_levels();
+            layout_values();
+            build_schedule();
+            build_device();
+            build_d2h();
+        } catch (...) {
+            if (up_thread.joinable()) up_thread.join();
+            throw;
+        }
+        stats.t_plan_ms = ms_since(t0);
+    }
+
+    static double ms_since(std::chrono::steady_clock::time_point t0) {
+        return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0)
+            .count();
     }
 
     ~Plan() override {
+        if (up_thread.joinable()) up_thread.join();
         for (auto e : ev_pan) (void)hipEventDestroy(e);
         for (auto e : ev_rest) (void)hipEventDestroy(e);
         if (ev_start) (void)hipEventDestroy(ev_start);
@@ -749,8 +779,6 @@ struct Plan : PlanBase {
     // ------------------------------------------------------- schedule
     void build_schedule() {
         // value buffers first: work items point straight into them
-        d_L.alloc(std::max<i64>(lval_total, 1));
-        d_U.alloc(std::max<i64>(uval_total, 1));
         d_dpk.alloc(std::max<i64>(dpk_total, 1));
         d_pan.alloc(std::max<i64>(pan_total, 1));
         d_dinv.alloc(std::max<i64>(dscr_max, 1));
@@ -1128,25 +1156,104 @@ struct Plan : PlanBase {
     }
 
     // ------------------------------------------------------- values
-    void upload() override {
+    // What the device factor storage holds: 0 nothing, 1 values
+    // of A not yet factored (upload / restore / fill_a), 2 factors of them.
+    // d_acur = the values of A behind the storage (fill_a only; an upload
+    // does not tell which A it came from), a_fact = d_acur of the factors.
+    int vstate = 0;
+    const T *a_fact = nullptr, *snap_acur = nullptr;
+    int snap_state = 0;
+
+    // ---- host <-> HBM copies of the values (hostio.h)
+    std::thread up_thread;
+    std::string up_err;
+    double up_ms = 0;
+    bool host_current = false; // the host LUstruct holds what the device holds
+
+    vector<Xfer> value_xfers() {
         LocalLU *Llu = LU->Llu;
-        if (l_contig && lval_total) {
-            HIPCHK(hipMemcpy(d_L.p, Llu->Lnzval_bc_dat, lval_total * sizeof(T), hipMemcpyHostToDevice));
-        } else {
+        vector<Xfer> xs;
+        if (l_contig && lval_total)
+            xs.push_back({(char *)d_L.p, (char *)Llu->Lnzval_bc_dat, lval_total * sizeof(T)});
+        else
             for (int ljb = 0; ljb < nlc; ++ljb)
                 if (lval_off[ljb] >= 0)
-                    HIPCHK(hipMemcpy(d_L.p + lval_off[ljb], Llu->Lnzval_bc_ptr[ljb],
-                                     (size_t)lval_ld[ljb] * W(ljb * Pc + mycol) * sizeof(T),
-                                     hipMemcpyHostToDevice));
-        }
-        if (u_contig && uval_total) {
-            HIPCHK(hipMemcpy(d_U.p, Llu->Unzval_br_dat, uval_total * sizeof(T), hipMemcpyHostToDevice));
-        } else {
+                    xs.push_back({(char *)(d_L.p + lval_off[ljb]), (char *)Llu->Lnzval_bc_ptr[ljb],
+                                  (size_t)lval_ld[ljb] * W(ljb * Pc + mycol) * sizeof(T)});
+        if (u_contig && uval_total)
+            xs.push_back({(char *)d_U.p, (char *)Llu->Unzval_br_dat, uval_total * sizeof(T)});
+        else
             for (int lb = 0; lb < nlr; ++lb)
                 if (uval_off[lb] >= 0)
-                    HIPCHK(hipMemcpy(d_U.p + uval_off[lb], Llu->Unzval_br_ptr[lb],
-                                     (size_t)Llu->Ufstnz_br_ptr[lb][1] * sizeof(T),
-                                     hipMemcpyHostToDevice));
+                    xs.push_back({(char *)(d_U.p + uval_off[lb]), (char *)Llu->Unzval_br_ptr[lb],
+                                  (size_t)Llu->Ufstnz_br_ptr[lb][1] * sizeof(T)});
+        return merge_xfers(std::move(xs));
+    }
+
+    void upload_values() {
+        const auto t0 = std::chrono::steady_clock::now();
+        vector<Xfer> xs = value_xfers();
+        staged_h2d(xs, comm ? comm->device : 0);
+        double b = 0;
+        for (auto &x : xs) b += (double)x.bytes;
+        stats.h2d_bytes = b;
+        up_ms = ms_since(t0);
+    }
+
+    void upload() override {
+        const auto t0 = std::chrono::steady_clock::now();
+        if (up_thread.joinable()) {
+            up_thread.join();
+            if (!up_err.empty()) {
+                std::string e;
+                e.swap(up_err);
+                throw Error(e);
+            }
+            stats.t_upload_wait_ms = ms_since(t0);
+        } else {
+            upload_values();
+            stats.t_upload_wait_ms = ms_since(t0);
+        }
+        stats.t_upload_ms = up_ms;
+        vstate = 1;
+        d_acur = nullptr;
+        host_current = true;
+    }
+
+    // D2H of the factors in batches of whole levels: after the panels of
+    // level L are done, the L columns and U rows of its supernodes are final
+    // (right-looking LU; later levels only read them).  Batches of >= 256 MB
+    // keep the copies large once adjacent supernodes' blocks coalesce.
+    struct D2HBatch {
+        int last_level;
+        vector<Xfer> xs;
+    };
+    vector<D2HBatch> d2h_batches;
+
+    void build_d2h() {
+        LocalLU *Llu = LU->Llu;
+        vector<Xfer> cur;
+        double acc = 0;
+        for (size_t L = 0; L < levels.size(); ++L) {
+            for (int k : bylev[L]) {
+                if (k % Pc == mycol && lval_off[k / Pc] >= 0) {
+                    const int ljb = k / Pc;
+                    const size_t b = (size_t)lval_ld[ljb] * W(k) * sizeof(T);
+                    cur.push_back({(char *)(d_L.p + lval_off[ljb]), (char *)Llu->Lnzval_bc_ptr[ljb], b});
+                    acc += b;
+                }
+                if (k % Pr == myrow && uval_off[k / Pr] >= 0) {
+                    const int lb = k / Pr;
+                    const size_t b = (size_t)Llu->Ufstnz_br_ptr[lb][1] * sizeof(T);
+                    cur.push_back({(char *)(d_U.p + uval_off[lb]), (char *)Llu->Unzval_br_ptr[lb], b});
+                    acc += b;
+                }
+            }
+            if (!cur.empty() && (acc >= 256e6 || L + 1 == levels.size())) {
+                d2h_batches.push_back({(int)L, merge_xfers(std::move(cur))});
+                cur.clear();
+                acc = 0;
+            }
         }
     }
 
@@ -1157,9 +1264,14 @@ struct Plan : PlanBase {
         HIPCHK(hipMemcpyAsync(d_L0.p, d_L.p, d_L.bytes(), hipMemcpyDeviceToDevice, stream));
         HIPCHK(hipMemcpyAsync(d_U0.p, d_U.p, d_U.bytes(), hipMemcpyDeviceToDevice, stream));
         HIPCHK(hipStreamSynchronize(stream));
+        snap_state = vstate;
+        snap_acur = d_acur;
     }
     void restore() override {
         SLU_REQUIRE(d_L0.p && d_U0.p, "restore without snapshot");
+        vstate = snap_state;
+        d_acur = snap_acur;
+        host_current = false;
         HIPCHK(hipMemcpyAsync(d_L.p, d_L0.p, d_L.bytes(), hipMemcpyDeviceToDevice, stream));
         HIPCHK(hipMemcpyAsync(d_U.p, d_U0.p, d_U.bytes(), hipMemcpyDeviceToDevice, stream));
     }
@@ -1175,6 +1287,7 @@ struct Plan : PlanBase {
     void download() override {
         LocalLU *Llu = LU->Llu;
         sync();
+        if (host_current) return; // overlap_download already wrote them back
         if (l_contig && lval_total) {
             HIPCHK(hipMemcpy(Llu->Lnzval_bc_dat, d_L.p, lval_total * sizeof(T), hipMemcpyDeviceToHost));
         } else {
@@ -1239,6 +1352,11 @@ struct Plan : PlanBase {
 
     // ------------------------------------------------------- factor
     void factor(double anorm, int *info, int *tiny) override {
+        SLU_REQUIRE(vstate == 1, "factor: no unfactored values on the device (%s)",
+                    vstate == 2 ? "already factored; upload / restore / fill_a first"
+                                : "upload or fill_a first");
+        vstate = 2;
+        a_fact = d_acur;
         // thresh = smach_dist("Epsilon") * anorm (SRC/pdgstrf.c:412-413); in
         // psgstrf thresh is a float product.
         const float s_eps = 5.9604644775390625e-08f; // FLT_EPSILON * 0.5
@@ -1357,7 +1475,51 @@ struct Plan : PlanBase {
         HIPCHK(hipStreamWaitEvent(stream, ev_pend, 0));
         HIPCHK(hipGetLastError());
         int e_end = timing ? mark() : -1;
-        sync();
+        std::thread d2h;
+        std::string d2h_err;
+        double d2h_ms = 0;
+        int64_t ncopies = 0;
+        double dbytes = 0;
+        const bool overlap_dl = opts.overlap_download != 0;
+        if (overlap_dl) {
+            d2h = std::thread([&] {
+                const auto t0 = std::chrono::steady_clock::now();
+                hipStream_t cs = nullptr;
+                try {
+                    HIPCHK(hipSetDevice(comm ? comm->device : 0));
+                    HIPCHK(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+                    for (const D2HBatch &B : d2h_batches) {
+                        HIPCHK(hipEventSynchronize(ev_pan[B.last_level]));
+                        for (const Xfer &x : B.xs) {
+                            HIPCHK(hipMemcpyAsync(x.host, x.dev, x.bytes, hipMemcpyDeviceToHost, cs));
+                            dbytes += (double)x.bytes;
+                            ++ncopies;
+                        }
+                    }
+                    HIPCHK(hipStreamSynchronize(cs));
+                } catch (const std::exception &e) {
+                    d2h_err = e.what();
+                }
+                if (cs) (void)hipStreamDestroy(cs);
+                d2h_ms = ms_since(t0);
+            });
+        }
+        try {
+            sync();
+        } catch (...) {
+            if (d2h.joinable()) d2h.join();
+            throw;
+        }
+        if (overlap_dl) {
+            const auto t1 = std::chrono::steady_clock::now();
+            d2h.join();
+            SLU_REQUIRE(d2h_err.empty(), "factor download: %s", d2h_err.c_str());
+            stats.t_d2h_tail_ms = ms_since(t1);
+            stats.t_d2h_ms = d2h_ms;
+            stats.d2h_bytes = dbytes;
+            stats.n_d2h_copies = ncopies;
+        }
+        host_current = overlap_dl;
         int hc[4];
         HIPCHK(hipMemcpy(hc, d_counters.p, sizeof hc, hipMemcpyDeviceToHost));
         vector<int> zp(nsupers);
@@ -1523,6 +1685,7 @@ struct Plan : PlanBase {
     // right-hand sides in batches of SvNr<T>: every factor element is read once
     // per batch and sweep
     void solve(void *b, int64_t ldb, int nrhs) override {
+        SLU_REQUIRE(vstate == 2, "solve: the device storage holds no factors (factor first)");
         if (!sv_ready) build_solve();
         SLU_REQUIRE(ldb >= n && nrhs >= 0, "solve: ldb %lld < n %d", (long long)ldb, n);
         constexpr int NB = SvNr<T>::v;
@@ -1567,7 +1730,10 @@ struct Plan : PlanBase {
 
     void refine(const void *b, void *x, int64_t ld, int nrhs, double *berr, int *steps) override {
         SLU_REQUIRE(Pr * Pc == 1, "refine: 1x1 grids only");
-        SLU_REQUIRE(d_acur != nullptr, "refine needs the values of A (slu_plan_fill_a)");
+        SLU_REQUIRE(vstate == 2, "refine: the device storage holds no factors (factor first)");
+        SLU_REQUIRE(a_fact != nullptr,
+                    "refine needs the values of A the factors came from (slu_plan_fill_a "
+                    "before slu_plan_factor)");
         SLU_REQUIRE(ld >= n && nrhs >= 0, "refine: ld %lld < n %d", (long long)ld, n);
         if (!sv_ready) build_solve();
         const bool dbl = !std::is_same<T, float>::value;
@@ -1594,7 +1760,7 @@ struct Plan : PlanBase {
             while (true) {
                 HIPCHK(hipMemsetAsync(d_rf_berr.p, 0, sizeof(unsigned long long), stream));
                 hipLaunchKernelGGL(k_resid<T>, dim3(rb), dim3(256), 0, stream, d_rp.p, d_rc.p, d_re.p,
-                                   d_acur, d_rf_x.p, d_rf_b.p, d_rf_r.p, n, safe1, safe2, d_rf_berr.p);
+                                   a_fact, d_rf_x.p, d_rf_b.p, d_rf_r.p, n, safe1, safe2, d_rf_berr.p);
                 HIPCHK(hipGetLastError());
                 unsigned long long bits = 0;
                 HIPCHK(hipMemcpyAsync(&bits, d_rf_berr.p, sizeof bits, hipMemcpyDeviceToHost, stream));
@@ -1684,7 +1850,7 @@ struct Plan : PlanBase {
         d_amap.upload(map.empty() ? vector<i64>(1, -1) : map);
         d_aval.alloc(std::max<i64>(nnz, 1));
         a_nnz = nnz;
-        d_acur = nullptr;
+        d_acur = a_fact = snap_acur = nullptr; // the previous pattern's values are gone
         if (Pr * Pc == 1) { // rows of A for the refinement's residual (k_resid)
             vector<i64> rp(n + 1, 0), re((size_t)nnz);
             vector<int> rc((size_t)nnz);
@@ -1712,6 +1878,8 @@ struct Plan : PlanBase {
             src = d_aval.p;
         }
         d_acur = src;
+        vstate = 1;
+        host_current = false;
         hipEvent_t e0, e1;
         HIPCHK(hipEventCreate(&e0));
         HIPCHK(hipEventCreate(&e1));

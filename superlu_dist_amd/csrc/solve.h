@@ -281,8 +281,14 @@ k_resid(const int64_t *rp, const int *rc, const int64_t *re, const T *a, const T
         if (tmp > safe2) s = ra / tmp;
         else if (tmp != 0.0) s = (safe1 + ra) / tmp;
     }
-    for (int off = 32; off > 0; off >>= 1) s = fmax(s, __shfl_xor(s, off, 64));
-    if ((threadIdx.x & 63) == 0 && s > 0.0)
+    // NaN must win the max, as SUPERLU_MAX lets it through to berr
+    // (SRC/pdgsrfs.c:222-226): fmax alone would drop it.  A NaN's bit
+    // pattern is above +Inf's as an unsigned integer, so atomicMax keeps it.
+    for (int off = 32; off > 0; off >>= 1) {
+        const double o = __shfl_xor(s, off, 64);
+        s = (s != s || o != o) ? __builtin_nan("") : fmax(s, o);
+    }
+    if ((threadIdx.x & 63) == 0 && !(s <= 0.0))
         atomicMax(berr, (unsigned long long)__double_as_longlong(s));
 }
 

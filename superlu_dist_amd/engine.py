@@ -69,11 +69,18 @@ class Comm:
 
 
 class Plan:
-    def __init__(self, lu, comm=None, replace_tiny=False, timing=False):
+    def __init__(self, lu, comm=None, replace_tiny=False, timing=False, overlap_upload=False,
+                 overlap_download=False):
+        """overlap_upload: the H2D copy of the values starts inside the
+        constructor, beside the plan build (upload() waits for it);
+        overlap_download: factor() writes each finished level back into the
+        host LUstruct while later levels run (download() is then a no-op)."""
         self.lu = lu
         o = EngineOpts()
         o.replace_tiny_pivot = int(bool(replace_tiny))
         o.timing = int(timing)
+        o.overlap_upload = int(bool(overlap_upload))
+        o.overlap_download = int(bool(overlap_download))
         err = C.create_string_buffer(1024)
         iam = lu.myrow * lu.npcol + lu.mycol
         self.comm = comm

@@ -167,6 +167,7 @@ class LUStruct:
         v = SluLuView()
         lib().slu_lu_get_view(self.ptr, self.dtype, C.byref(v))
         self.view = v
+        self.xsup = np.ctypeslib.as_array(v.xsup, shape=(nsupers + 1,))
         npt = DTYPES[self.dtype]
         isz = np.dtype(npt).itemsize
         self.Lidx = np.ctypeslib.as_array(v.Lidx, shape=(v.Lidx_cnt,))

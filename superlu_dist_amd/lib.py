@@ -42,7 +42,8 @@ class SluLuView(C.Structure):
 
 class EngineOpts(C.Structure):
     _fields_ = [("replace_tiny_pivot", C.c_int), ("timing", C.c_int), ("serial", C.c_int),
-                ("reserved", C.c_int * 5)]
+                ("overlap_upload", C.c_int), ("overlap_download", C.c_int),
+                ("reserved", C.c_int * 3)]
 
 
 class PlanStats(C.Structure):
@@ -58,7 +59,11 @@ class PlanStats(C.Structure):
                 ("schur_big_flops", C.c_double), ("n_schur_launches", C.c_int64),
                 ("n_schur_big_launches", C.c_int64), ("comm_bytes", C.c_double),
                 ("t_solve_ms", C.c_double), ("t_fill_ms", C.c_double),
-                ("t_refine_ms", C.c_double)]
+                ("t_refine_ms", C.c_double), ("t_plan_ms", C.c_double),
+                ("t_upload_ms", C.c_double), ("t_upload_wait_ms", C.c_double),
+                ("t_d2h_ms", C.c_double), ("t_d2h_tail_ms", C.c_double),
+                ("h2d_bytes", C.c_double), ("d2h_bytes", C.c_double),
+                ("n_d2h_copies", C.c_int64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

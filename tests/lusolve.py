@@ -1,15 +1,15 @@
 """Host-side supernodal triangular solves on a factored 1x1 LUstruct (test
-helper for backward-error checks; the reference's pdgstrs is out of scope)."""
+helper for backward-error checks), and the coordinate maps of pdgssvx's
+solve (SRC/pdgssvx.c): the LUstruct factors Pc Pr diag(R) A diag(C) Pc^T."""
 import numpy as np
 from scipy.linalg import solve_triangular
 
 
 def solve_1x1(lu, b):
     """Solve (P A P^T) x = b with the factors held in lu (1x1 grid)."""
-    S = lu.symb
-    xs = S.xsup
+    xs = lu.xsup
     x = np.array(b, dtype=np.result_type(lu.Lval.dtype, np.float64 if lu.Lval.dtype != np.complex128 else np.complex128)).copy()
-    ns = S.nsupers
+    ns = lu.nsupers
     cols = []
     for k in range(ns):
         w = xs[k + 1] - xs[k]
@@ -62,3 +62,35 @@ def backward_error(A, perm, x_perm, b_perm):
         r[ri[sl]] += v[sl] * x_perm[j]
         absrow[ri[sl]] += np.abs(v[sl])
     return float(np.abs(r).max() / (absrow.max() * np.abs(x_perm).max()))
+
+
+def to_lu_coords(b, perm_r, perm_c, R=None):
+    """b (original row order) -> Pc Pr diag(R) b, the right-hand side of the
+    factored system (row i of A is row perm_c[perm_r[i]] of the LUstruct)."""
+    b = np.asarray(b)
+    bb = b * (R if R is not None else 1.0)
+    out = np.empty_like(bb)
+    out[perm_c[perm_r]] = bb
+    return out
+
+
+def from_lu_coords(y, perm_c, C=None):
+    """Solution of the factored system -> x = diag(C) Pc^T y."""
+    x = np.asarray(y)[perm_c]
+    return x * (C if C is not None else 1.0)
+
+
+def lu_coords_matrix(fx):
+    """CSC (colptr, rowind, values) of Pc Pr diag(R) A diag(C) Pc^T from a
+    1x1 refdump fixture: pdgssvx leaves its local A scaled and with perm_c
+    applied to the column indices (SRC/pdgssvx.c:1140); rows are mapped here."""
+    rp, ci, av = fx.arr(0, "A_rowptr"), fx.arr(0, "A_colind"), fx.arr(0, "A_val")
+    pr, pc = fx.arr(0, "perm_r"), fx.arr(0, "perm_c")
+    n = fx.n
+    rows = pc[pr[np.repeat(np.arange(n), np.diff(rp))]]
+    order = np.lexsort((rows, ci))
+    cols_sorted = ci[order]
+    colptr = np.zeros(n + 1, dtype=np.int64)
+    np.add.at(colptr, cols_sorted + 1, 1)
+    colptr = np.cumsum(colptr)
+    return colptr, rows[order].astype(np.int64), av[order]

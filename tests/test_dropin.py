@@ -38,7 +38,7 @@ def _run(exe, nprocs, args, matrix, timeout=240):
     out = r.stdout + r.stderr
     assert r.returncode == 0, f"{exe} failed ({r.returncode}):\n{out[-3000:]}"
     assert "ERROR: INFO" not in out, out[-2000:]
-    errs = [float(x) for x in re.findall(r"\|\|X-Xtrue\|\|/\|\|X\|\| = ([0-9.eE+-]+)", out)]
+    errs = [float(x) for x in re.findall(r"\|\|X ?- ?Xtrue\|\| ?/ ?\|\|X\|\| = ([0-9.eE+-]+)", out)]
     assert errs, out[-2000:]
     m = re.search(r"FACTOR time\s+([0-9.]+)", out)
     return max(errs), (float(m.group(1)) if m else None), out

@@ -111,3 +111,45 @@ def test_refine_needs_values():
     assert p.factor(12.0) == (0, 0)
     with pytest.raises(RuntimeError, match="fill_a"):
         p.refine(np.ones(A.n), np.zeros(A.n))
+
+
+def test_refine_reports_nonfinite_backward_error():
+    """A NaN / Inf in x must surface in berr (SUPERLU_MAX passes NaN through,
+    SRC/pdgsrfs.c:222-226), not look like convergence."""
+    A = Csc.stencil(STENCIL_3D7, 6, 6, 6)
+    S = Symbolic(A, nd_order(6, 6, 6), 60, 256)
+    p = Plan(S.distribute())
+    cp, ri, v = A.permuted(S.perm_c).arrays()
+    p.set_a_pattern(cp, ri)
+    p.fill_a(v)
+    assert p.factor(12.0)[0] == 0
+    b = np.ones(A.n)
+    x0 = p.solve(b)
+    x0[5] = np.nan
+    _, berr, steps = p.refine(b, x0)
+    assert not np.isfinite(berr[0]) and steps[0] == 0
+
+
+def test_device_state_is_checked():
+    """solve / refine only on factors of the values they describe."""
+    A = Csc.stencil(STENCIL_3D7, 6, 6, 6)
+    S = Symbolic(A, nd_order(6, 6, 6), 60, 256)
+    p = Plan(S.distribute())
+    cp, ri, v = A.permuted(S.perm_c).arrays()
+    p.set_a_pattern(cp, ri)
+    p.fill_a(v)
+    with pytest.raises(RuntimeError, match="factor first"):
+        p.solve(np.ones(A.n))
+    assert p.factor(12.0)[0] == 0
+    with pytest.raises(RuntimeError, match="already factored"):
+        p.factor(12.0)
+    p.fill_a(2 * v)                       # refilled, not factored
+    with pytest.raises(RuntimeError, match="factor first"):
+        p.refine(np.ones(A.n), np.zeros(A.n))
+    assert p.factor(12.0)[0] == 0
+    x, berr, _ = p.refine(np.ones(A.n), np.zeros(A.n))
+    assert berr[0] < 1e-14
+    p.upload()                            # values of unknown origin
+    assert p.factor(12.0)[0] == 0
+    with pytest.raises(RuntimeError, match="fill_a"):
+        p.refine(np.ones(A.n), np.zeros(A.n))

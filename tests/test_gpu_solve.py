@@ -40,6 +40,10 @@ def _rhs(A, perm, xt):
     (STENCIL_3D7, (12, 12, 12), 0, 60, 256, 10),  # batches of 8 + 2 right-hand sides
     (STENCIL_3D27, (8, 8, 8), 1, 60, 256, 9),
     (STENCIL_3D7, (8, 8, 8), 2, 60, 256, 5),      # complex: batches of 2
+    # supernodes wider than 256 whose last 32-column panel starts in the upper
+    # half of a wave (width 300 / 100: j0 % 64 == 32) -- complex and fp32
+    (STENCIL_3D7, (20, 20, 20), 2, 60, 300, 3),
+    (STENCIL_3D7, (20, 20, 20), 1, 60, 300, 3),
 ])
 def test_device_solve_matches_host_solve(kind, dims, dtype, relax, maxsup, nrhs):
     kw = dict(diag=6 - 0.25, diag_im=-0.0025) if dtype == 2 else {}

@@ -120,6 +120,7 @@ def test_gpu_grid_on_reference_lustructs(name, tmp_path):
         for o, (Lr, Ur) in zip(out, fx.ref_factors()):
             for mine, r in ((o["L"], Lr), (o["U"], Ur)):
                 if len(r):
+                    mine = mine[:len(r)]  # library-built arrays carry one spare element
                     assert np.isfinite(mine).all()
                     d = np.abs(mine.astype(np.complex128) - r.astype(np.complex128)).max()
                     worst = max(worst, d / max(np.abs(r).max(), 1e-300))

@@ -1,0 +1,83 @@
+"""The device value fill, solve and refinement pinned to the REFERENCE
+(SURVEY 8(f) rows 1-2), on the 1x1 refdump fixtures: the reference's own
+pddistribute output (pre-factor L/U values), its pdgstrs solution
+(IterRefine = NOREFINE, x_norefine) and its pdgsrfs-refined solution (x,
+berr), all from oracle/_ref/ref_dump running p?gssvx.
+
+* CPU: the coordinate maps of pdgssvx (Pc Pr diag(R) A diag(C) Pc^T) applied
+  to the reference's factors with a host supernodal solve reproduce the
+  reference's x_norefine -- pins the test's own plumbing.
+* GPU: slu_plan_fill_a on the fixture's A reproduces the reference's
+  pddistribute values bit for bit; the device factorization of them, the
+  device solve and the device refinement reproduce the reference's x within
+  the accuracy the reference itself reaches (||x_ref - xtrue||), and the
+  refined backward error is at the reference's level.
+"""
+import numpy as np
+import pytest
+
+from lusolve import from_lu_coords, lu_coords_matrix, solve_1x1, to_lu_coords
+from refdump import Fixture, names
+
+CASES = [n for n in names() if "_1x1_" in n and not n.startswith("zeropiv")]
+EPS = {0: 2.2e-16, 1: 1.2e-7, 2: 2.2e-16}
+
+
+def _rhs(fx):
+    R = fx.z.get("r0_R")
+    C = fx.z.get("r0_C")
+    return fx.arr(0, "b"), R, C, fx.arr(0, "perm_r"), fx.arr(0, "perm_c")
+
+
+def _close(x, xref, xtrue, dtype):
+    """x agrees with the reference's x to the accuracy the reference has."""
+    nx = np.abs(xref).max()
+    ref_err = np.abs(xref - xtrue).max() / nx
+    d = np.abs(x - xref).max() / nx
+    return d, max(10 * ref_err, 50 * EPS[dtype])
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_host_solve_of_reference_factors_is_reference_pdgstrs(name):
+    fx = Fixture(name)
+    lu = fx.lu(0, "post")
+    b, R, C, pr, pc = _rhs(fx)
+    y = solve_1x1(lu, to_lu_coords(b, pr, pc, R))
+    x = from_lu_coords(y, pc, C)
+    d, tol = _close(x, fx.arr(0, "x_norefine"), fx.arr(0, "xtrue"), fx.dtype)
+    assert d < tol, (d, tol)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", CASES)
+def test_gpu_fill_solve_refine_match_reference(name):
+    from superlu_dist_amd.engine import Plan
+    fx = Fixture(name)
+    lu = fx.lu(0, "pre")
+    pre_L, pre_U = lu.Lval.copy(), lu.Uval.copy()
+    lu.Lval[:] = np.nan        # the fill must produce every value itself
+    lu.Uval[:] = np.nan
+    p = Plan(lu, replace_tiny=fx.replace_tiny)
+    cp, ri, v = lu_coords_matrix(fx)
+    p.set_a_pattern(cp, ri)
+    p.fill_a(v)
+    p.download()
+    # SamePattern_SameRowPerm refill == the reference's pddistribute, bit for bit
+    np.testing.assert_array_equal(lu.Lval[:-1], pre_L[:-1])
+    np.testing.assert_array_equal(lu.Uval[:-1], pre_U[:-1])
+    info, tiny = p.factor(fx.anorm)
+    assert (info, tiny) == (fx.info, fx.tiny)
+    b, R, C, pr, pc = _rhs(fx)
+    bl = to_lu_coords(b, pr, pc, R).astype(lu.Lval.dtype)
+    y = p.solve(bl)
+    x = from_lu_coords(y, pc, C)
+    xtrue = fx.arr(0, "xtrue")
+    d, tol = _close(x, fx.arr(0, "x_norefine"), xtrue, fx.dtype)
+    assert d < tol, ("solve", d, tol)
+    yr, berr, steps = p.refine(bl, y)
+    xr = from_lu_coords(yr, pc, C)
+    d, tol = _close(xr, fx.arr(0, "x"), xtrue, fx.dtype)
+    assert d < tol, ("refine", d, tol)
+    ref_berr = float(fx.arr(0, "berr")[0])
+    assert berr[0] <= max(4 * ref_berr, 4 * EPS[fx.dtype]), (berr[0], ref_berr)
+    assert abs(int(steps[0]) - fx.meta["ranks"][0]["refine_steps"]) <= 1
