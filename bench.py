@@ -144,7 +144,8 @@ def abi_leg(lu, anorm, factor_ms):
     p.download()
     st = p.stats()
     del p
-    same = bool(np.array_equal(Lf[:-1], lu.Lval[:-1]))
+    # atomics order the sums differently run to run: compare, do not demand bits
+    same = float(np.abs(Lf[:-1] - lu.Lval[:-1]).max() / max(np.abs(Lf[:-1]).max(), 1e-300))
     lu.Lval[:] = L0
     lu.Uval[:] = U0
     h2d = st["t_upload_ms"]
@@ -161,7 +162,7 @@ def abi_leg(lu, anorm, factor_ms):
             "h2d_gbs": round(st["h2d_bytes"] / h2d / 1e6, 1) if h2d else None,
             "d2h_copies": int(st["n_d2h_copies"]),
             "pcie_floor_ms": round((st["h2d_bytes"] + st["d2h_bytes"]) / pcie / 1e6, 1),
-            "factors_identical_abi_vs_engine": same,
+            "factors_rel_diff_abi_vs_engine": same,
             "note": "factor_ms in bar_ms = ms_per_step (HBM-resident); h2d = staged H2D of the "
                     "L/U values (hostio.h); D2H rides under the factorization"}
 

@@ -2,10 +2,17 @@
 // every extern "C" entry point catches slu::Error and stores the message
 // for slu_last_error().
 #pragma once
+#include <algorithm>
+#include <atomic>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
+#include <exception>
+#include <mutex>
 #include <stdexcept>
 #include <string>
+#include <thread>
+#include <vector>
 
 namespace slu {
 
@@ -23,6 +30,48 @@ inline std::string fmt(const char *f, ...) {
 }
 
 void set_last_error(const std::string &s);
+
+// Host threads for the plan build (SLU_PLAN_THREADS, default min(8, cores)).
+inline int plan_threads() {
+    static const int t = [] {
+        const char *e = getenv("SLU_PLAN_THREADS");
+        int v = e ? atoi(e) : (int)std::thread::hardware_concurrency();
+        return std::max(1, std::min(e ? 64 : 8, v));
+    }();
+    return t;
+}
+
+// f(i) for i in [0, n): dynamic chunks over plan_threads() threads; the
+// first exception is rethrown after every thread has stopped.
+template <typename F> void parallel_for(int n, F &&f, int chunk = 64) {
+    const int T = plan_threads();
+    if (n <= chunk || T == 1) {
+        for (int i = 0; i < n; ++i) f(i);
+        return;
+    }
+    std::atomic<int> next(0);
+    std::exception_ptr err;
+    std::mutex mu;
+    auto work = [&] {
+        try {
+            for (;;) {
+                const int a = next.fetch_add(chunk);
+                if (a >= n) break;
+                const int b = std::min(n, a + chunk);
+                for (int i = a; i < b; ++i) f(i);
+            }
+        } catch (...) {
+            std::lock_guard<std::mutex> lk(mu);
+            if (!err) err = std::current_exception();
+            next = n;
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < std::min(T, (n + chunk - 1) / chunk); ++t) th.emplace_back(work);
+    work();
+    for (auto &x : th) x.join();
+    if (err) std::rethrow_exception(err);
+}
 
 } // namespace slu
 

@@ -353,9 +353,12 @@ struct Plan : PlanBase {
         for (int k = 0; k < nsupers; ++k)
             SLU_REQUIRE(W(k) <= 512, "supernode %d has %d columns (> MAX_SUPER_SIZE 512)", k, W(k));
         const auto t0 = std::chrono::steady_clock::now();
-        build_local();
+        prof = getenv("SLU_PROFILE_PLAN") != nullptr;
+        tprev = t0;
+        value_layout();
         d_L.alloc(std::max<i64>(lval_total, 1));
         d_U.alloc(std::max<i64>(uval_total, 1));
+        tick("layout + alloc");
         if (opts.overlap_upload) {
             // the H2D copy of the values runs beside the rest of the plan
             // build (index exchange, levels, schedule, device tables)
@@ -369,17 +372,36 @@ struct Plan : PlanBase {
             });
         }
         try {
+            build_local();
+            tick("build_local");
             exchange_index();
+            tick("exchange_index");
             compute_levels();
+            tick("compute_levels");
             layout_values();
+            tick("layout_values");
             build_schedule();
+            if (prof) fprintf(stderr, "[slu plan %d]   (add_supernode %.1f ms)\n", iam, t_addsn);
+            tick("build_schedule");
             build_device();
+            tick("build_device");
             build_d2h();
+            tick("build_d2h");
         } catch (...) {
             if (up_thread.joinable()) up_thread.join();
             throw;
         }
         stats.t_plan_ms = ms_since(t0);
+    }
+
+    bool prof = false; // SLU_PROFILE_PLAN: phase times of the plan build on stderr
+    std::chrono::steady_clock::time_point tprev;
+    void tick(const char *what) {
+        if (!prof) return;
+        const auto now = std::chrono::steady_clock::now();
+        fprintf(stderr, "[slu plan %d] %-18s %8.1f ms\n", iam, what,
+                std::chrono::duration<double, std::milli>(now - tprev).count());
+        tprev = now;
     }
 
     static double ms_since(std::chrono::steady_clock::time_point t0) {
@@ -398,89 +420,140 @@ struct Plan : PlanBase {
     }
 
     // ------------------------------------------------------- local layout
-    void build_local() {
+    // Value offsets of the rank's L block columns / U block rows in d_L /
+    // d_U (the order of Lnzval_bc_dat / Unzval_br_dat, so that the upload can
+    // start before the rest of the plan exists).
+    void value_layout() {
         LocalLU *Llu = LU->Llu;
         lval_off.assign(nlc, -1);
         lval_ld.assign(nlc, 0);
-        lcol_first.assign(nlc, 0);
-        lcol_nblk.assign(nlc, 0);
         i64 off = 0;
         l_contig = Llu->Lnzval_bc_dat != nullptr;
         for (int ljb = 0; ljb < nlc; ++ljb) {
-            int jb = ljb * Pc + mycol;
-            int_t *index = Llu->Lrowind_bc_ptr[ljb];
-            lcol_first[ljb] = (int)lblk.size();
+            const int_t *index = Llu->Lrowind_bc_ptr[ljb];
             if (!index) continue;
-            int nb = (int)index[0], nsupr = (int)index[1];
             lval_off[ljb] = off;
-            lval_ld[ljb] = nsupr;
+            lval_ld[ljb] = (int)index[1];
             if (Llu->Lnzval_bc_dat && (HT *)Llu->Lnzval_bc_ptr[ljb] != (HT *)Llu->Lnzval_bc_dat + off)
                 l_contig = false;
-            i64 p = SLU_BC_HEADER;
+            off += (i64)index[1] * W(ljb * Pc + mycol);
+        }
+        lval_total = off;
+        uval_off.assign(nlr, -1);
+        off = 0;
+        u_contig = Llu->Unzval_br_dat != nullptr;
+        for (int lb = 0; lb < nlr; ++lb) {
+            const int_t *index = Llu->Ufstnz_br_ptr[lb];
+            if (!index) continue;
+            uval_off[lb] = off;
+            if (Llu->Unzval_br_dat && (HT *)Llu->Unzval_br_ptr[lb] != (HT *)Llu->Unzval_br_dat + off)
+                u_contig = false;
+            off += index[1];
+        }
+        uval_total = off;
+    }
+
+    // Destination tables (LBlk + lmap per L block, UBlk + per-column segment
+    // offsets per U block) in two parallel passes: sizes per block column /
+    // row, prefix sums, then every column / row fills its own slice.
+    void build_local() {
+        LocalLU *Llu = LU->Llu;
+        // ---- L block columns
+        lcol_first.assign(nlc + 1, 0);
+        lcol_nblk.assign(nlc, 0);
+        vector<i64> mapbase(nlc + 1, 0);
+        parallel_for(nlc, [&](int ljb) {
+            const int_t *index = Llu->Lrowind_bc_ptr[ljb];
+            if (!index) return;
+            i64 p = SLU_BC_HEADER, ml = 0;
+            for (int b = 0; b < index[0]; ++b) {
+                ml += W(index[p]);
+                p += SLU_LB_DESCRIPTOR + index[p + 1];
+            }
+            lcol_nblk[ljb] = (int)index[0];
+            mapbase[ljb + 1] = ml;
+        });
+        for (int j = 0; j < nlc; ++j) {
+            lcol_first[j + 1] = lcol_first[j] + lcol_nblk[j];
+            mapbase[j + 1] += mapbase[j];
+        }
+        lblk.assign(lcol_first[nlc], LBlk{});
+        lblk_ib.assign(lcol_first[nlc], 0);
+        lmap.assign(mapbase[nlc], -1);
+        parallel_for(nlc, [&](int ljb) {
+            const int jb = ljb * Pc + mycol;
+            const int_t *index = Llu->Lrowind_bc_ptr[ljb];
+            if (!index) return;
+            const int nb = (int)index[0], nsupr = (int)index[1];
+            i64 p = SLU_BC_HEADER, mo = mapbase[ljb];
             int rs = 0;
             for (int b = 0; b < nb; ++b) {
-                int gb = (int)index[p], nr = (int)index[p + 1];
+                const int gb = (int)index[p], nr = (int)index[p + 1];
                 SLU_REQUIRE(gb % Pr == myrow, "L block (%d,%d) is not on process row %d", gb, jb, myrow);
-                LBlk L{};
-                L.colvoff = off;
-                L.mapoff = (i64)lmap.size();
+                LBlk &L = lblk[lcol_first[ljb] + b];
+                L.colvoff = lval_off[ljb];
+                L.mapoff = mo;
                 L.ld = nsupr;
                 L.fcol = (int)xsup[jb];
                 L.frow = (int)xsup[gb];
-                lmap.resize(lmap.size() + W(gb), -1);
-                for (int i = 0; i < nr; ++i) {
-                    i64 gr = index[p + 2 + i];
-                    lmap[L.mapoff + gr - xsup[gb]] = rs + i;
-                }
-                lblk.push_back(L);
-                lblk_ib.push_back(gb);
+                for (int i = 0; i < nr; ++i) lmap[mo + index[p + 2 + i] - xsup[gb]] = rs + i;
+                lblk_ib[lcol_first[ljb] + b] = gb;
+                mo += W(gb);
                 rs += nr;
                 p += SLU_LB_DESCRIPTOR + nr;
             }
             SLU_REQUIRE(rs == nsupr, "L column %d: block rows %d != nsupr %d", jb, rs, nsupr);
-            lcol_nblk[ljb] = nb;
-            off += (i64)nsupr * W(jb);
-        }
-        lval_total = off;
+        });
+        lcol_first.resize(nlc);
 
-        uval_off.assign(nlr, -1);
-        urow_first.assign(nlr, 0);
+        // ---- U block rows
+        urow_first.assign(nlr + 1, 0);
         urow_nblk.assign(nlr, 0);
-        off = 0;
-        u_contig = Llu->Unzval_br_dat != nullptr;
-        for (int lb = 0; lb < nlr; ++lb) {
-            int gb = lb * Pr + myrow;
-            int_t *index = Llu->Ufstnz_br_ptr[lb];
-            urow_first[lb] = (int)ublk.size();
-            if (!index) continue;
-            int nb = (int)index[0];
-            i64 len = index[1];
-            uval_off[lb] = off;
-            if (Llu->Unzval_br_dat && (HT *)Llu->Unzval_br_ptr[lb] != (HT *)Llu->Unzval_br_dat + off)
-                u_contig = false;
-            i64 p = SLU_BR_HEADER, run = 0;
-            i64 klst = xsup[gb + 1];
+        vector<i64> colbase(nlr + 1, 0);
+        parallel_for(nlr, [&](int lb) {
+            const int_t *index = Llu->Ufstnz_br_ptr[lb];
+            if (!index) return;
+            i64 p = SLU_BR_HEADER, nc = 0;
+            for (int b = 0; b < index[0]; ++b) {
+                nc += W(index[p]);
+                p += SLU_UB_DESCRIPTOR + W(index[p]);
+            }
+            urow_nblk[lb] = (int)index[0];
+            colbase[lb + 1] = nc;
+        });
+        for (int j = 0; j < nlr; ++j) {
+            urow_first[j + 1] = urow_first[j] + urow_nblk[j];
+            colbase[j + 1] += colbase[j];
+        }
+        ublk.assign(urow_first[nlr], UBlk{});
+        ublk_jb.assign(urow_first[nlr], 0);
+        ucol_voff.assign(colbase[nlr], 0);
+        ucol_fst.assign(colbase[nlr], 0);
+        parallel_for(nlr, [&](int lb) {
+            const int gb = lb * Pr + myrow;
+            const int_t *index = Llu->Ufstnz_br_ptr[lb];
+            if (!index) return;
+            const int nb = (int)index[0];
+            const i64 len = index[1], klst = xsup[gb + 1], off = uval_off[lb];
+            i64 p = SLU_BR_HEADER, run = 0, co = colbase[lb];
             for (int b = 0; b < nb; ++b) {
-                int jb = (int)index[p];
+                const int jb = (int)index[p];
                 SLU_REQUIRE(jb % Pc == mycol, "U block (%d,%d) is not on process column %d", gb, jb, mycol);
-                UBlk U{};
-                U.coloff = (i64)ucol_voff.size();
+                UBlk &U = ublk[urow_first[lb] + b];
+                U.coloff = co;
                 U.fcol = (int)xsup[jb];
-                for (int c = 0; c < W(jb); ++c) {
-                    i64 fst = index[p + SLU_UB_DESCRIPTOR + c];
-                    ucol_voff.push_back(off + run);
-                    ucol_fst.push_back((int)fst);
+                for (int c = 0; c < W(jb); ++c, ++co) {
+                    const i64 fst = index[p + SLU_UB_DESCRIPTOR + c];
+                    ucol_voff[co] = off + run;
+                    ucol_fst[co] = (int)fst;
                     run += klst - fst;
                 }
-                ublk.push_back(U);
-                ublk_jb.push_back(jb);
+                ublk_jb[urow_first[lb] + b] = jb;
                 p += SLU_UB_DESCRIPTOR + W(jb);
             }
             SLU_REQUIRE(run == len, "U row %d: segment lengths %lld != %lld", gb, (long long)run, (long long)len);
-            urow_nblk[lb] = nb;
-            off += len;
-        }
-        uval_total = off;
+        });
+        urow_first.resize(nlr);
     }
 
     int find_lblk(int ib, int jb) const { // local column jb, block ib
@@ -777,6 +850,7 @@ struct Plan : PlanBase {
     }
 
     // ------------------------------------------------------- schedule
+    double t_addsn = 0;
     void build_schedule() {
         // value buffers first: work items point straight into them
         d_dpk.alloc(std::max<i64>(dpk_total, 1));
@@ -796,7 +870,9 @@ struct Plan : PlanBase {
             R.uf_off = (int)uf_items.size();
             R.dc_off = (int)dcopy.size();
             for (int c = 0; c < 2; ++c) lv_big[c].clear(), lv_small[c].clear();
+            const auto ta = std::chrono::steady_clock::now();
             for (int k : bylev[L]) add_supernode(k, R);
+            t_addsn += ms_since(ta);
             // critical tiles first: they are launched ahead of the rest so the
             // next level's panels can be factored while the rest runs
             R.bigc_n = (int)lv_big[0].size();
@@ -1220,41 +1296,129 @@ struct Plan : PlanBase {
         host_current = true;
     }
 
-    // D2H of the factors in batches of whole levels: after the panels of
-    // level L are done, the L columns and U rows of its supernodes are final
-    // (right-looking LU; later levels only read them).  Batches of >= 256 MB
-    // keep the copies large once adjacent supernodes' blocks coalesce.
-    struct D2HBatch {
-        int last_level;
-        vector<Xfer> xs;
+    // D2H of the factors while the factorization runs (opts.overlap_download).
+    // After the panels of level L are done, the L columns and U rows of its
+    // supernodes are final (right-looking LU; later levels only read them).
+    // Measured on the box (profiles/r02_pcie_micro.json): pageable D2H needs
+    // copies of >= 4 MB to reach 49 GB/s (512 KB: 12 GB/s), while GPU stores
+    // into pinned host memory reach 51-56 GB/s with 32-128 workgroups and
+    // pinned -> pageable memcpy 60 / 121 GB/s on 4 / 8 host threads.  So the
+    // finished blocks are pushed by a small kernel (k_push) into a pinned
+    // slot of <= SLOT bytes ("fill"), and host threads scatter the slot into
+    // the caller's arrays while the next fill is pushed.
+    // slot / minimum fill (SLU_D2H_SLOT_KB overrides the slot: tests use tiny
+    // slots so that blocks split across fills)
+    i64 D2H_SLOT = 256ll << 20, D2H_MIN = 64ll << 20;
+    static constexpr i64 D2H_PIECE = 1ll << 20;
+    struct D2HFill {
+        int level;        // all blocks final after ev_pan[level]
+        int seg_off, seg_n; // PushSeg range
+        int hs_off, hs_n; // HostSeg range
+        i64 bytes;
     };
-    vector<D2HBatch> d2h_batches;
+    struct HostSeg {
+        char *host;
+        i64 off, bytes; // in the slot
+    };
+    vector<D2HFill> d2h_fills;
+    vector<PushSeg> h_push;
+    vector<HostSeg> h_unpack;
+    DevBuf<PushSeg> d_push;
 
     void build_d2h() {
+        if (!opts.overlap_download) return;
+        if (const char *e = getenv("SLU_D2H_SLOT_KB")) {
+            D2H_SLOT = std::max<i64>(16, atoll(e)) << 10;
+            D2H_MIN = D2H_SLOT / 4;
+        }
         LocalLU *Llu = LU->Llu;
-        vector<Xfer> cur;
-        double acc = 0;
+        i64 fb = 0; // bytes in the open fill
+        int seg0 = 0, hs0 = 0;
+        auto close = [&](int L) {
+            if (fb == 0) return;
+            d2h_fills.push_back({L, seg0, (int)h_push.size() - seg0, hs0, (int)h_unpack.size() - hs0, fb});
+            seg0 = (int)h_push.size();
+            hs0 = (int)h_unpack.size();
+            fb = 0;
+        };
+        auto add = [&](const char *dev, char *host, i64 bytes, int L) {
+            i64 done = 0;
+            while (done < bytes) {
+                const i64 take = std::min(bytes - done, D2H_SLOT - fb);
+                for (i64 o = 0; o < take; o += D2H_PIECE)
+                    h_push.push_back({dev + done + o, fb + o, (int)std::min(D2H_PIECE, take - o)});
+                // host pieces of <= 4 MB so the unpack threads balance
+                for (i64 o = 0; o < take; o += 4 * D2H_PIECE)
+                    h_unpack.push_back({host + done + o, fb + o, std::min(4 * D2H_PIECE, take - o)});
+                fb += (take + 15) & ~(i64)15; // 16-byte aligned slot offsets
+                done += take;
+                if (fb >= D2H_SLOT) close(L);
+            }
+        };
         for (size_t L = 0; L < levels.size(); ++L) {
             for (int k : bylev[L]) {
                 if (k % Pc == mycol && lval_off[k / Pc] >= 0) {
                     const int ljb = k / Pc;
-                    const size_t b = (size_t)lval_ld[ljb] * W(k) * sizeof(T);
-                    cur.push_back({(char *)(d_L.p + lval_off[ljb]), (char *)Llu->Lnzval_bc_ptr[ljb], b});
-                    acc += b;
+                    add((const char *)(d_L.p + lval_off[ljb]), (char *)Llu->Lnzval_bc_ptr[ljb],
+                        (i64)lval_ld[ljb] * W(k) * (i64)sizeof(T), (int)L);
                 }
                 if (k % Pr == myrow && uval_off[k / Pr] >= 0) {
                     const int lb = k / Pr;
-                    const size_t b = (size_t)Llu->Ufstnz_br_ptr[lb][1] * sizeof(T);
-                    cur.push_back({(char *)(d_U.p + uval_off[lb]), (char *)Llu->Unzval_br_ptr[lb], b});
-                    acc += b;
+                    add((const char *)(d_U.p + uval_off[lb]), (char *)Llu->Unzval_br_ptr[lb],
+                        (i64)Llu->Ufstnz_br_ptr[lb][1] * (i64)sizeof(T), (int)L);
                 }
             }
-            if (!cur.empty() && (acc >= 256e6 || L + 1 == levels.size())) {
-                d2h_batches.push_back({(int)L, merge_xfers(std::move(cur))});
-                cur.clear();
-                acc = 0;
-            }
+            if (fb >= D2H_MIN || L + 1 == levels.size()) close((int)L);
         }
+        d_push.upload(h_push.empty() ? vector<PushSeg>(1) : h_push);
+    }
+
+    // The D2H coordinator (runs on a helper thread during factor()).
+    void run_d2h(double &bytes, int64_t &ncopies) {
+        HIPCHK(hipSetDevice(comm ? comm->device : 0));
+        std::lock_guard<std::mutex> in_use(pinned_pool(1).use);
+        std::vector<char *> slot = pinned_pool(1).get(2, D2H_SLOT);
+        hipStream_t cs = nullptr;
+        hipEvent_t evf[2] = {nullptr, nullptr};
+        std::string err;
+        try {
+            int prio_lo = 0, prio_hi = 0;
+            HIPCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+            HIPCHK(hipStreamCreateWithPriority(&cs, hipStreamNonBlocking, prio_lo));
+            for (auto &e : evf) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            auto unpack = [&](const D2HFill &F, const char *src) {
+                parallel_for(F.hs_n, [&](int i) {
+                    const HostSeg &h = h_unpack[F.hs_off + i];
+                    memcpy(h.host, src + h.off, (size_t)h.bytes);
+                }, 1);
+                for (int i = 0; i < F.hs_n; ++i) bytes += (double)h_unpack[F.hs_off + i].bytes;
+                ncopies += F.hs_n;
+            };
+            for (size_t j = 0; j < d2h_fills.size(); ++j) {
+                const D2HFill &F = d2h_fills[j];
+                HIPCHK(hipStreamWaitEvent(cs, ev_pan[F.level], 0));
+                hipLaunchKernelGGL(k_push, dim3(std::min(F.seg_n, 64)), dim3(256), 0, cs,
+                                   (const PushSeg *)(d_push.p + F.seg_off), F.seg_n, slot[j & 1]);
+                HIPCHK(hipGetLastError());
+                HIPCHK(hipEventRecord(evf[j & 1], cs));
+                if (j > 0) {
+                    HIPCHK(hipEventSynchronize(evf[(j - 1) & 1]));
+                    unpack(d2h_fills[j - 1], slot[(j - 1) & 1]);
+                }
+            }
+            if (!d2h_fills.empty()) {
+                const size_t j = d2h_fills.size() - 1;
+                HIPCHK(hipEventSynchronize(evf[j & 1]));
+                unpack(d2h_fills[j], slot[j & 1]);
+            }
+        } catch (const std::exception &e) {
+            err = e.what();
+        }
+        if (cs) (void)hipStreamSynchronize(cs);
+        for (auto &e : evf)
+            if (e) (void)hipEventDestroy(e);
+        if (cs) (void)hipStreamDestroy(cs);
+        if (!err.empty()) throw Error(err);
     }
 
     DevBuf<T> d_L0, d_U0; // pristine copies (snapshot)
@@ -1484,23 +1648,11 @@ struct Plan : PlanBase {
         if (overlap_dl) {
             d2h = std::thread([&] {
                 const auto t0 = std::chrono::steady_clock::now();
-                hipStream_t cs = nullptr;
                 try {
-                    HIPCHK(hipSetDevice(comm ? comm->device : 0));
-                    HIPCHK(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
-                    for (const D2HBatch &B : d2h_batches) {
-                        HIPCHK(hipEventSynchronize(ev_pan[B.last_level]));
-                        for (const Xfer &x : B.xs) {
-                            HIPCHK(hipMemcpyAsync(x.host, x.dev, x.bytes, hipMemcpyDeviceToHost, cs));
-                            dbytes += (double)x.bytes;
-                            ++ncopies;
-                        }
-                    }
-                    HIPCHK(hipStreamSynchronize(cs));
+                    run_d2h(dbytes, ncopies);
                 } catch (const std::exception &e) {
                     d2h_err = e.what();
                 }
-                if (cs) (void)hipStreamDestroy(cs);
                 d2h_ms = ms_since(t0);
             });
         }

@@ -8,8 +8,8 @@
 // * H2D: staged through small pinned buffers by several host threads, each
 //   with its own buffers and HIP stream: a thread memcpys chunk c into its
 //   pinned buffer while the DMA engine moves its previous chunk.
-// * D2H: pageable hipMemcpyAsync on a copy stream (the fast direction),
-//   issued by a helper thread as the factorization finishes each level.
+// * D2H: finished blocks pushed by a kernel into pinned slots, scattered
+//   into the caller's arrays by host threads (engine.hip, run_d2h).
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -67,9 +67,37 @@ struct PinnedPool {
         return std::vector<char *>(bufs.begin(), bufs.begin() + n);
     }
 };
-inline PinnedPool &pinned_pool() {
-    static PinnedPool p;
-    return p;
+// pool 0: H2D staging ring, pool 1: D2H slots
+inline PinnedPool &pinned_pool(int which = 0) {
+    static PinnedPool p[2];
+    return p[which];
+}
+
+// One piece of a D2H "fill": bytes (<= 1 MB) at src (HBM) -> slot offset dst.
+struct PushSeg {
+    const char *src;
+    int64_t dst;
+    int bytes;
+};
+
+// GPU stores of finished factor blocks straight into a pinned host slot
+// (zero-copy over PCIe; 32-128 workgroups saturate the link).  Workgroup w
+// copies pieces w, w + G, ...; 8-byte words when the piece allows (d / z
+// values always), else 4-byte (s).
+__global__ void __launch_bounds__(256) k_push(const PushSeg *segs, int n, char *slot) {
+    for (int i = blockIdx.x; i < n; i += gridDim.x) {
+        const PushSeg g = segs[i];
+        char *dst = slot + g.dst;
+        if (((uintptr_t)g.src | (uintptr_t)dst | (uintptr_t)g.bytes) % 8 == 0) {
+            const uint64_t *s8 = (const uint64_t *)g.src;
+            uint64_t *d8 = (uint64_t *)dst;
+            for (int e = threadIdx.x; e < g.bytes / 8; e += 256) __builtin_nontemporal_store(s8[e], d8 + e);
+        } else {
+            const uint32_t *s4 = (const uint32_t *)g.src;
+            uint32_t *d4 = (uint32_t *)dst;
+            for (int e = threadIdx.x; e < g.bytes / 4; e += 256) __builtin_nontemporal_store(s4[e], d4 + e);
+        }
+    }
 }
 
 // Host -> device through a pinned ring: nthr threads, 2 buffers each.
@@ -85,8 +113,8 @@ inline void staged_h2d(const std::vector<Xfer> &xs, int device, int nthr = 4,
             pieces.push_back({&x, o, std::min(chunk, x.bytes - o)});
     if (pieces.empty()) return;
     nthr = std::max(1, std::min<int>(nthr, (int)pieces.size()));
-    std::lock_guard<std::mutex> in_use(pinned_pool().use);
-    std::vector<char *> pin = pinned_pool().get(2 * nthr, chunk);
+    std::lock_guard<std::mutex> in_use(pinned_pool(0).use);
+    std::vector<char *> pin = pinned_pool(0).get(2 * nthr, chunk);
     std::vector<std::string> errs(nthr);
     auto work = [&](int t) {
         hipStream_t s = nullptr;

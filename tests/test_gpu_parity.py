@@ -128,3 +128,28 @@ def test_gpu_factors_finite_with_poisoned_lds(kind, dims, dtype):
     pyoracle.oracle_factor([ref], 1, 1, A.n, False, an)
     err = cases.factor_error([gpu], [(ref.Lval, ref.Uval)])
     assert err < TOL[dtype], err
+
+
+@pytest.mark.parametrize("slot_kb,dtype", [(64, 0), (1024, 1), (256, 2), (0, 0)])
+def test_gpu_overlapped_upload_download(slot_kb, dtype, monkeypatch):
+    """The drop-in path's copies (hostio.h): the values go up beside the plan
+    build, each level's factors come back while later levels run, through
+    pinned slots (tiny slots here, so blocks split across fills)."""
+    if slot_kb:
+        monkeypatch.setenv("SLU_D2H_SLOT_KB", str(slot_kb))
+    kw = dict(diag=6 - 0.25, diag_im=-0.0025) if dtype == 2 else {}
+    A = Csc.stencil(STENCIL_3D7, 14, 14, 14, dtype=dtype, **kw)
+    S = Symbolic(A, nd_order(14, 14, 14), 60, 256)
+    gpu, ref = S.distribute(), S.distribute()
+    an = cases.anorm(A)
+    p = Plan(gpu, overlap_upload=True, overlap_download=True)
+    p.upload()
+    gpu.Lval[:] = np.nan                   # the write-back must cover every value
+    gpu.Uval[:] = np.nan
+    assert p.factor(an) == (0, 0)
+    p.download()                           # a no-op: already written back
+    st = p.stats()
+    assert st["d2h_bytes"] == st["lu_bytes"] and st["h2d_bytes"] == st["lu_bytes"]
+    pyoracle.oracle_factor([ref], 1, 1, A.n, False, an)
+    err = cases.factor_error([gpu], [(ref.Lval[:-1], ref.Uval[:-1])])
+    assert err < TOL[dtype], err

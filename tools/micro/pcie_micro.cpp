@@ -81,6 +81,13 @@ static void staged(char *host, char *dev, size_t bytes, bool h2d, int nthr, size
     CK(hipStreamDestroy(s));
 }
 
+// GPU stores straight into pinned host memory (zero-copy), nwg workgroups
+__global__ void k_push(const double *__restrict__ src, double *__restrict__ dst, size_t n) {
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (size_t)gridDim.x * blockDim.x)
+        __builtin_nontemporal_store(src[i], dst + i);
+}
+
 int main(int argc, char **argv) {
     size_t gb = argc > 1 ? atol(argv[1]) : 4;
     size_t bytes = gb << 30;
@@ -106,6 +113,46 @@ int main(int argc, char **argv) {
         staged(host, dev, bytes, false, nthr, 64 << 20);
         double b = now() - t;
         printf("{\"staged_threads\": %d, \"h2d_gbs\": %.1f, \"d2h_gbs\": %.1f}\n", nthr, rate(a), rate(b));
+    }
+    // many pageable D2H copies (the per-level write-back of the factors)
+    for (size_t piece : {(size_t)64 << 10, (size_t)512 << 10, (size_t)4 << 20}) {
+        hipStream_t s;
+        CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        t = now();
+        for (size_t o = 0; o < bytes; o += piece)
+            CK(hipMemcpyAsync(host + o, dev + o, std::min(piece, bytes - o), hipMemcpyDeviceToHost, s));
+        CK(hipStreamSynchronize(s));
+        double a = now() - t;
+        printf("{\"d2h_pageable_pieces_kb\": %zu, \"gbs\": %.1f, \"us_per_copy\": %.1f}\n", piece >> 10,
+               rate(a), a / (bytes / piece) * 1e6);
+        CK(hipStreamDestroy(s));
+    }
+    // GPU stores into pinned host memory
+    {
+        size_t pb = std::min(bytes, (size_t)1 << 30);
+        double *pin;
+        CK(hipHostMalloc((void **)&pin, pb));
+        for (int nwg : {32, 128, 512}) {
+            hipLaunchKernelGGL(k_push, dim3(nwg), dim3(256), 0, 0, (const double *)dev, pin, pb / 8);
+            CK(hipDeviceSynchronize());
+            t = now();
+            hipLaunchKernelGGL(k_push, dim3(nwg), dim3(256), 0, 0, (const double *)dev, pin, pb / 8);
+            CK(hipDeviceSynchronize());
+            double a = now() - t;
+            printf("{\"gpu_store_to_pinned_wg\": %d, \"gbs\": %.1f}\n", nwg, pb / a / 1e9);
+        }
+        // pinned -> pageable host memcpy with threads (the unpack side)
+        for (int nthr : {1, 4, 8}) {
+            t = now();
+            std::vector<std::thread> th;
+            size_t per = pb / nthr;
+            for (int i = 0; i < nthr; ++i)
+                th.emplace_back([=] { memcpy(host + i * per, (char *)pin + i * per, per); });
+            for (auto &x : th) x.join();
+            double a = now() - t;
+            printf("{\"memcpy_pinned_to_pageable_threads\": %d, \"gbs\": %.1f}\n", nthr, pb / a / 1e9);
+        }
+        CK(hipHostFree(pin));
     }
     t = now();
     CK(hipHostRegister(host, bytes, hipHostRegisterDefault));
