@@ -34,6 +34,7 @@
 #include <numeric>
 #include <string>
 #include <type_traits>
+#include <condition_variable>
 #include <thread>
 #include <vector>
 
@@ -50,6 +51,21 @@ namespace slu {
 
 static thread_local std::string g_last_error;
 void set_last_error(const std::string &s) { g_last_error = s; }
+
+// Host array without value-initialisation: large plan tables are filled by
+// parallel passes, so the first touch (page faults) is spread over threads.
+template <typename T> struct RawVec {
+    std::unique_ptr<T[]> a;
+    size_t n = 0;
+    void resize_uninit(size_t cnt) {
+        a.reset(cnt ? new T[cnt] : nullptr);
+        n = cnt;
+    }
+    T &operator[](size_t i) { return a[i]; }
+    const T &operator[](size_t i) const { return a[i]; }
+    size_t size() const { return n; }
+    const T *data() const { return a.get(); }
+};
 
 template <typename T> struct DevBuf {
     T *p = nullptr;
@@ -68,9 +84,11 @@ template <typename T> struct DevBuf {
         n = cnt;
         if (cnt) HIPCHK(hipMalloc(&p, cnt * sizeof(T)));
     }
-    void upload(const vector<T> &v) {
-        alloc(v.size());
-        if (!v.empty()) HIPCHK(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+    void upload(const vector<T> &v) { upload(v.data(), v.size()); }
+    void upload(const RawVec<T> &v) { upload(v.data(), v.size()); }
+    void upload(const T *h, size_t cnt) {
+        alloc(cnt);
+        if (cnt) HIPCHK(hipMemcpy(p, h, cnt * sizeof(T), hipMemcpyHostToDevice));
     }
     size_t bytes() const { return n * sizeof(T); }
 };
@@ -255,12 +273,12 @@ struct Plan : PlanBase {
     vector<LBlk> lblk;
     vector<int> lblk_ib;
     vector<int> lcol_first, lcol_nblk; // per local column
-    vector<int> lmap;
+    RawVec<int> lmap;
     vector<UBlk> ublk;
     vector<int> ublk_jb;
     vector<int> urow_first, urow_nblk;
-    vector<i64> ucol_voff;
-    vector<int> ucol_fst;
+    RawVec<i64> ucol_voff;
+    RawVec<int> ucol_fst;
 
     // ---- panels of every supernode as seen from this rank
     vector<const int_t *> lidx; // L(:,k) on my process row (reference index format) or null
@@ -280,7 +298,7 @@ struct Plan : PlanBase {
     vector<TrsmUItem<T>> tu_items;
     vector<KInfo<T>> kinfos;
     vector<TileItem> tiles, tiles_big;
-    vector<TileItem> lv_big[2], lv_small[2]; // per level being built: [0] critical, [1] rest
+
     vector<DiagItemF<T>> df_items;
     vector<TrsmItemF<T>> lf_items, uf_items;
     vector<CopyItem<T>> dcopy, pcopy;
@@ -381,7 +399,9 @@ struct Plan : PlanBase {
             layout_values();
             tick("layout_values");
             build_schedule();
-            if (prof) fprintf(stderr, "[slu plan %d]   (add_supernode %.1f ms)\n", iam, t_addsn);
+            if (prof)
+                fprintf(stderr, "[slu plan %d]   (add_supernode %.1f ms, merge + atomics %.1f ms)\n",
+                        iam, t_addsn, t_merge);
             tick("build_schedule");
             build_device();
             tick("build_device");
@@ -479,13 +499,14 @@ struct Plan : PlanBase {
         }
         lblk.assign(lcol_first[nlc], LBlk{});
         lblk_ib.assign(lcol_first[nlc], 0);
-        lmap.assign(mapbase[nlc], -1);
+        lmap.resize_uninit(mapbase[nlc]);
         parallel_for(nlc, [&](int ljb) {
             const int jb = ljb * Pc + mycol;
             const int_t *index = Llu->Lrowind_bc_ptr[ljb];
             if (!index) return;
             const int nb = (int)index[0], nsupr = (int)index[1];
             i64 p = SLU_BC_HEADER, mo = mapbase[ljb];
+            std::fill(&lmap[mapbase[ljb]], &lmap[0] + mapbase[ljb + 1], -1);
             int rs = 0;
             for (int b = 0; b < nb; ++b) {
                 const int gb = (int)index[p], nr = (int)index[p + 1];
@@ -527,8 +548,8 @@ struct Plan : PlanBase {
         }
         ublk.assign(urow_first[nlr], UBlk{});
         ublk_jb.assign(urow_first[nlr], 0);
-        ucol_voff.assign(colbase[nlr], 0);
-        ucol_fst.assign(colbase[nlr], 0);
+        ucol_voff.resize_uninit(colbase[nlr]);
+        ucol_fst.resize_uninit(colbase[nlr]);
         parallel_for(nlr, [&](int lb) {
             const int gb = lb * Pr + myrow;
             const int_t *index = Llu->Ufstnz_br_ptr[lb];
@@ -782,8 +803,8 @@ struct Plan : PlanBase {
                         lrows(k, m, r0);
                         if (c == mycol) { // pack my rows below the diagonal block
                             int ljb = k / Pc;
-                            add_copy(pcopy, /*src*/ 0, lval_off[ljb] + r0, lval_ld[ljb], 1, pan_total,
-                                     m, m, W(k));
+                            add_copy(pcopy, pcopy_src, /*src*/ 0, lval_off[ljb] + r0, lval_ld[ljb], 1,
+                                     pan_total, m, m, W(k));
                         } else {
                             lpos[k] = pan_total;
                         }
@@ -798,7 +819,8 @@ struct Plan : PlanBase {
                         if (k % Pr != r || !uidx[k]) continue;
                         i64 len = uidx[k][1];
                         if (r == myrow) {
-                            add_copy(pcopy, /*src*/ 1, uval_off[k / Pr], len, 1, pan_total, len, len, 1);
+                            add_copy(pcopy, pcopy_src, /*src*/ 1, uval_off[k / Pr], len, 1, pan_total, len,
+                                     len, 1);
                         } else {
                             upos[k] = pan_total;
                         }
@@ -815,9 +837,8 @@ struct Plan : PlanBase {
     // 1 = U values; dst = d_dpk (dst_space 0) or d_pan (1)) and relocated in
     // build_device.  Chunked to <= COPY_CHUNK elements.
     vector<char> pcopy_src, dcopy_src;
-    void add_copy(vector<CopyItem<T>> &v, int src_space, i64 src_off, i64 lds, int dst_space,
-                  i64 dst_off, i64 ldd, i64 rows, i64 cols) {
-        vector<char> &tag = (&v == &pcopy) ? pcopy_src : dcopy_src;
+    static void add_copy(vector<CopyItem<T>> &v, vector<char> &tag, int src_space, i64 src_off,
+                         i64 lds, int dst_space, i64 dst_off, i64 ldd, i64 rows, i64 cols) {
         if (cols == 1) {
             for (i64 e = 0; e < rows; e += COPY_CHUNK) {
                 CopyItem<T> c{};
@@ -832,7 +853,7 @@ struct Plan : PlanBase {
             return;
         }
         if (lds == rows && ldd == rows) { // contiguous: copy as 1D
-            add_copy(v, src_space, src_off, 0, dst_space, dst_off, 0, rows * cols, 1);
+            add_copy(v, tag, src_space, src_off, 0, dst_space, dst_off, 0, rows * cols, 1);
             return;
         }
         const i64 cpc = std::max<i64>(1, COPY_CHUNK / std::max<i64>(rows, 1));
@@ -850,7 +871,40 @@ struct Plan : PlanBase {
     }
 
     // ------------------------------------------------------- schedule
-    double t_addsn = 0;
+    // One supernode's (or a chunk of one level's supernodes') share of the
+    // schedule; offsets into its own h_* arrays are relocated when merged.
+    struct KInfoHost {
+        vector<int> dests;
+    };
+    struct SchedOut {
+        vector<DiagItem<T>> diag_items;
+        vector<DiagItemF<T>> df_items;
+        vector<TrsmLItem<T>> tl_items;
+        vector<TrsmUItem<T>> tu_items;
+        vector<TrsmItemF<T>> lf_items, uf_items;
+        vector<KInfo<T>> kinfos;
+        vector<KInfoHost> khost;
+        vector<TileItem> big[2], small[2]; // [0] critical, [1] rest
+        vector<CopyItem<T>> dcopy;
+        vector<char> dcopy_src;
+        vector<int> h_rg, h_ra, h_cg, h_cb, h_pair, h_ct0;
+        vector<i64> h_cvoff;
+        double panel_flops = 0, schur_flops = 0, schur_flops_padded = 0, scatter_bytes = 0;
+        double R_schur_flops = 0, R_big_flops = 0;
+        i64 n_diag = 0, n_trsm_items = 0, n_schur_tiles = 0;
+        bool R_big = false;
+    };
+    vector<KInfoHost> khost;
+
+    template <typename V> static void append(V &dst, const V &src) {
+        dst.insert(dst.end(), src.begin(), src.end());
+    }
+    template <typename P> static P *shift(P *p, i64 d) { return (P *)((intptr_t)p + d); }
+
+    double t_addsn = 0, t_merge = 0;
+    // Supernodes of a level are independent: chunks of them are scheduled in
+    // parallel (parallel_for) into SchedOut's and merged in supernode order,
+    // which reproduces the sequential layout exactly.
     void build_schedule() {
         // value buffers first: work items point straight into them
         d_dpk.alloc(std::max<i64>(dpk_total, 1));
@@ -869,18 +923,134 @@ struct Plan : PlanBase {
             R.lf_off = (int)lf_items.size();
             R.uf_off = (int)uf_items.size();
             R.dc_off = (int)dcopy.size();
-            for (int c = 0; c < 2; ++c) lv_big[c].clear(), lv_small[c].clear();
+            const vector<int> &ks = bylev[L];
+            const int nk = (int)ks.size();
+            const int nch = nk >= 128 ? std::min(4 * plan_threads(), nk / 32) : 1;
+            vector<SchedOut> outs(nch);
             const auto ta = std::chrono::steady_clock::now();
-            for (int k : bylev[L]) add_supernode(k, R);
+            parallel_for(nch, [&](int c) {
+                const int a = (int)((i64)nk * c / nch), b = (int)((i64)nk * (c + 1) / nch);
+                for (int i = a; i < b; ++i) add_supernode(ks[i], outs[c]);
+            }, 1);
             t_addsn += ms_since(ta);
+            const auto tm0 = std::chrono::steady_clock::now();
+            // merge in supernode order: bases by prefix sums, then every chunk
+            // copies (and relocates) its slices in parallel
+            enum { V_DIAG, V_DF, V_TL, V_TU, V_LF, V_UF, V_K, V_DC, V_RG, V_CG, V_PAIR, V_N };
+            vector<std::array<i64, V_N>> base(nch);
+            {
+                std::array<i64, V_N> b = {(i64)diag_items.size(), (i64)df_items.size(),
+                                          (i64)tl_items.size(), (i64)tu_items.size(),
+                                          (i64)lf_items.size(), (i64)uf_items.size(),
+                                          (i64)kinfos.size(), (i64)dcopy.size(), (i64)h_rg.size(),
+                                          (i64)h_cg.size(), (i64)h_pair.size()};
+                for (int c = 0; c < nch; ++c) {
+                    const SchedOut &O = outs[c];
+                    base[c] = b;
+                    b[V_DIAG] += O.diag_items.size();
+                    b[V_DF] += O.df_items.size();
+                    b[V_TL] += O.tl_items.size();
+                    b[V_TU] += O.tu_items.size();
+                    b[V_LF] += O.lf_items.size();
+                    b[V_UF] += O.uf_items.size();
+                    b[V_K] += O.kinfos.size();
+                    b[V_DC] += O.dcopy.size();
+                    b[V_RG] += O.h_rg.size();
+                    b[V_CG] += O.h_cg.size();
+                    b[V_PAIR] += O.h_pair.size();
+                }
+                diag_items.resize(b[V_DIAG]);
+                df_items.resize(b[V_DF]);
+                tl_items.resize(b[V_TL]);
+                tu_items.resize(b[V_TU]);
+                lf_items.resize(b[V_LF]);
+                uf_items.resize(b[V_UF]);
+                kinfos.resize(b[V_K]);
+                khost.resize(b[V_K]);
+                dcopy.resize(b[V_DC]);
+                dcopy_src.resize(b[V_DC]);
+                h_rg.resize(b[V_RG]);
+                h_ra.resize(b[V_RG]);
+                h_cg.resize(b[V_CG]);
+                h_cb.resize(b[V_CG]);
+                h_ct0.resize(b[V_CG]);
+                h_cvoff.resize(b[V_CG]);
+                h_pair.resize(b[V_PAIR]);
+            }
+            parallel_for(nch, [&](int c) {
+                SchedOut &O = outs[c];
+                const std::array<i64, V_N> &B = base[c];
+                const i64 bc = B[V_CG], br = B[V_RG], bp = B[V_PAIR];
+                for (auto &k : O.kinfos) {
+                    k.cvoff = shift(k.cvoff, bc);
+                    k.ct0 = shift(k.ct0, bc);
+                    k.cg = shift(k.cg, bc);
+                    k.cb = shift(k.cb, bc);
+                    k.rg = shift(k.rg, br);
+                    k.ra = shift(k.ra, br);
+                    k.pair = shift(k.pair, bp);
+                }
+                for (auto &t : O.uf_items) {
+                    t.voff = shift(t.voff, bc);
+                    t.t0 = shift(t.t0, bc);
+                }
+                for (auto &t : O.tu_items) {
+                    t.voff = shift(t.voff, bc);
+                    t.t0 = shift(t.t0, bc);
+                }
+                auto put = [](auto &dst, const auto &src, i64 at) {
+                    std::copy(src.begin(), src.end(), dst.begin() + at);
+                };
+                put(diag_items, O.diag_items, B[V_DIAG]);
+                put(df_items, O.df_items, B[V_DF]);
+                put(tl_items, O.tl_items, B[V_TL]);
+                put(tu_items, O.tu_items, B[V_TU]);
+                put(lf_items, O.lf_items, B[V_LF]);
+                put(uf_items, O.uf_items, B[V_UF]);
+                put(kinfos, O.kinfos, B[V_K]);
+                for (size_t i = 0; i < O.khost.size(); ++i) khost[B[V_K] + i] = std::move(O.khost[i]);
+                put(dcopy, O.dcopy, B[V_DC]);
+                put(dcopy_src, O.dcopy_src, B[V_DC]);
+                put(h_rg, O.h_rg, br);
+                put(h_ra, O.h_ra, br);
+                put(h_cg, O.h_cg, bc);
+                put(h_cb, O.h_cb, bc);
+                put(h_ct0, O.h_ct0, bc);
+                put(h_cvoff, O.h_cvoff, bc);
+                put(h_pair, O.h_pair, bp);
+            }, 1);
+            vector<int> kbase(nch);
+            for (int c = 0; c < nch; ++c) {
+                const SchedOut &O = outs[c];
+                kbase[c] = (int)(base[c][V_K] - R.k_off);
+                stats.panel_flops += O.panel_flops;
+                stats.schur_flops += O.schur_flops;
+                stats.schur_flops_padded += O.schur_flops_padded;
+                stats.scatter_bytes += O.scatter_bytes;
+                stats.n_diag += O.n_diag;
+                stats.n_trsm_items += O.n_trsm_items;
+                stats.n_schur_tiles += O.n_schur_tiles;
+                R.schur_flops += O.R_schur_flops;
+                R.big_flops += O.R_big_flops;
+                R.big = R.big || O.R_big;
+            }
             // critical tiles first: they are launched ahead of the rest so the
             // next level's panels can be factored while the rest runs
-            R.bigc_n = (int)lv_big[0].size();
-            R.tilec_n = (int)lv_small[0].size();
-            for (int c = 0; c < 2; ++c) {
-                tiles_big.insert(tiles_big.end(), lv_big[c].begin(), lv_big[c].end());
-                tiles.insert(tiles.end(), lv_small[c].begin(), lv_small[c].end());
-            }
+            for (int cls = 0; cls < 2; ++cls)
+                for (int c = 0; c < nch; ++c) {
+                    for (TileItem t : outs[c].big[cls]) {
+                        t.kslot += kbase[c];
+                        tiles_big.push_back(t);
+                    }
+                    for (TileItem t : outs[c].small[cls]) {
+                        t.kslot += kbase[c];
+                        tiles.push_back(t);
+                    }
+                    if (cls == 0) {
+                        R.bigc_n += (int)outs[c].big[0].size();
+                        R.tilec_n += (int)outs[c].small[0].size();
+                    }
+                }
             R.big_n = (int)tiles_big.size() - R.big_off;
             R.df_n = (int)df_items.size() - R.df_off;
             R.lf_n = (int)lf_items.size() - R.lf_off;
@@ -907,6 +1077,7 @@ struct Plan : PlanBase {
                 }
             }
             for (int key : touched) owner[key] = -1;
+            t_merge += ms_since(tm0);
             for (int i = R.big_off; i < R.big_off + R.big_n; ++i)
                 R.atomic_tiles += kinfos[R.k_off + tiles_big[i].kslot].atomic;
             for (int i = R.tile_off; i < R.tile_off + R.tile_n; ++i)
@@ -915,12 +1086,7 @@ struct Plan : PlanBase {
         khost.clear();
     }
 
-    struct KInfoHost {
-        vector<int> dests;
-    };
-    vector<KInfoHost> khost;
-
-    void add_supernode(int k, LevelRange &R) {
+    void add_supernode(int k, SchedOut &O) const {
         const int w = W(k);
         const int ljb = k / Pc, lb = k / Pr;
         const bool lcol_here = (k % Pc) == mycol && lidx[k];
@@ -952,7 +1118,7 @@ struct Plan : PlanBase {
                 d.w = w;
                 d.k = k;
                 d.fcol = (int)xsup[k];
-                df_items.push_back(d);
+                O.df_items.push_back(d);
             } else {
                 DiagItem<T> d{};
                 d.a = dT;
@@ -960,13 +1126,13 @@ struct Plan : PlanBase {
                 d.w = w;
                 d.k = k;
                 d.fcol = (int)xsup[k];
-                diag_items.push_back(d);
+                O.diag_items.push_back(d);
             }
-            if (xmode) add_copy(dcopy, 0, lval_off[ljb], dld, 0, pkg[k], w, w, w);
-            stats.n_diag++;
+            if (xmode) add_copy(O.dcopy, O.dcopy_src, 0, lval_off[ljb], dld, 0, pkg[k], w, w, w);
+            O.n_diag++;
             // SRC/pdgstrf2.c:252,262 (complex weights SRC/pzgstrf2.c:253,263)
             double wd = w, s1 = wd * (wd - 1) / 2, s2 = (wd - 1) * wd * (2 * wd - 1) / 6;
-            stats.panel_flops += cplx ? 6 * s1 + 10 * wd + 8 * s2 : s1 + 2 * s2;
+            O.panel_flops += cplx ? 6 * s1 + 10 * wd + 8 * s2 : s1 + 2 * s2;
         }
         // ---- L panel TRSM (rows of column k below the diagonal block)
         int m = 0, r0 = 0;
@@ -983,8 +1149,8 @@ struct Plan : PlanBase {
                     t.ldt = dld;
                     t.w = w;
                     t.nrows = std::min(RB, m - c0);
-                    lf_items.push_back(t);
-                    stats.n_trsm_items++;
+                    O.lf_items.push_back(t);
+                    O.n_trsm_items++;
                 }
             } else {
                 for (int c0 = 0; c0 < m; c0 += TRSM_THREADS) {
@@ -995,16 +1161,16 @@ struct Plan : PlanBase {
                     t.ldu = dld;
                     t.w = w;
                     t.nrows = std::min(TRSM_THREADS, m - c0);
-                    tl_items.push_back(t);
-                    stats.n_trsm_items++;
+                    O.tl_items.push_back(t);
+                    O.n_trsm_items++;
                 }
             }
-            stats.panel_flops += (cplx ? 4.0 : 1.0) * (double)w * (w + 1) * m;
+            O.panel_flops += (cplx ? 4.0 : 1.0) * (double)w * (w + 1) * m;
         }
         // ---- U panel: nonempty columns of block row k on my process column
         vector<int> ujb; // U blocks with a nonempty column
         int ncols = 0, kmin = w;
-        const int cols_off = (int)h_cg.size();
+        const int cols_off = (int)O.h_cg.size();
         if (uidx[k]) {
             const int_t *ix = uidx[k];
             const i64 klst = xsup[k + 1];
@@ -1018,17 +1184,17 @@ struct Plan : PlanBase {
                     const i64 fst = ix[p + SLU_UB_DESCRIPTOR + c];
                     if (fst >= klst) continue;
                     any = true;
-                    h_cg.push_back((int)xsup[jb] + c);
-                    h_cb.push_back(bidx);
-                    h_cvoff.push_back(base + run);
+                    O.h_cg.push_back((int)xsup[jb] + c);
+                    O.h_cb.push_back(bidx);
+                    O.h_cvoff.push_back(base + run);
                     const int t0 = (int)(fst - xsup[k]);
-                    h_ct0.push_back(t0);
+                    O.h_ct0.push_back(t0);
                     kmin = std::min(kmin, t0);
                     ++ncols;
                     run += klst - fst;
                     if (urow_here) {
                         double seg = (double)(klst - fst);
-                        stats.panel_flops += seg * (seg + 1);
+                        O.panel_flops += seg * (seg + 1);
                     }
                 }
                 if (any) ujb.push_back(jb);
@@ -1049,8 +1215,8 @@ struct Plan : PlanBase {
                 t.ldt = dld;
                 t.w = w;
                 t.nrows = std::min(RB, ncols - c0);
-                uf_items.push_back(t);
-                stats.n_trsm_items++;
+                O.uf_items.push_back(t);
+                O.n_trsm_items++;
             }
             for (int c0 = 0; !fast && c0 < ncols; c0 += TRSM_THREADS) {
                 TrsmUItem<T> t{};
@@ -1062,10 +1228,10 @@ struct Plan : PlanBase {
                 t.voff = (const i64 *)(intptr_t)(cols_off + c0); // relocated
                 t.t0 = (const int *)(intptr_t)(cols_off + c0);
                 int km = w;
-                for (int c = 0; c < t.ncols; ++c) km = std::min(km, h_ct0[cols_off + c0 + c]);
+                for (int c = 0; c < t.ncols; ++c) km = std::min(km, O.h_ct0[cols_off + c0 + c]);
                 t.kmin = km;
-                tu_items.push_back(t);
-                stats.n_trsm_items++;
+                O.tu_items.push_back(t);
+                O.n_trsm_items++;
             }
         }
         if (m == 0 || ncols == 0) return; // nothing to update from k here
@@ -1090,7 +1256,7 @@ struct Plan : PlanBase {
         ki.ct0 = (const int *)(intptr_t)cols_off;
         ki.cg = (const int *)(intptr_t)cols_off;
         ki.cb = (const int *)(intptr_t)cols_off;
-        const int rows_off = (int)h_rg.size();
+        const int rows_off = (int)O.h_rg.size();
         vector<int> lib_; // L blocks (ib) of the panel below the diagonal
         {
             const int_t *ix = lidx[k];
@@ -1101,8 +1267,8 @@ struct Plan : PlanBase {
                     const int a = (int)lib_.size();
                     lib_.push_back(gb);
                     for (int i = 0; i < nr; ++i) {
-                        h_rg.push_back((int)ix[p + 2 + i]);
-                        h_ra.push_back(a);
+                        O.h_rg.push_back((int)ix[p + 2 + i]);
+                        O.h_ra.push_back(a);
                     }
                 }
                 p += SLU_LB_DESCRIPTOR + nr;
@@ -1110,19 +1276,19 @@ struct Plan : PlanBase {
         }
         ki.rg = (const int *)(intptr_t)rows_off;
         ki.ra = (const int *)(intptr_t)rows_off;
-        const int pair_off = (int)h_pair.size();
+        const int pair_off = (int)O.h_pair.size();
         KInfoHost kh;
         for (int ib : lib_)
             for (int jb : ujb) {
                 int h = ib >= jb ? find_lblk(ib, jb) : ~find_ublk(ib, jb);
-                h_pair.push_back(h);
+                O.h_pair.push_back(h);
                 kh.dests.push_back(h);
             }
         ki.pair = (const int *)(intptr_t)pair_off;
         ki.atomic = 0;
-        kinfos.push_back(ki);
-        khost.push_back(std::move(kh));
-        const int slot = (int)kinfos.size() - 1 - R.k_off;
+        O.kinfos.push_back(ki);
+        O.khost.push_back(std::move(kh));
+        const int slot = (int)O.kinfos.size() - 1; // relocated by the merge
         const bool big = !cplx && m >= SB_BM && ncols >= SB_BN;
         const int BM = big ? SB_BM : SC_BM, BN = big ? SB_BN : SC_BN;
         const int tm = (m + BM - 1) / BM, tn = (ncols + BN - 1) / BN;
@@ -1133,25 +1299,25 @@ struct Plan : PlanBase {
         const int nl = level_of[k] + 1;
         vector<char> crow(tm, 0), ccol(tn, 0);
         for (int r = 0; r < m; ++r)
-            if (level_of[lib_[h_ra[rows_off + r]]] == nl) crow[r / BM] = 1;
+            if (level_of[lib_[O.h_ra[rows_off + r]]] == nl) crow[r / BM] = 1;
         for (int c = 0; c < ncols; ++c)
-            if (level_of[ujb[h_cb[cols_off + c]]] == nl) ccol[c / BN] = 1;
+            if (level_of[ujb[O.h_cb[cols_off + c]]] == nl) ccol[c / BN] = 1;
         for (int i = 0; i < tm; ++i)
             for (int j = 0; j < tn; ++j) {
                 const int cls = (crow[i] || ccol[j]) ? 0 : 1;
-                (big ? lv_big[cls] : lv_small[cls]).push_back(TileItem{slot, i, j});
+                (big ? O.big[cls] : O.small[cls]).push_back(TileItem{slot, i, j});
             }
         // algorithmic work: exact unpadded flops and padded flops
         double fl = 0;
-        for (int c = 0; c < ncols; ++c) fl += 2.0 * m * (w - h_ct0[cols_off + c]);
+        for (int c = 0; c < ncols; ++c) fl += 2.0 * m * (w - O.h_ct0[cols_off + c]);
         const double mult = cplx ? 4.0 : 1.0; // complex: 8 real flops per multiply-add
-        stats.schur_flops += fl * mult;
-        stats.schur_flops_padded += 2.0 * m * ncols * (double)(w - kmin) * mult;
-        stats.scatter_bytes += 3.0 * sizeof(T) * (double)m * ncols;
-        stats.n_schur_tiles += (i64)tm * tn;
-        R.schur_flops += fl * mult;
-        if (big) R.big_flops += fl * mult;
-        if (w >= 64 && m >= 256 && ncols >= 256) R.big = true;
+        O.schur_flops += fl * mult;
+        O.schur_flops_padded += 2.0 * m * ncols * (double)(w - kmin) * mult;
+        O.scatter_bytes += 3.0 * sizeof(T) * (double)m * ncols;
+        O.n_schur_tiles += (i64)tm * tn;
+        O.R_schur_flops += fl * mult;
+        if (big) O.R_big_flops += fl * mult;
+        if (w >= 64 && m >= 256 && ncols >= 256) O.R_big = true;
     }
 
     // ------------------------------------------------------- device
@@ -1308,7 +1474,7 @@ struct Plan : PlanBase {
     // the caller's arrays while the next fill is pushed.
     // slot / minimum fill (SLU_D2H_SLOT_KB overrides the slot: tests use tiny
     // slots so that blocks split across fills)
-    i64 D2H_SLOT = 256ll << 20, D2H_MIN = 64ll << 20;
+    i64 D2H_SLOT = 128ll << 20, D2H_MIN = 32ll << 20;
     static constexpr i64 D2H_PIECE = 1ll << 20;
     struct D2HFill {
         int level;        // all blocks final after ev_pan[level]
@@ -1373,47 +1539,85 @@ struct Plan : PlanBase {
         d_push.upload(h_push.empty() ? vector<PushSeg>(1) : h_push);
     }
 
-    // The D2H coordinator (runs on a helper thread during factor()).
+    // The D2H pipeline (runs on a helper thread during factor()): this
+    // thread queues k_push of fill j into slot j % NS as soon as the slot's
+    // previous fill has been scattered; an unpack thread scatters fill j once
+    // its push event has fired (parallel host memcpy).
     void run_d2h(double &bytes, int64_t &ncopies) {
         HIPCHK(hipSetDevice(comm ? comm->device : 0));
+        constexpr int NS = 4;
         std::lock_guard<std::mutex> in_use(pinned_pool(1).use);
-        std::vector<char *> slot = pinned_pool(1).get(2, D2H_SLOT);
+        std::vector<char *> slot = pinned_pool(1).get(NS, D2H_SLOT);
         hipStream_t cs = nullptr;
-        hipEvent_t evf[2] = {nullptr, nullptr};
+        hipEvent_t evf[NS] = {};
+        std::mutex mu;
+        std::condition_variable cv;
+        int pushed = 0, unpacked = 0;
+        bool fail = false;
         std::string err;
+        auto set_err = [&](const char *what) {
+            std::lock_guard<std::mutex> lk(mu);
+            if (err.empty()) err = what;
+            fail = true;
+            cv.notify_all();
+        };
+        const int nf = (int)d2h_fills.size();
+        std::thread unpacker;
         try {
             int prio_lo = 0, prio_hi = 0;
             HIPCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
-            HIPCHK(hipStreamCreateWithPriority(&cs, hipStreamNonBlocking, prio_lo));
+            const char *pe = getenv("SLU_D2H_PRIO"); // diagnostics: lo | hi
+            HIPCHK(hipStreamCreateWithPriority(&cs, hipStreamNonBlocking,
+                                               pe && !strcmp(pe, "hi") ? prio_hi : prio_lo));
+            const char *ge = getenv("SLU_D2H_WG");
+            const int nwg = ge ? std::max(1, atoi(ge)) : 32;
             for (auto &e : evf) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-            auto unpack = [&](const D2HFill &F, const char *src) {
-                parallel_for(F.hs_n, [&](int i) {
-                    const HostSeg &h = h_unpack[F.hs_off + i];
-                    memcpy(h.host, src + h.off, (size_t)h.bytes);
-                }, 1);
-                for (int i = 0; i < F.hs_n; ++i) bytes += (double)h_unpack[F.hs_off + i].bytes;
-                ncopies += F.hs_n;
-            };
-            for (size_t j = 0; j < d2h_fills.size(); ++j) {
+            unpacker = std::thread([&] {
+                try {
+                    HIPCHK(hipSetDevice(comm ? comm->device : 0));
+                    for (int j = 0; j < nf; ++j) {
+                        {
+                            std::unique_lock<std::mutex> lk(mu);
+                            cv.wait(lk, [&] { return pushed > j || fail; });
+                            if (fail) return;
+                        }
+                        HIPCHK(hipEventSynchronize(evf[j % NS]));
+                        const D2HFill &F = d2h_fills[j];
+                        const char *src = slot[j % NS];
+                        parallel_for(F.hs_n, [&](int i) {
+                            const HostSeg &h = h_unpack[F.hs_off + i];
+                            memcpy(h.host, src + h.off, (size_t)h.bytes);
+                        }, 1);
+                        for (int i = 0; i < F.hs_n; ++i) bytes += (double)h_unpack[F.hs_off + i].bytes;
+                        ncopies += F.hs_n;
+                        std::lock_guard<std::mutex> lk(mu);
+                        unpacked = j + 1;
+                        cv.notify_all();
+                    }
+                } catch (const std::exception &e) {
+                    set_err(e.what());
+                }
+            });
+            for (int j = 0; j < nf; ++j) {
+                {
+                    std::unique_lock<std::mutex> lk(mu);
+                    cv.wait(lk, [&] { return unpacked >= j - NS + 1 || fail; });
+                    if (fail) break;
+                }
                 const D2HFill &F = d2h_fills[j];
                 HIPCHK(hipStreamWaitEvent(cs, ev_pan[F.level], 0));
-                hipLaunchKernelGGL(k_push, dim3(std::min(F.seg_n, 64)), dim3(256), 0, cs,
-                                   (const PushSeg *)(d_push.p + F.seg_off), F.seg_n, slot[j & 1]);
+                hipLaunchKernelGGL(k_push, dim3(std::min(F.seg_n, nwg)), dim3(256), 0, cs,
+                                   (const PushSeg *)(d_push.p + F.seg_off), F.seg_n, slot[j % NS]);
                 HIPCHK(hipGetLastError());
-                HIPCHK(hipEventRecord(evf[j & 1], cs));
-                if (j > 0) {
-                    HIPCHK(hipEventSynchronize(evf[(j - 1) & 1]));
-                    unpack(d2h_fills[j - 1], slot[(j - 1) & 1]);
-                }
-            }
-            if (!d2h_fills.empty()) {
-                const size_t j = d2h_fills.size() - 1;
-                HIPCHK(hipEventSynchronize(evf[j & 1]));
-                unpack(d2h_fills[j], slot[j & 1]);
+                HIPCHK(hipEventRecord(evf[j % NS], cs));
+                std::lock_guard<std::mutex> lk(mu);
+                pushed = j + 1;
+                cv.notify_all();
             }
         } catch (const std::exception &e) {
-            err = e.what();
+            set_err(e.what());
         }
+        if (unpacker.joinable()) unpacker.join();
         if (cs) (void)hipStreamSynchronize(cs);
         for (auto &e : evf)
             if (e) (void)hipEventDestroy(e);
@@ -1645,6 +1849,10 @@ struct Plan : PlanBase {
         int64_t ncopies = 0;
         double dbytes = 0;
         const bool overlap_dl = opts.overlap_download != 0;
+        // diagnostics: SLU_D2H_AFTER=1 starts the D2H only after the device
+        // finished the factorization (no overlap, same copy path)
+        const bool d2h_after = overlap_dl && getenv("SLU_D2H_AFTER");
+        if (d2h_after) sync();
         if (overlap_dl) {
             d2h = std::thread([&] {
                 const auto t0 = std::chrono::steady_clock::now();
