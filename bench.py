@@ -397,7 +397,12 @@ def main():
                        "nnz_L": S.nnzL, "parallelism": f"2D block-cyclic {pr}x{pc}",
                        "transport": ("host-staged gloo (REHEARSAL, not a measurement)"
                                      if grid is not None else
-                                     ("rccl" if world > 1 else "none"))},
+                                     (f"rccl ({world} ranks, row/column communicators)"
+                                      if world > 1 else "none")),
+                       "hbm_gb_rank0": round((st0["lu_bytes"] + st0["index_bytes"] +
+                                              st0["comm_buf_bytes"]) / 1e9, 2),
+                       "comm_ring_gb_rank0": round(st0["comm_buf_bytes"] / 1e9, 3),
+                       "comm_volume_gb_rank0": round(st0["comm_bytes"] / 1e9, 3)},
             "roofline": roof,
             "cpu_baseline": cpu,
             "next_rows": nxt,

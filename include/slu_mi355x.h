@@ -211,7 +211,8 @@ typedef struct {
     double schur_big_flops;    /* flops of the supernodes on 128x128 tiles */
     int64_t n_schur_launches;
     int64_t n_schur_big_launches;
-    double comm_bytes;         /* bytes this rank sends + receives per factor */
+    double comm_bytes;         /* bytes of the broadcast sections this rank
+                                  takes part in (as root or receiver) per factor */
     double t_solve_ms;         /* device time of the last slu_plan_solve */
     double t_fill_ms;          /* device time of the last slu_plan_fill_a */
     double t_refine_ms;        /* device time of the last slu_plan_refine */
@@ -225,6 +226,7 @@ typedef struct {
     double t_d2h_tail_ms;      /* D2H after the device finished the factorization */
     double h2d_bytes, d2h_bytes;
     int64_t n_d2h_copies;
+    double comm_buf_bytes;     /* HBM of the receive ring (diag packages + panels) */
 } slu_plan_stats;
 int slu_plan_get_stats(const slu_plan *p, slu_plan_stats *st);
 

@@ -740,6 +740,14 @@ struct Plan : PlanBase {
     // Diagonal packages [w*w factored block, ld w | Dinv] and remote panels
     // are laid out per level in broadcast order: sections of the owners in my
     // process column (root = their process row), then of my process row.
+    // Receive buffers are a ring, as the reference's num_lookaheads + 1
+    // rotating Lsub_buf_2 / Lval_buf_2 (SRC/pdgstrf.c:454-512): with the
+    // one-level look-ahead of factor() only levels L and L+1 are live at a
+    // time -- panel(L+2) is issued on the panel stream after it waited for
+    // the rest of level L's Schur update (ev_rest[L]) -- so the panels use
+    // two slots of the largest level, and the diagonal packages (read only
+    // by the TRSMs of their own level, on the same stream) one.
+    vector<i64> pan_level; // panel bytes (elements) per level
     bool lsend(int k) const { // L(:,k) on my process row has rows below the diagonal block
         int m, r0;
         lrows(k, m, r0);
@@ -763,6 +771,8 @@ struct Plan : PlanBase {
                 continue;
             }
             // ---- diag packages: owner (r, mycol) for all r, then (myrow, c), c != mycol
+            dpk_total = 0;  // per-level cursor (one slot, reused by every level)
+            pan_total = 0;  // per-level cursor (the slot base is added below)
             vector<i64> own_off(Pr * Pc, -1), own_cnt(Pr * Pc, 0);
             auto lay_owner = [&](int orow, int ocol) {
                 const int o = orow * Pc + ocol;
@@ -830,8 +840,27 @@ struct Plan : PlanBase {
                 }
             R.ps_n = (int)psecs.size() - R.ps_off;
             R.pc_n = (int)pcopy.size() - R.pc_off;
+            pan_level.push_back(pan_total);
+            dpk_slot = std::max(dpk_slot, dpk_total);
+            comm_volume += dpk_total + pan_total;
         }
+        if (!xmode) return;
+        // odd levels use the second panel slot
+        const i64 slot = *std::max_element(pan_level.begin(), pan_level.end());
+        for (size_t L = 1; L < levels.size(); L += 2) {
+            const LevelRange &R = levels[L];
+            for (int k : bylev[L]) {
+                if (lpos[k] >= 0) lpos[k] += slot;
+                if (upos[k] >= 0) upos[k] += slot;
+            }
+            for (int i = R.ps_off; i < R.ps_off + R.ps_n; ++i) psecs[i].off += slot;
+            for (int i = R.pc_off; i < R.pc_off + R.pc_n; ++i)
+                pcopy[i].dst = (T *)((intptr_t)pcopy[i].dst + slot);
+        }
+        pan_total = levels.size() > 1 ? 2 * slot : slot;
+        dpk_total = dpk_slot;
     }
+    i64 dpk_slot = 0, comm_volume = 0;
 
     // Copy items are recorded with symbolic bases (src space 0 = L values,
     // 1 = U values; dst = d_dpk (dst_space 0) or d_pan (1)) and relocated in
@@ -1394,7 +1423,8 @@ struct Plan : PlanBase {
                                      d_cg.bytes() + d_cb.bytes() + d_pair.bytes() +
                                      d_ct0.bytes() + d_cvoff.bytes() + d_dcopy.bytes() +
                                      d_pcopy.bytes());
-        stats.comm_bytes = (double)(dpk_total + pan_total) * sizeof(T);
+        stats.comm_bytes = (double)comm_volume * sizeof(T);
+        stats.comm_buf_bytes = (double)(dpk_total + pan_total) * sizeof(T);
     }
 
     // ------------------------------------------------------- values

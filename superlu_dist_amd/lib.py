@@ -63,7 +63,7 @@ class PlanStats(C.Structure):
                 ("t_upload_ms", C.c_double), ("t_upload_wait_ms", C.c_double),
                 ("t_d2h_ms", C.c_double), ("t_d2h_tail_ms", C.c_double),
                 ("h2d_bytes", C.c_double), ("d2h_bytes", C.c_double),
-                ("n_d2h_copies", C.c_int64)]
+                ("n_d2h_copies", C.c_int64), ("comm_buf_bytes", C.c_double)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
