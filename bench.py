@@ -313,7 +313,7 @@ def main():
     # kernel-level roofline: one more factorization with every launch on one
     # stream, so k_schur_big launch durations are not stretched by the
     # look-ahead kernels running beside them (not part of the timed steps)
-    plan.set_timing(1, serial=True)
+    plan.set_timing(2 if args.level_log else 1, serial=True)  # level log: serialized kernel times
     one_step()
     sst = plan.stats()
     plan.set_timing(2 if args.level_log else 1, serial=False)

@@ -123,18 +123,28 @@ struct Xport {
     hipStream_t s = nullptr;
     struct Op {
         int g, root;
-        void *buf;
+        void *buf; // null on a member that does not need the section
         size_t bytes;
+        uint32_t mask; // members (group ranks) that receive it
     };
     vector<Op> ops;
     vector<char> hbuf;
+    double sent = 0, recvd = 0; // bytes this rank moved (RCCL sections)
     int gsize(int g) const {
         return g == G_WORLD ? c->nprow * c->npcol : g == G_ROW ? c->npcol : c->nprow;
     }
     int grank(int g) const { return g == G_WORLD ? c->iam : g == G_ROW ? c->mycol : c->myrow; }
     ncclComm_t comm_of(int g) const { return g == G_WORLD ? c->world : g == G_ROW ? c->row : c->col; }
     void bcast(int g, int root, void *buf, size_t bytes) {
-        if (bytes && gsize(g) > 1) ops.push_back({g, root, buf, bytes});
+        if (bytes && gsize(g) > 1) ops.push_back({g, root, buf, bytes, ~0u});
+    }
+    // A section of root's data for the members in mask (the reference sends
+    // L(:,k) only to the process columns flagged in ToSendR,
+    // SRC/pdgstrf.c:1039-1044, SRC/pddistribute.c:779).  Every member of the
+    // group queues the op (buf = null when not in mask), so that the host
+    // transport, which can only broadcast, stays in step.
+    void section(int g, int root, uint32_t mask, void *buf, size_t bytes) {
+        if (bytes && gsize(g) > 1 && (mask & ~(1u << root))) ops.push_back({g, root, buf, bytes, mask});
     }
     void flush() {
         if (ops.empty()) return;
@@ -142,17 +152,37 @@ struct Xport {
             HIPCHK(hipStreamSynchronize(s));
             for (auto &o : ops) {
                 hbuf.resize(o.bytes);
-                const bool root = grank(o.g) == o.root;
+                const int me = grank(o.g);
+                const bool root = me == o.root;
                 if (root) HIPCHK(hipMemcpy(hbuf.data(), o.buf, o.bytes, hipMemcpyDeviceToHost));
                 SLU_REQUIRE(c->host_fn(c->host_ctx, o.g, o.root, hbuf.data(), (int64_t)o.bytes) == 0,
                             "host broadcast (group %d, root %d, %zu bytes) failed", o.g, o.root,
                             o.bytes);
-                if (!root) HIPCHK(hipMemcpy(o.buf, hbuf.data(), o.bytes, hipMemcpyHostToDevice));
+                if (!root && (o.mask >> me & 1)) {
+                    SLU_REQUIRE(o.buf, "section of group %d root %d has no buffer", o.g, o.root);
+                    HIPCHK(hipMemcpy(o.buf, hbuf.data(), o.bytes, hipMemcpyHostToDevice));
+                }
             }
         } else {
+            // bcast ops as ncclBroadcast; sections as direct sends from the
+            // root to each member that needs them (xGMI is point to point:
+            // a root's sends to its row / column peers use distinct links)
             NCCLCHK(ncclGroupStart());
-            for (auto &o : ops)
-                NCCLCHK(ncclBroadcast(o.buf, o.buf, o.bytes, ncclChar, o.root, comm_of(o.g), s));
+            for (auto &o : ops) {
+                const int me = grank(o.g), P = gsize(o.g);
+                if (o.mask == ~0u) {
+                    NCCLCHK(ncclBroadcast(o.buf, o.buf, o.bytes, ncclChar, o.root, comm_of(o.g), s));
+                } else if (me == o.root) {
+                    for (int m = 0; m < P; ++m)
+                        if (m != me && (o.mask >> m & 1)) {
+                            NCCLCHK(ncclSend(o.buf, o.bytes, ncclChar, m, comm_of(o.g), s));
+                            sent += (double)o.bytes;
+                        }
+                } else if (o.mask >> me & 1) {
+                    NCCLCHK(ncclRecv(o.buf, o.bytes, ncclChar, o.root, comm_of(o.g), s));
+                    recvd += (double)o.bytes;
+                }
+            }
             NCCLCHK(ncclGroupEnd());
         }
         ops.clear();
@@ -217,7 +247,8 @@ struct LevelRange {
 // one broadcast of a contiguous section of a device arena
 struct Sec {
     int g, root, arena; // arena 0: diag packages, 1: panels
-    i64 off, cnt;       // in elements
+    i64 off, cnt;       // in elements; off < 0: not received here
+    uint32_t mask;      // group ranks that receive the section
 };
 
 struct PlanBase {
@@ -393,6 +424,7 @@ struct Plan : PlanBase {
             build_local();
             tick("build_local");
             exchange_index();
+            exchange_needs();
             tick("exchange_index");
             compute_levels();
             tick("compute_levels");
@@ -675,6 +707,46 @@ struct Plan : PlanBase {
         }
     }
 
+    // Who needs what (2D grids), as the reference's ToSendR / ToSendD
+    // (SRC/pddistribute.c:752-801) but derived from the exchanged structure:
+    //   rneed[k*Pc + pc]: U(k,:) has blocks on process column pc -- those
+    //     ranks need L(:,k) and the factored diagonal block (U-TRSM on the
+    //     owner's process row);
+    //   cneed[k*Pr + pr]: L(:,k) has rows below the diagonal block on process
+    //     row pr -- those ranks need U(k,:) and the diagonal block (L-TRSM).
+    // Each rank knows its own column's / row's entries; one row and one
+    // column all-gather make them global on every rank.
+    vector<char> rneed, cneed;
+    void exchange_needs() {
+        if (!xmode) return;
+        rneed.assign((size_t)nsupers * Pc, 0);
+        cneed.assign((size_t)nsupers * Pr, 0);
+        vector<i64> mine_r(nsupers), mine_c(nsupers);
+        for (int k = 0; k < nsupers; ++k) {
+            mine_r[k] = uidx[k] != nullptr;
+            mine_c[k] = lsend(k);
+        }
+        vector<vector<i64>> ar, ac;
+        if (Pc > 1) ar = X.allgatherv(G_ROW, mine_r);
+        else ar.push_back(mine_r);
+        if (Pr > 1) ac = X.allgatherv(G_COL, mine_c);
+        else ac.push_back(mine_c);
+        for (int k = 0; k < nsupers; ++k) {
+            for (int c = 0; c < Pc; ++c) rneed[(size_t)k * Pc + c] = (char)ar[c][k];
+            for (int r = 0; r < Pr; ++r) cneed[(size_t)k * Pr + r] = (char)ac[r][k];
+        }
+    }
+    uint32_t rmask(int k) const {
+        uint32_t m = 0;
+        for (int c = 0; c < Pc; ++c) m |= (uint32_t)rneed[(size_t)k * Pc + c] << c;
+        return m;
+    }
+    uint32_t cmask(int k) const {
+        uint32_t m = 0;
+        for (int r = 0; r < Pr; ++r) m |= (uint32_t)cneed[(size_t)k * Pr + r] << r;
+        return m;
+    }
+
     // ------------------------------------------------------- levels
     // Dependency DAG k -> ib (L(ib,k) != 0) and k -> jb (U(k,jb) != 0); all
     // edges point to larger supernode numbers, so one ascending sweep gives
@@ -770,79 +842,117 @@ struct Plan : PlanBase {
                 dscr_max = std::max(dscr_max, off);
                 continue;
             }
-            // ---- diag packages: owner (r, mycol) for all r, then (myrow, c), c != mycol
+            // ---- diag packages: owner (r, mycol) for all r, then (myrow, c),
+            // c != mycol.  One section per owner and group; its mask is the
+            // union over the owner's supernodes of the ranks that need a
+            // package (packages are small: w*w + Dinv per supernode).
             dpk_total = 0;  // per-level cursor (one slot, reused by every level)
             pan_total = 0;  // per-level cursor (the slot base is added below)
-            vector<i64> own_off(Pr * Pc, -1), own_cnt(Pr * Pc, 0);
             auto lay_owner = [&](int orow, int ocol) {
-                const int o = orow * Pc + ocol;
-                i64 start = dpk_total;
+                const bool me = orow == myrow && ocol == mycol;
+                uint32_t cm = 0, rm = 0;
+                i64 cnt = 0;
                 for (int k : ks)
                     if (k % Pr == orow && k % Pc == ocol) {
-                        pkg[k] = dpk_total;
-                        dpk_total += (i64)W(k) * W(k) + dinv_len(W(k));
+                        cm |= cmask(k);
+                        rm |= rmask(k);
+                        cnt += (i64)W(k) * W(k) + dinv_len(W(k));
                     }
-                own_off[o] = start;
-                own_cnt[o] = dpk_total - start;
+                if (!cnt) return;
+                cm &= ~(1u << orow);
+                rm &= ~(1u << ocol);
+                const bool here = me || (ocol == mycol && (cm >> myrow & 1)) ||
+                                  (orow == myrow && (rm >> mycol & 1));
+                const i64 start = here ? dpk_total : -1;
+                if (here)
+                    for (int k : ks)
+                        if (k % Pr == orow && k % Pc == ocol) {
+                            pkg[k] = dpk_total;
+                            dpk_total += (i64)W(k) * W(k) + dinv_len(W(k));
+                        }
+                auto sec = [&](int g, int root, uint32_t mask, bool rcv) {
+                    if (!mask) return;
+                    dsecs.push_back({g, root, 0, (me || rcv) ? start : -1, cnt, mask});
+                    if (me) comm_volume += cnt * __builtin_popcount(mask);
+                    else if (rcv) comm_volume += cnt;
+                };
+                if (Pr > 1 && ocol == mycol) sec(G_COL, orow, cm, cm >> myrow & 1);
+                if (Pc > 1 && orow == myrow) sec(G_ROW, ocol, rm, rm >> mycol & 1);
             };
+            R.ds_off = (int)dsecs.size();
             for (int r = 0; r < Pr; ++r) lay_owner(r, mycol);
             for (int c = 0; c < Pc; ++c)
                 if (c != mycol) lay_owner(myrow, c);
-            R.ds_off = (int)dsecs.size();
-            if (Pr > 1)
-                for (int r = 0; r < Pr; ++r) {
-                    int o = r * Pc + mycol;
-                    if (own_cnt[o]) dsecs.push_back({G_COL, r, 0, own_off[o], own_cnt[o]});
-                }
-            if (Pc > 1)
-                for (int c = 0; c < Pc; ++c) {
-                    int o = myrow * Pc + c;
-                    if (own_cnt[o]) dsecs.push_back({G_ROW, c, 0, own_off[o], own_cnt[o]});
-                }
             R.ds_n = (int)dsecs.size() - R.ds_off;
             // ---- panels: L(:,k) along my process row (root = owning column),
-            //      U(k,:) along my process column (root = owning row)
+            //      U(k,:) along my process column (root = owning row).  The
+            //      supernodes of a root are grouped by the set of ranks that
+            //      need them (same order on every member), one section per
+            //      group, sent only to those ranks.
             R.ps_off = (int)psecs.size();
             R.pc_off = (int)pcopy.size();
+            auto lay_panels = [&](int g, int root, vector<std::pair<uint32_t, int>> &km) {
+                std::sort(km.begin(), km.end());
+                const int me = g == G_ROW ? mycol : myrow;
+                for (size_t i = 0; i < km.size();) {
+                    size_t j = i;
+                    while (j < km.size() && km[j].first == km[i].first) ++j;
+                    const uint32_t mask = km[i].first;
+                    const bool rcv = me != root && (mask >> me & 1);
+                    if (mask) {
+                        const i64 start = (me == root || rcv) ? pan_total : -1;
+                        i64 cnt = 0;
+                        for (size_t q = i; q < j; ++q) {
+                            const int k = km[q].second;
+                            i64 len;
+                            if (g == G_ROW) {
+                                int m, r0;
+                                lrows(k, m, r0);
+                                len = (i64)m * W(k);
+                                if (me == root) {
+                                    const int ljb = k / Pc;
+                                    add_copy(pcopy, pcopy_src, /*src*/ 0, lval_off[ljb] + r0,
+                                             lval_ld[ljb], 1, pan_total, m, m, W(k));
+                                } else if (rcv) {
+                                    lpos[k] = pan_total;
+                                }
+                            } else {
+                                len = uidx[k][1];
+                                if (me == root) {
+                                    add_copy(pcopy, pcopy_src, /*src*/ 1, uval_off[k / Pr], len, 1,
+                                             pan_total, len, len, 1);
+                                } else if (rcv) {
+                                    upos[k] = pan_total;
+                                }
+                            }
+                            if (me == root || rcv) pan_total += len;
+                            cnt += len;
+                        }
+                        psecs.push_back({g, root, 1, start, cnt, mask});
+                        if (me == root) comm_volume += cnt * __builtin_popcount(mask);
+                        else if (rcv) comm_volume += cnt;
+                    }
+                    i = j;
+                }
+            };
             if (Pc > 1)
                 for (int c = 0; c < Pc; ++c) {
-                    i64 start = pan_total;
-                    for (int k : ks) {
-                        if (k % Pc != c || !lsend(k)) continue;
-                        int m, r0;
-                        lrows(k, m, r0);
-                        if (c == mycol) { // pack my rows below the diagonal block
-                            int ljb = k / Pc;
-                            add_copy(pcopy, pcopy_src, /*src*/ 0, lval_off[ljb] + r0, lval_ld[ljb], 1,
-                                     pan_total, m, m, W(k));
-                        } else {
-                            lpos[k] = pan_total;
-                        }
-                        pan_total += (i64)m * W(k);
-                    }
-                    if (pan_total > start) psecs.push_back({G_ROW, c, 1, start, pan_total - start});
+                    vector<std::pair<uint32_t, int>> km;
+                    for (int k : ks)
+                        if (k % Pc == c && lsend(k)) km.push_back({rmask(k) & ~(1u << c), k});
+                    lay_panels(G_ROW, c, km);
                 }
             if (Pr > 1)
                 for (int r = 0; r < Pr; ++r) {
-                    i64 start = pan_total;
-                    for (int k : ks) {
-                        if (k % Pr != r || !uidx[k]) continue;
-                        i64 len = uidx[k][1];
-                        if (r == myrow) {
-                            add_copy(pcopy, pcopy_src, /*src*/ 1, uval_off[k / Pr], len, 1, pan_total, len,
-                                     len, 1);
-                        } else {
-                            upos[k] = pan_total;
-                        }
-                        pan_total += len;
-                    }
-                    if (pan_total > start) psecs.push_back({G_COL, r, 1, start, pan_total - start});
+                    vector<std::pair<uint32_t, int>> km;
+                    for (int k : ks)
+                        if (k % Pr == r && uidx[k]) km.push_back({cmask(k) & ~(1u << r), k});
+                    lay_panels(G_COL, r, km);
                 }
             R.ps_n = (int)psecs.size() - R.ps_off;
             R.pc_n = (int)pcopy.size() - R.pc_off;
             pan_level.push_back(pan_total);
             dpk_slot = std::max(dpk_slot, dpk_total);
-            comm_volume += dpk_total + pan_total;
         }
         if (!xmode) return;
         // odd levels use the second panel slot
@@ -853,7 +963,8 @@ struct Plan : PlanBase {
                 if (lpos[k] >= 0) lpos[k] += slot;
                 if (upos[k] >= 0) upos[k] += slot;
             }
-            for (int i = R.ps_off; i < R.ps_off + R.ps_n; ++i) psecs[i].off += slot;
+            for (int i = R.ps_off; i < R.ps_off + R.ps_n; ++i)
+                if (psecs[i].off >= 0) psecs[i].off += slot;
             for (int i = R.pc_off; i < R.pc_off + R.pc_n; ++i)
                 pcopy[i].dst = (T *)((intptr_t)pcopy[i].dst + slot);
         }
@@ -1743,7 +1854,8 @@ struct Plan : PlanBase {
         for (int i = off; i < off + n_; ++i) {
             const Sec &s = secs[i];
             T *base = s.arena ? d_pan.p : d_dpk.p;
-            X.bcast(s.g, s.root, base + s.off, (size_t)s.cnt * sizeof(T));
+            X.section(s.g, s.root, s.mask, s.off >= 0 ? base + s.off : nullptr,
+                      (size_t)s.cnt * sizeof(T));
         }
         X.flush();
     }
