@@ -848,41 +848,52 @@ struct Plan : PlanBase {
             // package (packages are small: w*w + Dinv per supernode).
             dpk_total = 0;  // per-level cursor (one slot, reused by every level)
             pan_total = 0;  // per-level cursor (the slot base is added below)
+            // layout first (owners (r, mycol) for all r, then (myrow, c)), then
+            // the sections in the canonical order every member of a group
+            // shares: column groups by root row, row groups by root column
+            struct Own {
+                uint32_t cm = 0, rm = 0;
+                i64 start = -1, cnt = 0;
+            };
+            vector<Own> own(Pr * Pc);
             auto lay_owner = [&](int orow, int ocol) {
                 const bool me = orow == myrow && ocol == mycol;
-                uint32_t cm = 0, rm = 0;
-                i64 cnt = 0;
+                Own &o = own[orow * Pc + ocol];
                 for (int k : ks)
                     if (k % Pr == orow && k % Pc == ocol) {
-                        cm |= cmask(k);
-                        rm |= rmask(k);
-                        cnt += (i64)W(k) * W(k) + dinv_len(W(k));
+                        o.cm |= cmask(k);
+                        o.rm |= rmask(k);
+                        o.cnt += (i64)W(k) * W(k) + dinv_len(W(k));
                     }
-                if (!cnt) return;
-                cm &= ~(1u << orow);
-                rm &= ~(1u << ocol);
-                const bool here = me || (ocol == mycol && (cm >> myrow & 1)) ||
-                                  (orow == myrow && (rm >> mycol & 1));
-                const i64 start = here ? dpk_total : -1;
-                if (here)
-                    for (int k : ks)
-                        if (k % Pr == orow && k % Pc == ocol) {
-                            pkg[k] = dpk_total;
-                            dpk_total += (i64)W(k) * W(k) + dinv_len(W(k));
-                        }
-                auto sec = [&](int g, int root, uint32_t mask, bool rcv) {
-                    if (!mask) return;
-                    dsecs.push_back({g, root, 0, (me || rcv) ? start : -1, cnt, mask});
-                    if (me) comm_volume += cnt * __builtin_popcount(mask);
-                    else if (rcv) comm_volume += cnt;
-                };
-                if (Pr > 1 && ocol == mycol) sec(G_COL, orow, cm, cm >> myrow & 1);
-                if (Pc > 1 && orow == myrow) sec(G_ROW, ocol, rm, rm >> mycol & 1);
+                if (!o.cnt) return;
+                o.cm &= ~(1u << orow);
+                o.rm &= ~(1u << ocol);
+                const bool here = me || (ocol == mycol && (o.cm >> myrow & 1)) ||
+                                  (orow == myrow && (o.rm >> mycol & 1));
+                if (!here) return;
+                o.start = dpk_total;
+                for (int k : ks)
+                    if (k % Pr == orow && k % Pc == ocol) {
+                        pkg[k] = dpk_total;
+                        dpk_total += (i64)W(k) * W(k) + dinv_len(W(k));
+                    }
             };
-            R.ds_off = (int)dsecs.size();
             for (int r = 0; r < Pr; ++r) lay_owner(r, mycol);
             for (int c = 0; c < Pc; ++c)
                 if (c != mycol) lay_owner(myrow, c);
+            R.ds_off = (int)dsecs.size();
+            auto sec = [&](int g, int root, const Own &o, uint32_t mask) {
+                if (!mask || !o.cnt) return;
+                const int me = g == G_ROW ? mycol : myrow;
+                const bool rcv = me != root && (mask >> me & 1);
+                dsecs.push_back({g, root, 0, (me == root || rcv) ? o.start : -1, o.cnt, mask});
+                if (me == root) comm_volume += o.cnt * __builtin_popcount(mask);
+                else if (rcv) comm_volume += o.cnt;
+            };
+            if (Pr > 1)
+                for (int r = 0; r < Pr; ++r) sec(G_COL, r, own[r * Pc + mycol], own[r * Pc + mycol].cm);
+            if (Pc > 1)
+                for (int c = 0; c < Pc; ++c) sec(G_ROW, c, own[myrow * Pc + c], own[myrow * Pc + c].rm);
             R.ds_n = (int)dsecs.size() - R.ds_off;
             // ---- panels: L(:,k) along my process row (root = owning column),
             //      U(k,:) along my process column (root = owning row).  The
