@@ -420,6 +420,22 @@ struct Plan : PlanBase {
                 }
             });
         }
+        if (opts.overlap_download) {
+            // the pinned D2H slots (hipHostMalloc, ~0.1 s the first time in a
+            // process) are allocated beside the plan build too
+            if (const char *e = getenv("SLU_D2H_SLOT_KB")) {
+                D2H_SLOT = std::max<i64>(16, atoll(e)) << 10;
+                D2H_MIN = D2H_SLOT / 4;
+            }
+            pin_thread = std::thread([this] {
+                try {
+                    HIPCHK(hipSetDevice(comm ? comm->device : 0));
+                    pinned_pool(1).get(D2H_NS, D2H_SLOT);
+                } catch (const std::exception &e) {
+                    up_err = e.what();
+                }
+            });
+        }
         try {
             build_local();
             tick("build_local");
@@ -441,6 +457,7 @@ struct Plan : PlanBase {
             tick("build_d2h");
         } catch (...) {
             if (up_thread.joinable()) up_thread.join();
+            if (pin_thread.joinable()) pin_thread.join();
             throw;
         }
         stats.t_plan_ms = ms_since(t0);
@@ -463,6 +480,7 @@ struct Plan : PlanBase {
 
     ~Plan() override {
         if (up_thread.joinable()) up_thread.join();
+        if (pin_thread.joinable()) pin_thread.join();
         for (auto e : ev_pan) (void)hipEventDestroy(e);
         for (auto e : ev_rest) (void)hipEventDestroy(e);
         if (ev_start) (void)hipEventDestroy(ev_start);
@@ -1559,7 +1577,7 @@ struct Plan : PlanBase {
     int snap_state = 0;
 
     // ---- host <-> HBM copies of the values (hostio.h)
-    std::thread up_thread;
+    std::thread up_thread, pin_thread;
     std::string up_err;
     double up_ms = 0;
     bool host_current = false; // the host LUstruct holds what the device holds
@@ -1596,6 +1614,7 @@ struct Plan : PlanBase {
 
     void upload() override {
         const auto t0 = std::chrono::steady_clock::now();
+        if (pin_thread.joinable()) pin_thread.join();
         if (up_thread.joinable()) {
             up_thread.join();
             if (!up_err.empty()) {
@@ -1628,6 +1647,7 @@ struct Plan : PlanBase {
     // slots so that blocks split across fills)
     i64 D2H_SLOT = 128ll << 20, D2H_MIN = 32ll << 20;
     static constexpr i64 D2H_PIECE = 1ll << 20;
+    static constexpr int D2H_NS = 4; // pinned slots in flight
     struct D2HFill {
         int level;        // all blocks final after ev_pan[level]
         int seg_off, seg_n; // PushSeg range
@@ -1642,13 +1662,10 @@ struct Plan : PlanBase {
     vector<PushSeg> h_push;
     vector<HostSeg> h_unpack;
     DevBuf<PushSeg> d_push;
+    DevBuf<char> d_stage; // HBM staging slots of the D2H (SDMA mode)
 
     void build_d2h() {
         if (!opts.overlap_download) return;
-        if (const char *e = getenv("SLU_D2H_SLOT_KB")) {
-            D2H_SLOT = std::max<i64>(16, atoll(e)) << 10;
-            D2H_MIN = D2H_SLOT / 4;
-        }
         LocalLU *Llu = LU->Llu;
         i64 fb = 0; // bytes in the open fill
         int seg0 = 0, hs0 = 0;
@@ -1696,8 +1713,9 @@ struct Plan : PlanBase {
     // previous fill has been scattered; an unpack thread scatters fill j once
     // its push event has fired (parallel host memcpy).
     void run_d2h(double &bytes, int64_t &ncopies) {
+        double t_wait_push = 0, t_unpack = 0, t_wait_slot = 0;
         HIPCHK(hipSetDevice(comm ? comm->device : 0));
-        constexpr int NS = 4;
+        constexpr int NS = D2H_NS;
         std::lock_guard<std::mutex> in_use(pinned_pool(1).use);
         std::vector<char *> slot = pinned_pool(1).get(NS, D2H_SLOT);
         hipStream_t cs = nullptr;
@@ -1723,6 +1741,9 @@ struct Plan : PlanBase {
                                                pe && !strcmp(pe, "hi") ? prio_hi : prio_lo));
             const char *ge = getenv("SLU_D2H_WG");
             const int nwg = ge ? std::max(1, atoi(ge)) : 32;
+            const char *me = getenv("SLU_D2H_MODE"); // diagnostics: push (zero-copy) | sdma
+            const bool use_sdma = !(me && !strcmp(me, "push"));
+            if (use_sdma && d_stage.n < (size_t)NS * D2H_SLOT) d_stage.alloc((size_t)NS * D2H_SLOT);
             for (auto &e : evf) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
             unpacker = std::thread([&] {
                 try {
@@ -1733,13 +1754,17 @@ struct Plan : PlanBase {
                             cv.wait(lk, [&] { return pushed > j || fail; });
                             if (fail) return;
                         }
+                        const auto tw = std::chrono::steady_clock::now();
                         HIPCHK(hipEventSynchronize(evf[j % NS]));
+                        const auto tu = std::chrono::steady_clock::now();
+                        t_wait_push += std::chrono::duration<double, std::milli>(tu - tw).count();
                         const D2HFill &F = d2h_fills[j];
                         const char *src = slot[j % NS];
                         parallel_for(F.hs_n, [&](int i) {
                             const HostSeg &h = h_unpack[F.hs_off + i];
                             memcpy(h.host, src + h.off, (size_t)h.bytes);
                         }, 1);
+                        t_unpack += ms_since(tu);
                         for (int i = 0; i < F.hs_n; ++i) bytes += (double)h_unpack[F.hs_off + i].bytes;
                         ncopies += F.hs_n;
                         std::lock_guard<std::mutex> lk(mu);
@@ -1752,15 +1777,28 @@ struct Plan : PlanBase {
             });
             for (int j = 0; j < nf; ++j) {
                 {
+                    const auto tw = std::chrono::steady_clock::now();
                     std::unique_lock<std::mutex> lk(mu);
                     cv.wait(lk, [&] { return unpacked >= j - NS + 1 || fail; });
+                    t_wait_slot += ms_since(tw);
                     if (fail) break;
                 }
                 const D2HFill &F = d2h_fills[j];
                 HIPCHK(hipStreamWaitEvent(cs, ev_pan[F.level], 0));
-                hipLaunchKernelGGL(k_push, dim3(std::min(F.seg_n, nwg)), dim3(256), 0, cs,
-                                   (const PushSeg *)(d_push.p + F.seg_off), F.seg_n, slot[j % NS]);
-                HIPCHK(hipGetLastError());
+                if (use_sdma) {
+                    // gather into an HBM slot (HBM-bound, microseconds), then
+                    // one DMA-engine copy to the pinned slot: the PCIe-bound
+                    // part occupies no CU while the factorization runs
+                    char *ds = d_stage.p + (size_t)(j % NS) * D2H_SLOT;
+                    hipLaunchKernelGGL(k_push, dim3(std::min(F.seg_n, 4 * nwg)), dim3(256), 0, cs,
+                                       (const PushSeg *)(d_push.p + F.seg_off), F.seg_n, ds);
+                    HIPCHK(hipGetLastError());
+                    HIPCHK(hipMemcpyAsync(slot[j % NS], ds, (size_t)F.bytes, hipMemcpyDeviceToHost, cs));
+                } else {
+                    hipLaunchKernelGGL(k_push, dim3(std::min(F.seg_n, nwg)), dim3(256), 0, cs,
+                                       (const PushSeg *)(d_push.p + F.seg_off), F.seg_n, slot[j % NS]);
+                    HIPCHK(hipGetLastError());
+                }
                 HIPCHK(hipEventRecord(evf[j % NS], cs));
                 std::lock_guard<std::mutex> lk(mu);
                 pushed = j + 1;
@@ -1770,6 +1808,9 @@ struct Plan : PlanBase {
             set_err(e.what());
         }
         if (unpacker.joinable()) unpacker.join();
+        if (prof)
+            fprintf(stderr, "[slu d2h %d] fills %d, unpack waits for push %.1f ms, unpack %.1f ms, "
+                    "push waits for a slot %.1f ms\n", iam, nf, t_wait_push, t_unpack, t_wait_slot);
         if (cs) (void)hipStreamSynchronize(cs);
         for (auto &e : evf)
             if (e) (void)hipEventDestroy(e);

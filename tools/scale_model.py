@@ -57,39 +57,60 @@ def parse_log(path):
 
 
 def level_volumes(nx):
-    """Per level: bytes of L panels below the diagonal blocks and of U panels."""
+    """Per supernode: level, bytes of L(:,k) below the diagonal block, bytes
+    of U(k,:), and the L block rows / U block columns (for the need masks)."""
     from superlu_dist_amd.frontend import STENCIL_3D7, Csc, Symbolic, nd_order
     A = Csc.stencil(STENCIL_3D7, nx, nx, nx)
     S = Symbolic(A, nd_order(nx, nx, nx), 60, 256)
     lu = S.distribute()
     ns, xs = S.nsupers, S.xsup
     lvl = np.zeros(ns, dtype=np.int64)
-    lp = np.zeros(ns)
-    up = np.zeros(ns)
+    sn = []
     for k in range(ns):
         ix = lu.Lidx[lu.Loff[k]:]
         w = xs[k + 1] - xs[k]
-        lp[k] = (ix[1] - w) * w * 8.0
-        p = 2
+        lrows, p, ib_list = [], 2, []
         for _ in range(int(ix[0])):
-            ib = ix[p]
+            ib, nr = int(ix[p]), int(ix[p + 1])
             if ib != k:
                 lvl[ib] = max(lvl[ib], lvl[k] + 1)
-            p += 2 + ix[p + 1]
+                ib_list.append((ib, nr))
+            p += 2 + nr
+        jb_list, ub = [], 0.0
         if lu.Uoff[k] >= 0:
             iu = lu.Uidx[lu.Uoff[k]:]
-            up[k] = iu[1] * 8.0
+            ub = iu[1] * 8.0
             p = 3
             for _ in range(int(iu[0])):
-                jb = iu[p]
+                jb = int(iu[p])
                 lvl[jb] = max(lvl[jb], lvl[k] + 1)
+                jb_list.append(jb)
                 p += 2 + xs[jb + 1] - xs[jb]
+        sn.append((k, int(w), ib_list, jb_list, ub))
+    return lvl, sn
+
+
+def recv_volumes(lvl, sn, pr, pc):
+    """Average bytes a rank receives per level with the sparse sections of
+    engine.hip (a rank gets L(:,k) only if U(k,:) has blocks on its process
+    column, U(k,:) only if L(:,k) has rows on its process row)."""
     nl = int(lvl.max()) + 1
-    return ([float(lp[lvl == L].sum()) for L in range(nl)],
-            [float(up[lvl == L].sum()) for L in range(nl)])
+    vol = np.zeros(nl)
+    for k, w, ib_list, jb_list, ub in sn:
+        cols = {jb % pc for jb in jb_list} - {k % pc}
+        rows_with = {}
+        for ib, nr in ib_list:
+            rows_with[ib % pr] = rows_with.get(ib % pr, 0) + nr
+        # L panel rows of process row r go to the needing columns of that row
+        lbytes = sum(nr * w * 8.0 for nr in rows_with.values())
+        vol[lvl[k]] += lbytes * len(cols) / (pr * pc)
+        # U(k,:) on column c (1/pc of it) goes to the rows that have L rows
+        need_rows = set(rows_with) - {k % pr}
+        vol[lvl[k]] += ub * len(need_rows) / (pr * pc)
+    return vol
 
 
-def model(rows, Lp, Up, pr, pc, bw, lat):
+def model(rows, vol, pr, pc, bw, lat):
     P = pr * pc
     waves = lambda t: max(1, math.ceil(t / 512))  # noqa: E731
     chain, schur = [], []
@@ -99,7 +120,7 @@ def model(rows, Lp, Up, pr, pc, bw, lat):
             chain.append(r["diag"] + r["trsm"])
             schur.append(r["schur"])
             continue
-        recv = Lp[L] / pr * (pc - 1) / pc + Up[L] / pc * (pr - 1) / pr
+        recv = vol[L]
         ncoll = (pr > 1) + (pc > 1)  # one grouped diag broadcast + one grouped panel broadcast
         comm = 2 * ncoll * lat * 1e-3 + recv / bw / 1e6
         chain.append(r["diag"] + r["trsm"] / ((pr + pc) / 2) + comm)
@@ -118,21 +139,23 @@ def main():
     ap.add_argument("--nx", type=int, default=100)
     ap.add_argument("--bw", type=float, default=50.0, help="GB/s per rank per broadcast")
     ap.add_argument("--lat", type=float, default=30.0, help="us per collective")
+    ap.add_argument("--t1", type=float, default=None,
+                    help="measured 1-GPU factor time (ms); default: sum of the log's level walls")
     a = ap.parse_args()
     rows = parse_log(a.log)
-    Lp, Up = level_volumes(a.nx)
-    t1, _, _ = model(rows, Lp, Up, 1, 1, a.bw, a.lat)
-    out = {"levels": len(rows), "bw_GBs": a.bw, "lat_us": a.lat, "t1_ms": round(t1, 1),
-           "panel_volume_GB": round((sum(Lp) + sum(Up)) / 1e9, 2)}
+    lvl, sn = level_volumes(a.nx)
+    t1, _, _ = model(rows, None, 1, 1, a.bw, a.lat)
+    if a.t1:
+        t1 = a.t1
+    out = {"levels": len(rows), "bw_GBs": a.bw, "lat_us": a.lat, "t1_ms": round(t1, 1)}
     for pr, pc in ((1, 2), (2, 2), (2, 4), (4, 2)):
-        t, chain, schur = model(rows, Lp, Up, pr, pc, a.bw, a.lat)
+        vol = recv_volumes(lvl, sn, pr, pc)
+        t, chain, schur = model(rows, vol, pr, pc, a.bw, a.lat)
         bound = sum(1 for i in range(len(rows) - 1) if chain[i + 1] > schur[i])
         out[f"{pr}x{pc}"] = {"t_ms": round(t, 1), "speedup": round(t1 / t, 2),
                              "levels_chain_bound": bound,
-                             "comm_recv_GB_per_rank": round(
-                                 sum(Lp[L] / pr * (pc - 1) / pc + Up[L] / pc * (pr - 1) / pr
-                                     for L in range(len(rows))) / 1e9, 2)}
-    print(json.dumps(out, indent=1))
+                             "recv_GB_per_rank": round(float(vol.sum()) / 1e9, 2)}
+    print(json.dumps(out))
 
 
 if __name__ == "__main__":
