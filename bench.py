@@ -51,6 +51,11 @@ WORKLOADS = {
 }
 
 
+def log(msg):
+    """Progress on stderr (a long GPU job must keep writing, gpurun kills silent ones)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def grid_shape(n):
     return {1: (1, 1), 2: (1, 2), 4: (2, 2), 8: (2, 4), 16: (4, 4)}.get(n, (1, n))
 
@@ -266,8 +271,10 @@ def main():
             dist.barrier()
 
     t0 = time.time()
+    log(f"front-end {args.workload} nx={args.nx} grid {pr}x{pc}")
     A, S, lu = build_lu(args.workload, args.nx, pr, pc, myrow, mycol)
     t_front = time.time() - t0
+    log(f"front-end {t_front:.1f} s, {S.nsupers} supernodes")
     if world == 1:
         comm = None
     elif grid is not None:
@@ -297,8 +304,10 @@ def main():
         barrier()
         return dt, info
 
+    log("plan + upload done; warmup")
     for _ in range(args.warmup):
         one_step()
+    log(f"timed steps: {args.steps}")
     if args.roofline_only:
         args.steps = 0
     times = []
@@ -320,11 +329,13 @@ def main():
     st = plan.stats()
     nxt = None
     if world == 1 and not args.no_next and not args.roofline_only:
+        log("next rows (fill / solve / refine)")
         nxt = next_rows(plan, A, S, anorm, one_step)
     abi = None
     if world == 1 and not args.no_abi and not args.roofline_only:
         t_step_local = float(np.mean(times)) * 1e3
         del plan
+        log("drop-in pdgstrf leg (utime[FACT])")
         abi = abi_leg(lu, anorm, t_step_local)
     if args.roofline_only:
         if rank == 0:
@@ -376,6 +387,7 @@ def main():
                                           3) if acc["t_schur_ms"] else None}
         cpu = None
         if not args.no_cpu and world == 1:
+            log(f"cpu baseline (reference pdgstrf, {args.cpu_sample}^3, {args.cpu_ranks} ranks)")
             cpu = cpu_baseline(args.cpu_sample, args.cpu_ranks, timeout=600)
         out = {
             "metric": W[5],

@@ -22,4 +22,7 @@ timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format cs
 echo "== pmc WRITE_SIZE" && \
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $OUT/pmc_write -o run \
     -- python3 bench.py --no-cpu --roofline-only --warmup 0 "$@" > $OUT/pmc_write.json 2> $OUT/pmc_write.err && \
+echo "== pmc MFMA busy" && \
+timeout -s KILL 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d $OUT/pmc_mfma -o run \
+    -- python3 bench.py --no-cpu --roofline-only --warmup 0 "$@" > $OUT/pmc_mfma.json 2> $OUT/pmc_mfma.err && \
 echo "== done"
