@@ -1458,8 +1458,9 @@ struct Plan : PlanBase {
         O.kinfos.push_back(ki);
         O.khost.push_back(std::move(kh));
         const int slot = (int)O.kinfos.size() - 1; // relocated by the merge
-        const bool big = !cplx && m >= SB_BM && ncols >= SB_BN;
-        const int BM = big ? SB_BM : SC_BM, BN = big ? SB_BN : SC_BN;
+        constexpr int BBN = BigCfg<T>::BN; // 128 (d, s) or 64 (z) columns per big tile
+        const bool big = m >= SB_BM && ncols >= BBN;
+        const int BM = big ? SB_BM : SC_BM, BN = big ? BBN : SC_BN;
         const int tm = (m + BM - 1) / BM, tn = (ncols + BN - 1) / BN;
         // A destination (ib,jb) belongs to the panel of supernode min(ib,jb);
         // it is critical when that panel is factored at the next level.  All
@@ -1888,13 +1889,9 @@ struct Plan : PlanBase {
     }
 
     void launch_big(const LevelRange &R, int off, int cnt, hipStream_t st) {
-        if constexpr (cplx) {
-            SLU_REQUIRE(false, "no 128x128 Schur tiles for complex");
-        } else {
-            hipLaunchKernelGGL(k_schur_big<T>, dim3(cnt), dim3(SB_THREADS), 0, st,
-                               d_tiles_big.p + off, d_kinfo.p + R.k_off, d_L.p, d_U.p,
-                               d_lblk.p, d_lmap.p, d_ublk.p, d_ucol_voff.p, d_ucol_fst.p);
-        }
+        hipLaunchKernelGGL(k_schur_big<T>, dim3(cnt), dim3(SB_THREADS), 0, st,
+                           d_tiles_big.p + off, d_kinfo.p + R.k_off, d_L.p, d_U.p,
+                           d_lblk.p, d_lmap.p, d_ublk.p, d_ucol_voff.p, d_ucol_fst.p);
     }
     void launch_small(const LevelRange &R, int off, int cnt, hipStream_t st) {
         hipLaunchKernelGGL(k_schur<T>, dim3(cnt), dim3(SC_THREADS), 0, st, d_tiles.p + off,

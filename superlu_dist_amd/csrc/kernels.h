@@ -100,6 +100,11 @@ __device__ inline zc one_of(zc) { return {1.0, 0.0}; }
 template <typename T> __device__ __forceinline__ T gld(const T *p) {
     return *(const __attribute__((address_space(1))) T *)p;
 }
+template <> __device__ __forceinline__ zc gld<zc>(const zc *p) {
+    typedef double d2 __attribute__((ext_vector_type(2)));
+    const d2 v = *(const __attribute__((address_space(1))) d2 *)p; // one 16-byte load
+    return {v.x, v.y};
+}
 
 // ------------------------------------------------------------ MFMA
 template <typename T> struct Mma;
@@ -988,7 +993,19 @@ k_trsm_blk(const TrsmItemF<T> *items) {
 // MFMAs.  Epilogue: the C tile goes through LDS in two 64-column passes and
 // is scatter-subtracted column-contiguously into the destination blocks
 // (dscatter_l / dscatter_u, SRC/dscatter.c:175-187,240-272).
-constexpr int SB_BM = 128, SB_BN = 128, SB_BK = 16, SB_THREADS = 512;
+//
+// Complex (pzgstrf): 128x64 tiles, each wave 32x32 = 2x2 fragments of four
+// real MFMAs each (Mma<zc>), K staged 8 deep -- the same accumulator VGPRs,
+// MFMAs per stage and LDS per workgroup as the real tile, at twice the
+// MFMAs per LDS operand; the epilogue stages 16 columns per pass.
+constexpr int SB_BM = 128, SB_THREADS = 512;
+template <typename T> struct BigCfg {
+    static constexpr int BN = 128, BK = 16, FN = 4, PASSW = 64;
+};
+template <> struct BigCfg<zc> {
+    static constexpr int BN = 64, BK = 8, FN = 2, PASSW = 16;
+};
+constexpr int SB_BN = BigCfg<double>::BN;
 
 template <typename T>
 __global__ void __launch_bounds__(SB_THREADS, 2)
@@ -997,13 +1014,16 @@ k_schur_big(const TileItem *tiles, const KInfo<T> *kinfo, T *Lval, T *Uval,
             const int64_t *ucol_voff, const int *ucol_fst) {
     using Sx = S<T>;
     using M = Mma<T>;
+    constexpr int SB_BN = BigCfg<T>::BN, SB_BK = BigCfg<T>::BK;
     constexpr int WN = 2;                   // waves along N
-    constexpr int FM = 2, FN = 4;           // fragments per wave (32 x 64)
+    constexpr int FM = 2, FN = BigCfg<T>::FN; // fragments per wave (32 x 16*FN)
+    constexpr int PASSW = BigCfg<T>::PASSW; // epilogue columns per pass
     constexpr int LDS_A = SB_BM + 4, LDS_B = SB_BN + 4;
     constexpr int STAGE = SB_BK * LDS_A + SB_BK * LDS_B;
-    constexpr int CLD = SB_BM + 1; // C staging: [64 cols][CLD]
-    constexpr int AE = SB_BM * SB_BK / SB_THREADS, BE = SB_BN * SB_BK / SB_THREADS; // 4, 4
-    static_assert(64 * CLD <= 2 * STAGE, "C staging must fit in the stage buffers");
+    constexpr int CLD = SB_BM + 1; // C staging: [PASSW cols][CLD]
+    constexpr int AE = SB_BM * SB_BK / SB_THREADS, BE = SB_BN * SB_BK / SB_THREADS;
+    static_assert(PASSW * CLD <= 2 * STAGE, "C staging must fit in the stage buffers");
+    static_assert(WN * 16 * FN == SB_BN && AE >= 1 && BE >= 1, "tile shape");
     __shared__ T smem[2 * STAGE];
     __shared__ int s_rg[SB_BM], s_ra[SB_BM], s_cg[SB_BN], s_cb[SB_BN];
 
@@ -1095,30 +1115,32 @@ k_schur_big(const TileItem *tiles, const KInfo<T> *kinfo, T *Lval, T *Uval,
         __syncthreads();
     }
 
-    // ---- epilogue: two passes of 64 columns through LDS, column-contiguous.
+    // ---- epilogue: passes of PASSW columns through LDS, column-contiguous.
     // Thread (r, q) owns row r and columns q, q+4, ...; destination addresses
     // are formed for EB columns at a time and their EB read-modify-writes are
     // issued as one batch of independent loads, then the stores (no two
     // elements of a tile share a destination, so nothing aliases).
     T *sC = smem; // [c][r], ld CLD
-    constexpr int TPR = SB_THREADS / SB_BM, CPT = 64 / TPR, EB = 4;
+    constexpr int TPR = SB_THREADS / SB_BM, CPT = PASSW / TPR, EB = CPT < 4 ? CPT : 4;
+    static_assert(CPT % EB == 0, "epilogue batches");
     const int r = tid & (SB_BM - 1), q = tid / SB_BM;
     const int gr = s_rg[r], a = s_ra[r];
     const int *prow = ki.pair + (int64_t)a * ki.nub;
     int lastb = -1, h = 0, ldh = 0;
     int64_t rbase = 0;
-    for (int pass = 0; pass < 2; ++pass) {
-        if (wc == pass) {
+    for (int pass = 0; pass < SB_BN / PASSW; ++pass) {
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn) {
+            const int c0 = wc * 16 * FN + fn * 16; // first tile column of fragment column fn
+            if (c0 / PASSW != pass) continue;
 #pragma unroll
             for (int fm = 0; fm < FM; ++fm)
 #pragma unroll
-                for (int fn = 0; fn < FN; ++fn)
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const int rr = wr * (16 * FM) + fm * 16 + M::row(lane, i);
-                        const int cc = fn * 16 + (lane & 15);
-                        sC[cc * CLD + rr] = M::get(acc[fm][fn], i);
-                    }
+                for (int i = 0; i < 4; ++i) {
+                    const int rr = wr * (16 * FM) + fm * 16 + M::row(lane, i);
+                    const int cc = c0 - pass * PASSW + (lane & 15);
+                    sC[cc * CLD + rr] = M::get(acc[fm][fn], i);
+                }
         }
         __syncthreads();
         if (r < mrows) {
@@ -1128,7 +1150,7 @@ k_schur_big(const TileItem *tiles, const KInfo<T> *kinfo, T *Lval, T *Uval,
                 T v[EB];
 #pragma unroll
                 for (int j = 0; j < EB; ++j) {
-                    const int cl = q + TPR * (j0 + j), c = pass * 64 + cl;
+                    const int cl = q + TPR * (j0 + j), c = pass * PASSW + cl;
                     dp[j] = nullptr;
                     v[j] = Sx::zero();
                     if (c < ncols) {
