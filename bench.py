@@ -359,18 +359,16 @@ def main():
         dtype = W[2]
         peak = FP32_MFMA_PEAK_TFLOPS if dtype == 1 else FP64_MFMA_PEAK_TFLOPS
         if dtype == 2:
-            # complex supernodes use the 64x64 tile kernel only (4 real MFMAs per
-            # complex multiply-add); its launches are the Schur launches
-            kname = "k_schur<zc> (64x64 complex fp64 MFMA GEMM + fused scatter)"
-            ker_ms, ker_flops = sst["t_schur_ms"], sst["schur_flops"]
-            launches = max(int(sst["n_schur_launches"]), 1)
-            tkey = "k_schur<zc>"
+            # complex tiles are 128 rows x 64 columns (4 real MFMAs per complex
+            # multiply-add, kernels.h BigCfg<zc>)
+            kname = "k_schur_big<zc> (128x64 complex fp64 MFMA GEMM + fused scatter)"
+            tkey = "k_schur_big<zc>"
         else:
             tn = "double" if dtype == 0 else "float"
             kname = f"k_schur_big<{tn}> (128x128 {W[7]} MFMA GEMM + fused scatter)"
-            ker_ms, ker_flops = sst["t_schur_big_ms"], sst["schur_big_flops"]
-            launches = max(int(sst["n_schur_big_launches"]), 1)
             tkey = f"k_schur_big<{tn}>"
+        ker_ms, ker_flops = sst["t_schur_big_ms"], sst["schur_big_flops"]
+        launches = max(int(sst["n_schur_big_launches"]), 1)
         achieved = ker_flops / (ker_ms / 1e3) / 1e12 if ker_ms > 0 else 0.0
         roof = {"bound": "mfma", "achieved": round(achieved, 3),
                 "peak": peak, "unit": "TFLOP/s",

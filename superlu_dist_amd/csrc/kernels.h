@@ -1121,7 +1121,10 @@ k_schur_big(const TileItem *tiles, const KInfo<T> *kinfo, T *Lval, T *Uval,
     // issued as one batch of independent loads, then the stores (no two
     // elements of a tile share a destination, so nothing aliases).
     T *sC = smem; // [c][r], ld CLD
-    constexpr int TPR = SB_THREADS / SB_BM, CPT = PASSW / TPR, EB = CPT < 4 ? CPT : 4;
+#ifndef SLU_SB_EB
+#define SLU_SB_EB 4 // epilogue read-modify-writes in flight per thread (A/B builds: -DSLU_SB_EB=8)
+#endif
+    constexpr int TPR = SB_THREADS / SB_BM, CPT = PASSW / TPR, EB = CPT < SLU_SB_EB ? CPT : SLU_SB_EB;
     static_assert(CPT % EB == 0, "epilogue batches");
     const int r = tid & (SB_BM - 1), q = tid / SB_BM;
     const int gr = s_rg[r], a = s_ra[r];
