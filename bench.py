@@ -215,7 +215,7 @@ def main():
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="lap3d",
                     help="lap3d = C3 (headline), lap2d = C2, helm3d = C4 (complex), st27 = C5 (fp32)")
     ap.add_argument("--nx", type=int, default=None, help="grid points per dimension")
-    ap.add_argument("--cpu-sample", type=int, default=80)
+    ap.add_argument("--cpu-sample", type=int, default=100)
     ap.add_argument("--cpu-ranks", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-next", action="store_true",
