@@ -354,6 +354,7 @@ struct Plan : PlanBase {
     DevBuf<TrsmItemF<T>> d_lf, d_uf;
     DevBuf<CopyItem<T>> d_dcopy, d_pcopy;
     DevBuf<int> d_rg, d_ra, d_cg, d_cb, d_pair, d_ct0;
+    DevBuf<DRec> d_prec;
     DevBuf<i64> d_cvoff;
     DevBuf<int> d_counters; // [0] tiny pivots
     DevBuf<int> d_zpiv;     // per supernode: max zero-pivot column + 1
@@ -1497,6 +1498,30 @@ struct Plan : PlanBase {
         d_cg.upload(h_cg);
         d_cb.upload(h_cb);
         d_pair.upload(h_pair);
+        {
+            // destinations resolved once (DRec, kernels.h): the Schur
+            // epilogue reads one record per (L block, U block) of a tile
+            RawVec<DRec> prec;
+            prec.resize_uninit(h_pair.size());
+            parallel_for((int)((h_pair.size() + 4095) / 4096), [&](int ch) {
+                const size_t e = std::min(h_pair.size(), (size_t)(ch + 1) * 4096);
+                for (size_t i = (size_t)ch * 4096; i < e; ++i) {
+                    const int h = h_pair[i];
+                    DRec d{0, 0, -1, 0};
+                    if (h >= 0) {
+                        const LBlk &L = lblk[h];
+                        d.base = L.colvoff - (i64)L.fcol * L.ld;
+                        d.mb = L.mapoff - L.frow;
+                        d.ld = L.ld;
+                    } else {
+                        const UBlk &U = ublk[~h];
+                        d.base = U.coloff - U.fcol;
+                    }
+                    prec[i] = d;
+                }
+            });
+            d_prec.upload(prec);
+        }
         d_ct0.upload(h_ct0);
         d_cvoff.upload(h_cvoff);
         for (auto &t : tu_items) {
@@ -1513,6 +1538,7 @@ struct Plan : PlanBase {
             k.rg = d_rg.p + ro;
             k.ra = d_ra.p + ro;
             k.pair = d_pair.p + po;
+            k.prec = d_prec.p + po;
         }
         for (auto &t : uf_items) {
             intptr_t co = (intptr_t)t.voff;
@@ -1561,7 +1587,7 @@ struct Plan : PlanBase {
                                      d_tl.bytes() + d_tu.bytes() + d_kinfo.bytes() + d_tiles_big.bytes() +
                                      d_df.bytes() + d_lf.bytes() + d_uf.bytes() + d_dinv.bytes() +
                                      d_tiles.bytes() + d_rg.bytes() + d_ra.bytes() +
-                                     d_cg.bytes() + d_cb.bytes() + d_pair.bytes() +
+                                     d_cg.bytes() + d_cb.bytes() + d_pair.bytes() + d_prec.bytes() +
                                      d_ct0.bytes() + d_cvoff.bytes() + d_dcopy.bytes() +
                                      d_pcopy.bytes());
         stats.comm_bytes = (double)comm_volume * sizeof(T);
@@ -1922,6 +1948,12 @@ struct Plan : PlanBase {
         double thresh = sizeof(T) == 4 ? (double)(float)(s_eps * (float)anorm) : (double)s_eps * anorm;
         HIPCHK(hipMemsetAsync(d_counters.p, 0, d_counters.bytes(), stream));
         HIPCHK(hipMemsetAsync(d_zpiv.p, 0, d_zpiv.bytes(), stream));
+#ifdef SLU_SB_STAMP
+        {
+            const unsigned z = 0;
+            HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(slu_stamp_n), &z, sizeof z));
+        }
+#endif
         const bool timing = opts.timing != 0;
         vector<hipEvent_t> ev;
         auto mark = [&]() -> int {
@@ -2128,6 +2160,19 @@ struct Plan : PlanBase {
             }
             for (auto e : ev) (void)hipEventDestroy(e);
         }
+#ifdef SLU_SB_STAMP
+        if (const char *fn = getenv("SLU_STAMP_OUT")) { // diagnostics build: per-tile stamps
+            unsigned cnt = 0;
+            HIPCHK(hipMemcpyFromSymbol(&cnt, HIP_SYMBOL(slu_stamp_n), sizeof cnt));
+            cnt = std::min(cnt, SLU_STAMP_MAX);
+            vector<uint64_t> h((size_t)cnt * 4);
+            if (cnt) HIPCHK(hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(slu_stamp), h.size() * 8));
+            if (FILE *f = fopen(fn, "wb")) {
+                fwrite(h.data(), 8, h.size(), f);
+                fclose(f);
+            }
+        }
+#endif
     }
 
     // ------------------------------------------------------- device solve

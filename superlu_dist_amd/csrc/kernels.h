@@ -185,7 +185,19 @@ template <typename T> struct KInfo {
     const int *cg;       // per U column: global column index
     const int *cb;       // per U column: index of its U block in the panel
     const int *pair;     // nLb x nUb destination handles
+    const struct DRec *prec; // nLb x nUb destinations resolved at plan time
     int lda, m, n, kmin, kw, nub, atomic, pad;
+};
+
+// One (L block ib, U block jb) destination of a panel, resolved by the plan
+// from LBlk / UBlk so the Schur epilogue needs no chained table walk:
+//   L(ib,jb): element (gr, gc) at Lval[base + gc*ld + lmap[mb + gr]]
+//   U(ib,jb): element (gr, gc) at Uval[ucol_voff[e] - ucol_fst[e] + gr], e = base + gc
+struct DRec {
+    int64_t base; // L: colvoff - fcol*ld; U: coloff - fcol
+    int64_t mb;   // L: mapoff - frow
+    int ld;       // L: nsupr of block column jb; U: -1
+    int pad;
 };
 
 struct TileItem {
@@ -1006,9 +1018,28 @@ template <> struct BigCfg<zc> {
     static constexpr int BN = 64, BK = 8, FN = 2, PASSW = 16;
 };
 constexpr int SB_BN = BigCfg<double>::BN;
+constexpr int SB_TB = 4; // epilogue tables: row blocks x column blocks per tile
+#ifndef SLU_SB_AEB
+#define SLU_SB_AEB 4 // atomic scatters formed per batch (A/B builds: -DSLU_SB_AEB=8)
+#endif
 
+#ifdef SLU_SB_STAMP
+// Diagnostics build only (tools/ab_build.sh NAME "-DSLU_SB_STAMP"): per-tile
+// phase timestamps of k_schur_big, read back by the engine after a factor()
+// (SLU_STAMP_OUT) and summarised by tools/stamp_analyze.py.  Four u64 per
+// tile: realtime start (40 b) + duration (24 b, 100 MHz) | prologue, K-loop
+// cycles | epilogue cycles, HW_ID | XCC_ID, tile shape, workgroup id.
+constexpr unsigned SLU_STAMP_MAX = 1u << 21;
+__device__ uint64_t slu_stamp[SLU_STAMP_MAX * 4];
+__device__ unsigned slu_stamp_n;
+#define SB_STAMP(v) if (threadIdx.x == 0) s_stamp_[v] = __builtin_readcyclecounter()
+#else
+#define SB_STAMP(v)
+#endif
+
+// 2 workgroups (16 waves) per CU need <= 128 VGPRs: ask for 4 waves per SIMD
 template <typename T>
-__global__ void __launch_bounds__(SB_THREADS, 2)
+__global__ void __launch_bounds__(SB_THREADS, 4)
 k_schur_big(const TileItem *tiles, const KInfo<T> *kinfo, T *Lval, T *Uval,
             const LBlk *lblk, const int *lmap, const UBlk *ublk,
             const int64_t *ucol_voff, const int *ucol_fst) {
@@ -1026,13 +1057,37 @@ k_schur_big(const TileItem *tiles, const KInfo<T> *kinfo, T *Lval, T *Uval,
     static_assert(WN * 16 * FN == SB_BN && AE >= 1 && BE >= 1, "tile shape");
     __shared__ T smem[2 * STAGE];
     __shared__ int s_rg[SB_BM], s_ra[SB_BM], s_cg[SB_BN], s_cb[SB_BN];
+    __shared__ int64_t s_db[SB_TB * SB_TB], s_dmb[SB_TB * SB_TB]; // destination records
+    __shared__ int s_dld[SB_TB * SB_TB];                          // ld (L) or -1 (U)
+    __shared__ int64_t s_cp[SB_TB * SB_BN];                       // [row block][column] column parts
+    __shared__ int s_rl[SB_TB * SB_BM];                           // [column block][row] lmap positions
 
+#ifdef SLU_SB_STAMP
+    __shared__ uint64_t s_stamp_[5]; // in LDS: the stamps must not add VGPRs (occupancy)
+    enum { c0_, c1_, c2_, c3_, rt_ };
+    if (threadIdx.x == 0) s_stamp_[rt_] = wall_clock64();
+#endif
+    SB_STAMP(c0_);
     const TileItem ti = tiles[blockIdx.x];
     const KInfo<T> ki = kinfo[ti.kslot];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wr = wid / WN, wc = wid % WN;
     const int row0 = ti.tm * SB_BM, col0 = ti.tn * SB_BN;
     const int mrows = min(SB_BM, ki.m - row0), ncols = min(SB_BN, ki.n - col0);
+    // destination tables (epilogue fast path, below): the tile's rows lie in
+    // NA consecutive L blocks of the panel, its columns in NB consecutive U
+    // blocks; their NA x NB destination records come in with the first stage
+    const int a0 = ki.ra[row0], b0 = ki.cb[col0];
+    const int NA = ki.ra[row0 + mrows - 1] - a0 + 1, NB = ki.cb[col0 + ncols - 1] - b0 + 1;
+    const bool tbl = NA <= SB_TB && NB <= SB_TB;
+    if (tbl && tid < SB_TB * SB_TB) {
+        const int al = tid / SB_TB, bl = tid % SB_TB;
+        DRec d{0, 0, -1, 0};
+        if (al < NA && bl < NB) d = ki.prec[(int64_t)(a0 + al) * ki.nub + b0 + bl];
+        s_db[tid] = d.base;
+        s_dmb[tid] = d.mb;
+        s_dld[tid] = d.ld;
+    }
     if (tid < SB_BM) {
         s_rg[tid] = tid < mrows ? ki.rg[row0 + tid] : 0;
         s_ra[tid] = tid < mrows ? ki.ra[row0 + tid] : 0;
@@ -1094,9 +1149,8 @@ k_schur_big(const TileItem *tiles, const KInfo<T> *kinfo, T *Lval, T *Uval,
     gload(0);
     lstore(0, 0);
     __syncthreads();
-    for (int st = 0; st < nst; ++st) {
-        const bool more = st + 1 < nst;
-        if (more) gload((st + 1) * SB_BK);
+    SB_STAMP(c1_);
+    auto mfma_stage = [&](int st) {
         const T *sA = smem + (st & 1) * STAGE, *sB = sA + SB_BK * LDS_A;
 #pragma unroll
         for (int ks = 0; ks < SB_BK; ks += M::KSTEP) {
@@ -1111,27 +1165,60 @@ k_schur_big(const TileItem *tiles, const KInfo<T> *kinfo, T *Lval, T *Uval,
 #pragma unroll
                 for (int fn = 0; fn < FN; ++fn) M::step(acc[fm][fn], av[fm], bv[fn]);
         }
-        if (more) lstore((st + 1) & 1, (st + 1) * SB_BK);
+    };
+    for (int st = 0; st + 1 < nst; ++st) {
+        gload((st + 1) * SB_BK);
+        mfma_stage(st);
+        lstore((st + 1) & 1, (st + 1) * SB_BK);
         __syncthreads();
+    }
+    // last stage (peeled: no prefetch, so its registers carry the second
+    // half of the destination tables instead): per (row block, column) the
+    // column part of the address, tagged with the column block (1 + bl) or
+    // 0 for a U destination; per (column block, row) the lmap position.
+    constexpr int CPN = SB_TB * SB_BN, RLN = SB_TB * SB_BM;
+    static_assert(CPN <= SB_THREADS && RLN <= SB_THREADS, "one table entry per thread");
+    int64_t t_code = 0, t_uv = 0;
+    int t_fst = 0, t_rl = 0;
+    if (tbl) {
+        if (tid < CPN) {
+            const int al = tid / SB_BN, c = tid % SB_BN;
+            if (al < NA && c < ncols) {
+                const int bl = s_cb[c] - b0, rec = al * SB_TB + bl, ld = s_dld[rec];
+                const int64_t x = s_db[rec] + s_cg[c];
+                if (ld >= 0) {
+                    t_code = (s_db[rec] + (int64_t)s_cg[c] * ld) * 8 + 1 + bl;
+                } else {
+                    t_uv = ucol_voff[x];
+                    t_fst = ucol_fst[x];
+                }
+            }
+        }
+        {
+            const int bl = tid / SB_BM, rr = tid % SB_BM;
+            if (bl < NB && rr < mrows) {
+                const int rec = (s_ra[rr] - a0) * SB_TB + bl;
+                if (s_dld[rec] >= 0) t_rl = lmap[s_dmb[rec] + s_rg[rr]];
+            }
+        }
+    }
+    mfma_stage(nst - 1);
+    __syncthreads();
+    if (tbl) {
+        if (tid < CPN) s_cp[tid] = t_code ? t_code : (t_uv - t_fst) * 8;
+        s_rl[tid] = t_rl;
     }
 
     // ---- epilogue: passes of PASSW columns through LDS, column-contiguous.
-    // Thread (r, q) owns row r and columns q, q+4, ...; destination addresses
-    // are formed for EB columns at a time and their EB read-modify-writes are
-    // issued as one batch of independent loads, then the stores (no two
-    // elements of a tile share a destination, so nothing aliases).
+    // Thread (r, q) owns row r and columns q, q+4, ...  (a wave = 64 rows of
+    // one column, so column data is wave-uniform).
+    SB_STAMP(c2_);
     T *sC = smem; // [c][r], ld CLD
-#ifndef SLU_SB_EB
-#define SLU_SB_EB 4 // epilogue read-modify-writes in flight per thread (A/B builds: -DSLU_SB_EB=8)
-#endif
-    constexpr int TPR = SB_THREADS / SB_BM, CPT = PASSW / TPR, EB = CPT < SLU_SB_EB ? CPT : SLU_SB_EB;
-    static_assert(CPT % EB == 0, "epilogue batches");
+    constexpr int TPR = SB_THREADS / SB_BM, CPT = PASSW / TPR;
     const int r = tid & (SB_BM - 1), q = tid / SB_BM;
     const int gr = s_rg[r], a = s_ra[r];
-    const int *prow = ki.pair + (int64_t)a * ki.nub;
-    int lastb = -1, h = 0, ldh = 0;
-    int64_t rbase = 0;
-    for (int pass = 0; pass < SB_BN / PASSW; ++pass) {
+    // C tile columns [pass*PASSW, (pass+1)*PASSW) from the accumulators into LDS
+    auto stage_c = [&](int pass) {
 #pragma unroll
         for (int fn = 0; fn < FN; ++fn) {
             const int c0 = wc * 16 * FN + fn * 16; // first tile column of fragment column fn
@@ -1145,55 +1232,161 @@ k_schur_big(const TileItem *tiles, const KInfo<T> *kinfo, T *Lval, T *Uval,
                     sC[cc * CLD + rr] = M::get(acc[fm][fn], i);
                 }
         }
-        __syncthreads();
-        if (r < mrows) {
+    };
+    // Fast path (tbl): a tile's rows lie in NA consecutive L blocks of the
+    // panel and its columns in NB consecutive U blocks; with NA, NB <= TB
+    // (99.6 % of the 100^3 flops) every destination address splits into a
+    // column part and a row part,
+    //   L(ib,jb): Lval + [colvoff + (gc - fcol)*ld] + [lmap position of gr]
+    //   U(ib,jb): Uval + [ucol_voff - ucol_fst](ib, gc) + [gr]
+    // resolved once per tile above: the column parts per (row block, column)
+    // in LDS (tagged with the column block, 0 = U destination), the lmap
+    // positions per column block in the row's registers.  The scatter then
+    // reads one LDS word per element besides the destination itself
+    // (dscatter_l / dscatter_u, SRC/dscatter.c:137-142,229-235 search per
+    // element).  The stores are fire-and-forget atomic adds: no load round
+    // trip per element; where a tile is the only writer of its destinations
+    // the sums are the plain subtraction's, bit for bit.
+    if (tbl) {
+        int rl[SB_TB];
+        const int al = a - a0;
+        for (int pass = 0; pass < SB_BN / PASSW; ++pass) {
+            stage_c(pass);
+            __syncthreads();
+            if (pass == 0) {
 #pragma unroll
-            for (int j0 = 0; j0 < CPT; j0 += EB) {
-                T *dp[EB];
-                T v[EB];
+                for (int bl = 0; bl < SB_TB; ++bl) rl[bl] = s_rl[bl * SB_BM + r];
+            }
+            if (r < mrows) {
+#ifdef SLU_SB_RMW
+                constexpr int EB = CPT < 4 ? CPT : 4;
+#else
+                constexpr int EB = CPT < SLU_SB_AEB ? CPT : SLU_SB_AEB;
+#endif
 #pragma unroll
-                for (int j = 0; j < EB; ++j) {
-                    const int cl = q + TPR * (j0 + j), c = pass * PASSW + cl;
-                    dp[j] = nullptr;
-                    v[j] = Sx::zero();
-                    if (c < ncols) {
-                        v[j] = sC[cl * CLD + r];
-                        const int b = s_cb[c], gc = s_cg[c];
-                        if (b != lastb) {
-                            lastb = b;
-                            h = prow[b];
-                            if (h >= 0) {
-                                const LBlk L = lblk[h];
-                                ldh = L.ld;
-                                rbase = L.colvoff + lmap[L.mapoff + gr - L.frow] -
-                                        (int64_t)L.fcol * L.ld;
-                            }
-                        }
-                        if (h >= 0) {
-                            dp[j] = Lval + rbase + (int64_t)gc * ldh;
-                        } else {
-                            const UBlk U = ublk[~h];
-                            const int64_t e = U.coloff + gc - U.fcol;
-                            dp[j] = Uval + ucol_voff[e] + gr - ucol_fst[e];
+                for (int j0 = 0; j0 < CPT; j0 += EB) {
+                    T *dp[EB];
+                    T v[EB];
+#pragma unroll
+                    for (int j = 0; j < EB; ++j) {
+                        const int cl = q + TPR * (j0 + j), c = pass * PASSW + cl;
+                        dp[j] = nullptr;
+                        v[j] = Sx::zero();
+                        if (c < ncols) {
+                            v[j] = sC[cl * CLD + r];
+                            const int64_t code = s_cp[al * SB_BN + c];
+                            const int tag = (int)(code & 7);
+                            int rp = gr; // branch-free: U row part, or the column block's lmap position
+                            rp = tag == 1 ? rl[0] : rp;
+                            rp = tag == 2 ? rl[1] : rp;
+                            rp = tag == 3 ? rl[2] : rp;
+                            rp = tag == 4 ? rl[3] : rp;
+                            T *const base = tag ? Lval : Uval;
+                            dp[j] = base + ((code >> 3) + rp);
                         }
                     }
-                }
-                if (ki.atomic) {
+#ifdef SLU_SB_RMW
+                    if (ki.atomic) {
+#pragma unroll
+                        for (int j = 0; j < EB; ++j)
+                            if (dp[j]) Sx::atomic_sub(dp[j], v[j]);
+                    } else {
+                        T o[EB];
+#pragma unroll
+                        for (int j = 0; j < EB; ++j) o[j] = dp[j] ? *dp[j] : Sx::zero();
+#pragma unroll
+                        for (int j = 0; j < EB; ++j)
+                            if (dp[j]) *dp[j] = Sx::sub(o[j], v[j]);
+                    }
+#else
 #pragma unroll
                     for (int j = 0; j < EB; ++j)
                         if (dp[j]) Sx::atomic_sub(dp[j], v[j]);
-                } else {
-                    T o[EB];
-#pragma unroll
-                    for (int j = 0; j < EB; ++j) o[j] = dp[j] ? *dp[j] : Sx::zero();
-#pragma unroll
-                    for (int j = 0; j < EB; ++j)
-                        if (dp[j]) *dp[j] = Sx::sub(o[j], v[j]);
+#endif
                 }
             }
+            __syncthreads();
         }
-        __syncthreads();
+    } else {
+        // slow path (tiles over more blocks): per-element table walk, EB
+        // read-modify-writes in flight per thread
+#ifndef SLU_SB_EB
+#define SLU_SB_EB 4 // slow path read-modify-writes in flight per thread (A/B builds: -DSLU_SB_EB=8)
+#endif
+        constexpr int EB = CPT < SLU_SB_EB ? CPT : SLU_SB_EB;
+        static_assert(CPT % EB == 0, "epilogue batches");
+        const int *prow = ki.pair + (int64_t)a * ki.nub;
+        int lastb = -1, h = 0, ldh = 0;
+        int64_t rbase = 0;
+        for (int pass = 0; pass < SB_BN / PASSW; ++pass) {
+            stage_c(pass);
+            __syncthreads();
+            if (r < mrows) {
+#pragma unroll
+                for (int j0 = 0; j0 < CPT; j0 += EB) {
+                    T *dp[EB];
+                    T v[EB];
+#pragma unroll
+                    for (int j = 0; j < EB; ++j) {
+                        const int cl = q + TPR * (j0 + j), c = pass * PASSW + cl;
+                        dp[j] = nullptr;
+                        v[j] = Sx::zero();
+                        if (c < ncols) {
+                            v[j] = sC[cl * CLD + r];
+                            const int b = s_cb[c], gc = s_cg[c];
+                            if (b != lastb) {
+                                lastb = b;
+                                h = prow[b];
+                                if (h >= 0) {
+                                    const LBlk L = lblk[h];
+                                    ldh = L.ld;
+                                    rbase = L.colvoff + lmap[L.mapoff + gr - L.frow] -
+                                            (int64_t)L.fcol * L.ld;
+                                }
+                            }
+                            if (h >= 0) {
+                                dp[j] = Lval + rbase + (int64_t)gc * ldh;
+                            } else {
+                                const UBlk U = ublk[~h];
+                                const int64_t e = U.coloff + gc - U.fcol;
+                                dp[j] = Uval + ucol_voff[e] + gr - ucol_fst[e];
+                            }
+                        }
+                    }
+                    if (ki.atomic) {
+#pragma unroll
+                        for (int j = 0; j < EB; ++j)
+                            if (dp[j]) Sx::atomic_sub(dp[j], v[j]);
+                    } else {
+                        T o[EB];
+#pragma unroll
+                        for (int j = 0; j < EB; ++j) o[j] = dp[j] ? *dp[j] : Sx::zero();
+#pragma unroll
+                        for (int j = 0; j < EB; ++j)
+                            if (dp[j]) *dp[j] = Sx::sub(o[j], v[j]);
+                    }
+                }
+            }
+            __syncthreads();
+        }
     }
+#ifdef SLU_SB_STAMP
+    SB_STAMP(c3_);
+    if (tid == 0) {
+        const unsigned s = atomicAdd(&slu_stamp_n, 1u);
+        if (s < SLU_STAMP_MAX) {
+            const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
+            const unsigned xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20); // XCC_ID
+            uint64_t *o = slu_stamp + (size_t)s * 4;
+            const uint64_t *t = s_stamp_;
+            o[0] = (t[rt_] & ((1ull << 40) - 1)) | (((wall_clock64() - t[rt_]) & 0xFFFFFFull) << 40);
+            o[1] = (uint64_t)(t[c1_] - t[c0_]) | ((uint64_t)(t[c2_] - t[c1_]) << 32);
+            o[2] = (uint64_t)(t[c3_] - t[c2_]) | ((uint64_t)hw << 32);
+            o[3] = (uint64_t)(xcc & 15) | ((uint64_t)ki.kw << 4) | ((uint64_t)mrows << 14) |
+                   ((uint64_t)ncols << 22) | ((uint64_t)ki.atomic << 30) | ((uint64_t)blockIdx.x << 32);
+        }
+    }
+#endif
 }
 
 

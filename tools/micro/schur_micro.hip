@@ -118,6 +118,8 @@ int main(int argc, char **argv) {
     ki.pair = (const int *)up(pair.data(), 4);
     LBlk L{};
     L.colvoff = 0; L.mapoff = 0; L.ld = m; L.fcol = 0; L.frow = 0;
+    DRec rec{0, 0, m, 0}; // the one destination: L block (0,0), identity row map, ld = m
+    ki.prec = (const DRec *)up(&rec, sizeof rec);
     auto *dk = (KInfo<double> *)up(&ki, sizeof ki);
     auto *dl = (LBlk *)up(&L, sizeof L);
     auto *dmap = (int *)up(lmap.data(), m * 4);
