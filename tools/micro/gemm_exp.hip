@@ -16,8 +16,8 @@ template <typename T> __device__ __forceinline__ T gld(const T *p) {
 }
 
 // WM x WN waves, each wave FM x FN fragments of 16x16.
-template <int BM, int BN, int BK, int WM, int WN, bool PRIO, bool B2>
-__global__ void __launch_bounds__(64 * WM * WN)
+template <int BM, int BN, int BK, int WM, int WN, bool PRIO, bool B2, int MINW = 1>
+__global__ void __launch_bounds__(64 * WM * WN, MINW)
 k_gemm(const double *A, const double *B, double *C, int m, int n, int kw) {
     constexpr int NT = 64 * WM * WN, FM = BM / WM / 16, FN = BN / WN / 16;
     constexpr int LA = BM + 4, LB = BN + 4, STAGE = BK * (LA + LB);
@@ -103,7 +103,7 @@ k_gemm(const double *A, const double *B, double *C, int m, int n, int kw) {
             }
 }
 
-template <int BM, int BN, int BK, int WM, int WN, bool PRIO, bool B2>
+template <int BM, int BN, int BK, int WM, int WN, bool PRIO, bool B2, int MINW = 1>
 void run(const char *name, const double *A, const double *B, double *C, int m, int n, int kw) {
     int nb = (m / BM) * (n / BN);
     hipEvent_t e0, e1;
@@ -112,7 +112,7 @@ void run(const char *name, const double *A, const double *B, double *C, int m, i
     float best = 1e30f;
     for (int r = 0; r < 4; ++r) {
         hipEventRecord(e0);
-        hipLaunchKernelGGL((k_gemm<BM, BN, BK, WM, WN, PRIO, B2>), dim3(nb), dim3(64 * WM * WN), 0, 0, A, B, C, m, n, kw);
+        hipLaunchKernelGGL((k_gemm<BM, BN, BK, WM, WN, PRIO, B2, MINW>), dim3(nb), dim3(64 * WM * WN), 0, 0, A, B, C, m, n, kw);
         hipEventRecord(e1);
         hipEventSynchronize(e1);
         float ms;
@@ -136,6 +136,9 @@ int main(int argc, char **argv) {
     CK(hipMemcpy(B, h.data(), (size_t)std::min(m, n) * kw * 8, hipMemcpyHostToDevice));
     CK(hipMemset(C, 0, (size_t)m * n * 8));
     run<128, 128, 16, 2, 2, false, true>("128x128x16 2x2w (64x64/wave)", A, B, C, m, n, kw);
+    run<128, 128, 16, 2, 2, false, true, 2>("128x128x16 2x2w 64x64/wave, 2 waves/SIMD", A, B, C, m, n, kw);
+    run<128, 128, 16, 4, 2, false, true, 4>("128x128x16 4x2w 4 waves/SIMD bound", A, B, C, m, n, kw);
+    run<256, 128, 16, 4, 2, false, true, 2>("256x128x16 4x2w 64x64/wave, 2 waves/SIMD", A, B, C, m, n, kw);
     run<128, 128, 16, 2, 2, true, true>("128x128x16 2x2w prio", A, B, C, m, n, kw);
     run<128, 128, 32, 2, 2, false, true>("128x128x32 2x2w", A, B, C, m, n, kw);
     run<256, 128, 16, 4, 2, false, true>("256x128x16 4x2w (64x64/wave)", A, B, C, m, n, kw);
