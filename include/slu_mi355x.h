@@ -162,10 +162,14 @@ int slu_plan_sync(slu_plan *p);
 /* Copy factors back into the host LUstruct arrays. */
 int slu_plan_download(slu_plan *p);
 /* Solve L U x = b with the device-resident factors of the last
- * slu_plan_factor (1x1 grid; SURVEY 8(f) row 2, the supernodal solve of
- * SRC/pdgstrs.c in the LUstruct's permuted coordinates).  b: host array of
- * nrhs columns of n values (ld ldb, element type of the plan), overwritten
- * with x.  t_solve_ms in the stats is the device time of the last call. */
+ * slu_plan_factor (the supernodal solve of SRC/pdgstrs.c
+ * in the LUstruct's permuted coordinates).  b: host array of nrhs columns of
+ * n values (ld ldb, element type of the plan), overwritten with x.  On a 2D
+ * grid the call is collective: every rank passes the same b and gets the
+ * whole x; partial sums of a block row are reduced along its process row to
+ * the diagonal owner and solved pieces travel down the owner's process
+ * column (pdgstrs_lsum.c's scheme, level by level).  t_solve_ms in the stats
+ * is the device time of the last call. */
 int slu_plan_solve(slu_plan *p, void *b, int64_t ldb, int nrhs);
 /* Device-side refill of the factor storage from new values of A with the
  * same pattern (replaces the options->Fact ==

@@ -154,13 +154,21 @@ struct Xport {
                 hbuf.resize(o.bytes);
                 const int me = grank(o.g);
                 const bool root = me == o.root;
-                if (root) HIPCHK(hipMemcpy(hbuf.data(), o.buf, o.bytes, hipMemcpyDeviceToHost));
+                // copies on the transport's stream and waited for: a pageable
+                // hipMemcpy returns once the host buffer is staged, before the
+                // DMA has landed, and kernels on a non-blocking stream could
+                // read the destination first
+                if (root) {
+                    HIPCHK(hipMemcpyAsync(hbuf.data(), o.buf, o.bytes, hipMemcpyDeviceToHost, s));
+                    HIPCHK(hipStreamSynchronize(s));
+                }
                 SLU_REQUIRE(c->host_fn(c->host_ctx, o.g, o.root, hbuf.data(), (int64_t)o.bytes) == 0,
                             "host broadcast (group %d, root %d, %zu bytes) failed", o.g, o.root,
                             o.bytes);
                 if (!root && (o.mask >> me & 1)) {
                     SLU_REQUIRE(o.buf, "section of group %d root %d has no buffer", o.g, o.root);
-                    HIPCHK(hipMemcpy(o.buf, hbuf.data(), o.bytes, hipMemcpyHostToDevice));
+                    HIPCHK(hipMemcpyAsync(o.buf, hbuf.data(), o.bytes, hipMemcpyHostToDevice, s));
+                    HIPCHK(hipStreamSynchronize(s));
                 }
             }
         } else {
@@ -1592,6 +1600,9 @@ struct Plan : PlanBase {
                                      d_pcopy.bytes());
         stats.comm_bytes = (double)comm_volume * sizeof(T);
         stats.comm_buf_bytes = (double)(dpk_total + pan_total) * sizeof(T);
+        // the tables went up by pageable hipMemcpy on the null stream; the
+        // plan's streams are non-blocking, so make sure every copy has landed
+        HIPCHK(hipDeviceSynchronize());
     }
 
     // ------------------------------------------------------- values
@@ -2180,13 +2191,14 @@ struct Plan : PlanBase {
     bool sv_ready = false;
     vector<int> sv_d_off, sv_l_off, sv_u_off; // per level: diag items, L chunks, U chunks
     DevBuf<SvDiag> d_sv_diag, d_sv_lvl;       // per supernode / in level order
+    DevBuf<SvDiag> d_sv_pan;                  // per supernode: this rank's L rows below the diagonal block
     DevBuf<SvChunk> d_sv_lch, d_sv_uch;
     DevBuf<i64> d_sv_roff, d_sv_coff;
     DevBuf<int> d_sv_rows, d_sv_ncol, d_sv_gc;
     DevBuf<T> d_sv_x;
 
     void build_solve() {
-        SLU_REQUIRE(!xmode, "the device solve is implemented for 1x1 grids");
+        if (xmode) return build_solve_2d();
         vector<SvDiag> dg(nsupers), lvl;
         vector<i64> roff(nsupers), coff(nsupers, 0);
         vector<int> rows, ncol(nsupers, 0), gc;
@@ -2235,6 +2247,14 @@ struct Plan : PlanBase {
         sv_l_off[nl] = (int)lch.size();
         sv_u_off[nl] = (int)uch.size();
         d_sv_diag.upload(dg);
+        {
+            vector<SvDiag> pan(dg);
+            for (auto &d : pan) {
+                d.pad = d.ld - d.w;
+                d.voff += d.w;
+            }
+            d_sv_pan.upload(pan);
+        }
         d_sv_lvl.upload(lvl);
         d_sv_lch.upload(lch);
         d_sv_uch.upload(uch);
@@ -2244,6 +2264,7 @@ struct Plan : PlanBase {
         d_sv_ncol.upload(ncol);
         d_sv_gc.upload(gc.empty() ? vector<int>(1, 0) : gc);
         d_sv_x.alloc(std::max(n, 1));
+        HIPCHK(hipDeviceSynchronize()); // pageable table uploads landed (non-blocking streams)
         sv_ready = true;
     }
 
@@ -2257,7 +2278,7 @@ struct Plan : PlanBase {
                                    d_sv_lvl.p + sv_d_off[L], d_L.p, xv, ldx, nr);
             if (nc)
                 hipLaunchKernelGGL((k_sv_lpanel<T, NR>), dim3(nc), dim3(SV_THREADS), 0, stream,
-                                   d_sv_lch.p + sv_l_off[L], d_sv_diag.p, d_sv_roff.p,
+                                   d_sv_lch.p + sv_l_off[L], d_sv_pan.p, d_sv_roff.p,
                                    d_sv_rows.p, d_L.p, xv, ldx, nr);
         }
         for (int L = nl - 1; L >= 0; --L) { // U x = y
@@ -2278,11 +2299,224 @@ struct Plan : PlanBase {
         else sweep_nr<SvNr<T>::v>(xv, ldx, nr);
     }
 
+    // ---- 2D grids: the distributed supernodal solve of pdgstrs
+    // (SRC/pdgstrs.c, pdgstrs_lsum.c), level-scheduled.  Block row k's partial
+    // sums (lsum) live on its process row; per level they are sent to the
+    // diagonal owner (k mod Pr, k mod Pc) along the row and added there; the
+    // owner solves with the diagonal block; the solved piece goes down the
+    // owner's process column to the ranks whose L(:,k) (forward) or U(:,k)
+    // (backward) blocks use it, which push -L(i,k) y_k into their partial
+    // sums of rows i (forward) or pull -U(i,k) x_k into rows i (backward).
+    // b comes in and x goes out replicated on every rank (n values); each
+    // rank starts from b on the block rows it owns and zero elsewhere.
+    struct SvRed {                       // one partial-sum section of a level
+        int k, c;                        // block row, sending process column
+        i64 slot;                        // owner: offset of its slot in d_sv_slot
+    };
+    vector<vector<SvRed>> sv_red;        // per level, this rank's process row's sections
+    vector<int> sv_add_off;              // per level: owner's slot-add items
+    DevBuf<SvAdd> d_sv_add, d_sv_zero;
+    DevBuf<T> d_sv_slot;
+    vector<int> sv_own;                  // per supernode: this rank is the diagonal owner
+
+    void build_solve_2d() {
+        const int nl = (int)bylev.size();
+        vector<SvDiag> dg(nsupers), pan(nsupers), lvl;
+        vector<i64> roff(nsupers, 0), coff(nsupers, 0);
+        vector<int> rows, ncol(nsupers, 0), gc;
+        sv_own.assign(nsupers, 0);
+        vector<SvAdd> zero;
+        for (int k = 0; k < nsupers; ++k) {
+            SvDiag d{};
+            d.w = W(k);
+            d.fst = (int)xsup[k];
+            d.ld = 0;
+            d.voff = 0;
+            const bool lcol = k % Pc == mycol, own = lcol && k % Pr == myrow;
+            sv_own[k] = own;
+            if (!own) zero.push_back({(i64)xsup[k], -1, W(k), 0});
+            SvDiag pd = d;
+            pd.pad = 0;
+            roff[k] = (i64)rows.size();
+            if (lcol && lidx[k]) {
+                const int ljb = k / Pc;
+                SLU_REQUIRE(lval_off[ljb] >= 0, "supernode %d: no L column block", k);
+                d.voff = lval_off[ljb];
+                d.ld = lval_ld[ljb];
+                int m = 0, r0 = 0;
+                lrows(k, m, r0);
+                SLU_REQUIRE(r0 == (own ? W(k) : 0), "supernode %d: diagonal block rows %d", k, r0);
+                pd.voff = lval_off[ljb] + r0;
+                pd.ld = lval_ld[ljb];
+                pd.pad = m;
+                const int_t *ix = lidx[k];
+                i64 p = SLU_BC_HEADER;
+                for (i64 b = 0; b < ix[0]; ++b) {
+                    const int gb = (int)ix[p], nr = (int)ix[p + 1];
+                    if (gb != k)
+                        for (int i = 0; i < nr; ++i) rows.push_back((int)ix[p + 2 + i]);
+                    p += SLU_LB_DESCRIPTOR + nr;
+                }
+            }
+            dg[k] = d;
+            pan[k] = pd;
+            if (k % Pr == myrow) {
+                const int lb = k / Pr;
+                if (uval_off[lb] >= 0 && urow_nblk[lb] > 0) {
+                    coff[k] = ublk[urow_first[lb]].coloff;
+                    for (int b = urow_first[lb]; b < urow_first[lb] + urow_nblk[lb]; ++b)
+                        ncol[k] += W(ublk_jb[b]);
+                }
+            }
+        }
+        gc.resize(ucol_voff.size());
+        for (size_t b = 0; b < ublk.size(); ++b)
+            for (int c = 0; c < W(ublk_jb[b]); ++c) gc[ublk[b].coloff + c] = ublk[b].fcol + c;
+        vector<SvChunk> lch, uch;
+        vector<SvAdd> adds;
+        sv_d_off.assign(nl + 1, 0);
+        sv_l_off.assign(nl + 1, 0);
+        sv_u_off.assign(nl + 1, 0);
+        sv_add_off.assign(nl + 1, 0);
+        sv_red.assign(nl, {});
+        i64 slot_max = 0;
+        for (int L = 0; L < nl; ++L) {
+            sv_d_off[L] = (int)lvl.size();
+            sv_l_off[L] = (int)lch.size();
+            sv_u_off[L] = (int)uch.size();
+            sv_add_off[L] = (int)adds.size();
+            i64 slot = 0;
+            for (int k : bylev[L]) {
+                if (sv_own[k]) lvl.push_back(dg[k]);
+                for (int r0 = 0; r0 < pan[k].pad; r0 += SV_THREADS) lch.push_back({k, r0});
+                for (int c0 = 0; c0 < ncol[k]; c0 += SVU_COLS) uch.push_back({k, c0});
+                if (k % Pr != myrow) continue;
+                if (sv_own[k] && Pc > 1) adds.push_back({(i64)xsup[k], slot, W(k), Pc - 1});
+                for (int c = 0; c < Pc; ++c) {
+                    if (c == k % Pc) continue;
+                    SvRed r{k, c, -1};
+                    if (sv_own[k]) {
+                        r.slot = slot; // the Pc - 1 slots of k are consecutive
+                        slot += W(k);
+                    }
+                    sv_red[L].push_back(r);
+                }
+            }
+            slot_max = std::max(slot_max, slot);
+        }
+        sv_d_off[nl] = (int)lvl.size();
+        sv_l_off[nl] = (int)lch.size();
+        sv_u_off[nl] = (int)uch.size();
+        sv_add_off[nl] = (int)adds.size();
+        d_sv_diag.upload(dg);
+        d_sv_pan.upload(pan);
+        d_sv_lvl.upload(lvl.empty() ? vector<SvDiag>(1) : lvl);
+        d_sv_lch.upload(lch.empty() ? vector<SvChunk>(1) : lch);
+        d_sv_uch.upload(uch.empty() ? vector<SvChunk>(1) : uch);
+        d_sv_roff.upload(roff);
+        d_sv_coff.upload(coff);
+        d_sv_rows.upload(rows.empty() ? vector<int>(1, 0) : rows);
+        d_sv_ncol.upload(ncol);
+        d_sv_gc.upload(gc.empty() ? vector<int>(1, 0) : gc);
+        d_sv_add.upload(adds.empty() ? vector<SvAdd>(1) : adds);
+        d_sv_zero.upload(zero.empty() ? vector<SvAdd>(1) : zero);
+        d_sv_slot.alloc(std::max<i64>(slot_max, 1));
+        d_sv_x.alloc(std::max(n, 1));
+        HIPCHK(hipDeviceSynchronize()); // pageable table uploads landed (non-blocking streams)
+        sv_ready = true;
+    }
+
+    // partial sums of the level's block rows to their owners, added there
+    void sv_reduce(int L, T *xv) {
+        for (const SvRed &r : sv_red[L]) {
+            const int own_c = r.k % Pc;
+            T *buf = mycol == r.c ? xv + xsup[r.k] : (mycol == own_c ? d_sv_slot.p + r.slot : nullptr);
+            X.section(G_ROW, r.c, 1u << own_c, buf, (size_t)W(r.k) * sizeof(T));
+        }
+        X.flush();
+        const int na = sv_add_off[L + 1] - sv_add_off[L];
+        if (na)
+            hipLaunchKernelGGL(k_sv_add<T>, dim3(na), dim3(256), 0, stream, d_sv_add.p + sv_add_off[L],
+                               xv, (const T *)d_sv_slot.p);
+    }
+    // the solved pieces of the level down their owners' process columns
+    void sv_bcast(int L, T *xv, bool fwd) {
+        const uint32_t all = Pr >= 32 ? ~0u : (1u << Pr) - 1;
+        for (int k : bylev[L]) {
+            if (k % Pc != mycol) continue;
+            X.section(G_COL, k % Pr, fwd ? cmask(k) : all, xv + xsup[k], (size_t)W(k) * sizeof(T));
+        }
+        X.flush();
+    }
+
+    void sweep_2d(T *xv) {
+        const int nl = (int)bylev.size();
+        X.s = stream;
+        const unsigned nz = (unsigned)(nsupers - std::accumulate(sv_own.begin(), sv_own.end(), 0));
+        if (nz) hipLaunchKernelGGL(k_sv_add<T>, dim3(nz), dim3(256), 0, stream, d_sv_zero.p, xv, (const T *)nullptr);
+        for (int L = 0; L < nl; ++L) { // L y = b
+            sv_reduce(L, xv);
+            const int nd = sv_d_off[L + 1] - sv_d_off[L], nc = sv_l_off[L + 1] - sv_l_off[L];
+            if (nd)
+                hipLaunchKernelGGL((k_sv_ldiag<T, 1>), dim3(nd), dim3(SVD_THREADS), 0, stream,
+                                   d_sv_lvl.p + sv_d_off[L], d_L.p, xv, (i64)n, 1);
+            sv_bcast(L, xv, true);
+            if (nc)
+                hipLaunchKernelGGL((k_sv_lpanel<T, 1>), dim3(nc), dim3(SV_THREADS), 0, stream,
+                                   d_sv_lch.p + sv_l_off[L], d_sv_pan.p, d_sv_roff.p,
+                                   d_sv_rows.p, d_L.p, xv, (i64)n, 1);
+        }
+        const bool fwd_only = getenv("SLU_SV_FWD_ONLY") != nullptr; // diagnostics: y = L^-1 b
+        if (nz && !fwd_only) hipLaunchKernelGGL(k_sv_add<T>, dim3(nz), dim3(256), 0, stream, d_sv_zero.p, xv, (const T *)nullptr);
+        for (int L = fwd_only ? -1 : nl - 1; L >= 0; --L) { // U x = y
+            const int nd = sv_d_off[L + 1] - sv_d_off[L], nc = sv_u_off[L + 1] - sv_u_off[L];
+            if (nc)
+                hipLaunchKernelGGL((k_sv_upanel<T, 1>), dim3(nc), dim3(SV_THREADS), 0, stream,
+                                   d_sv_uch.p + sv_u_off[L], d_sv_diag.p, d_sv_coff.p,
+                                   d_sv_ncol.p, d_ucol_voff.p, d_ucol_fst.p, d_sv_gc.p,
+                                   d_U.p, xv, (i64)n, 1);
+            sv_reduce(L, xv);
+            if (nd)
+                hipLaunchKernelGGL((k_sv_udiag<T, 1>), dim3(nd), dim3(SVD_THREADS), 0, stream,
+                                   d_sv_lvl.p + sv_d_off[L], d_L.p, xv, (i64)n, 1);
+            sv_bcast(L, xv, false);
+        }
+        // x replicated on every rank: each owner's pieces to the world
+        for (int k = 0; k < nsupers; ++k)
+            X.section(G_WORLD, (k % Pr) * Pc + k % Pc, ~0u, xv + xsup[k], (size_t)W(k) * sizeof(T));
+        X.flush();
+        HIPCHK(hipGetLastError());
+    }
+
     // right-hand sides in batches of SvNr<T>: every factor element is read once
     // per batch and sweep
     void solve(void *b, int64_t ldb, int nrhs) override {
         SLU_REQUIRE(vstate == 2, "solve: the device storage holds no factors (factor first)");
         if (!sv_ready) build_solve();
+        if (xmode) {
+            SLU_REQUIRE(ldb >= n && nrhs >= 0, "solve: ldb %lld < n %d", (long long)ldb, n);
+            HIPCHK(hipStreamSynchronize(pstream));
+            hipEvent_t e0, e1;
+            HIPCHK(hipEventCreate(&e0));
+            HIPCHK(hipEventCreate(&e1));
+            float total = 0;
+            for (int j = 0; j < nrhs; ++j) {
+                HT *bj = (HT *)b + (i64)j * ldb;
+                HIPCHK(hipMemcpyAsync(d_sv_x.p, bj, (size_t)n * sizeof(T), hipMemcpyHostToDevice, stream));
+                HIPCHK(hipEventRecord(e0, stream));
+                sweep_2d(d_sv_x.p);
+                HIPCHK(hipEventRecord(e1, stream));
+                HIPCHK(hipMemcpyAsync(bj, d_sv_x.p, (size_t)n * sizeof(T), hipMemcpyDeviceToHost, stream));
+                HIPCHK(hipStreamSynchronize(stream));
+                float ms = 0;
+                HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+                total += ms;
+            }
+            (void)hipEventDestroy(e0);
+            (void)hipEventDestroy(e1);
+            stats.t_solve_ms = total;
+            return;
+        }
         SLU_REQUIRE(ldb >= n && nrhs >= 0, "solve: ldb %lld < n %d", (long long)ldb, n);
         constexpr int NB = SvNr<T>::v;
         if (nrhs > 1 && d_sv_x.n < (size_t)n * NB) d_sv_x.alloc((size_t)std::max(n, 1) * NB);

@@ -166,22 +166,26 @@ k_sv_udiag(const SvDiag *items, const T *Lval, T *x, int64_t ldx, int nr) {
         if (q < nr && t < w) x[it.fst + t + q * ldx] = yi[q];
 }
 
-// x[rows below] -= L_panel(256-row chunk) * y_k.
+// x[rows below] -= L_panel(256-row chunk) * y_k.  The panel descriptor
+// (SvDiag fields) points at the first row below the diagonal block: voff =
+// its offset in Lval, ld = nsupr, pad = number of rows below (on a 2D grid
+// the rank's rows of L(:,k) on its process row; on the diagonal owner they
+// follow the diagonal block, elsewhere the column block has none).
 template <typename T, int NR>
 __global__ void __launch_bounds__(SV_THREADS)
-k_sv_lpanel(const SvChunk *chunks, const SvDiag *diag, const int64_t *roff, const int *rows,
+k_sv_lpanel(const SvChunk *chunks, const SvDiag *pan, const int64_t *roff, const int *rows,
             const T *Lval, T *x, int64_t ldx, int nr) {
     using Sx = S<T>;
     const SvChunk ch = chunks[blockIdx.x];
-    const SvDiag it = diag[ch.sn];
-    const int t = threadIdx.x, w = it.w, nb = it.ld - it.w;
+    const SvDiag it = pan[ch.sn];
+    const int t = threadIdx.x, w = it.w, nb = it.pad;
     __shared__ T s_y[NR][FAST_MAXW * 2];
     for (int q = 0; q < nr; ++q)
         for (int j = t; j < w; j += SV_THREADS) s_y[q][j] = x[it.fst + j + q * ldx];
     __syncthreads();
     const int r = ch.c0 + t;
     if (r >= nb) return;
-    const T *L = Lval + it.voff + w + r;
+    const T *L = Lval + it.voff + r;
     T acc[NR];
 #pragma unroll
     for (int q = 0; q < NR; ++q) acc[q] = Sx::zero();
@@ -253,6 +257,29 @@ k_sv_upanel(const SvChunk *chunks, const SvDiag *diag, const int64_t *coff, cons
 #pragma unroll
         for (int q = 0; q < NR; ++q)
             if (q < nr) Sx::atomic_sub(x + it.fst + i + q * ldx, Sx::neg(acc[q]));
+    }
+}
+
+// 2D-grid solve helpers (pdgstrs's lsum reduction, SRC/pdgstrs_lsum.c): the
+// diagonal owner of a block row adds the nslot partial sums its process row
+// sent, stored one after another (x[dst + i] += sum_s slot[src + s*len + i]);
+// one item per block row, so no two workgroups update the same x.  Rows this
+// rank does not own start a sweep at zero (x[dst + i] = 0 for src < 0).
+struct SvAdd {
+    int64_t dst, src;
+    int len, nslot;
+};
+template <typename T>
+__global__ void __launch_bounds__(256) k_sv_add(const SvAdd *items, T *x, const T *slot) {
+    const SvAdd it = items[blockIdx.x];
+    for (int i = threadIdx.x; i < it.len; i += 256) {
+        if (it.src < 0) {
+            x[it.dst + i] = S<T>::zero();
+            continue;
+        }
+        T v = x[it.dst + i];
+        for (int q = 0; q < it.nslot; ++q) v = S<T>::sub(v, S<T>::neg(slot[it.src + (int64_t)q * it.len + i]));
+        x[it.dst + i] = v;
     }
 }
 

@@ -123,8 +123,9 @@ class Plan:
         self._chk(lib().slu_plan_download(self.ptr))
 
     def solve(self, b):
-        """Solve L U x = b with the device-resident factors (1x1 grid, the
-        LUstruct's permuted coordinates); b: (n,) or (n, nrhs).  Returns x."""
+        """Solve L U x = b with the device-resident factors (the LUstruct's
+        permuted coordinates); b: (n,) or (n, nrhs).  Returns x.  On a 2D grid
+        every rank calls it with the same b and receives the whole x."""
         dt = self.lu.Lval.dtype
         x = np.array(b, dtype=dt, order="F", copy=True)
         nrhs = 1 if x.ndim == 1 else x.shape[1]

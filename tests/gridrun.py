@@ -49,7 +49,7 @@ class GlooGrid:
         self.dist.broadcast(t, src=self.global_root(group, root), group=g)
 
 
-def _worker(rank, world, port, recipe, out_dir, device, fill=False):
+def _worker(rank, world, port, recipe, out_dir, device, fill=False, solve=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     try:
         import torch.distributed as dist
@@ -81,9 +81,15 @@ def _worker(rank, world, port, recipe, out_dir, device, fill=False):
             else:
                 p.upload()
             info, ntiny = p.factor(anorm)
+            if solve:  # the 2D-grid device solve of the fixture's right-hand side
+                from lusolve import from_lu_coords, to_lu_coords
+                b, R, C, perm_r, perm_c, _, _ = fx.full_rhs()
+                y = p.solve(to_lu_coords(b, perm_r, perm_c, R).astype(lu.Lval.dtype))
+                res["x"] = from_lu_coords(y, perm_c, C)
+                res["t_solve_ms"] = p.stats()["t_solve_ms"]
             p.download()
             st = p.stats()
-            res = dict(info=info, tiny=ntiny, flops=st["schur_flops"] + st["panel_flops"],
+            res.update(info=info, tiny=ntiny, flops=st["schur_flops"] + st["panel_flops"],
                        comm_bytes=st["comm_bytes"])
             del p
         else:  # group plumbing only
@@ -103,7 +109,7 @@ def _worker(rank, world, port, recipe, out_dir, device, fill=False):
         raise
 
 
-def run_grid(recipe, pr, pc, out_dir, device=0, timeout=240, fill=False):
+def run_grid(recipe, pr, pc, out_dir, device=0, timeout=240, fill=False, solve=False):
     """Run ``recipe`` (picklable callable returning cases.build()-style
     tuples, or "refdump:<case>" for the per-rank LUstructs of a reference
     dump fixture) on a pr x pc grid; returns the per-rank result dicts.
@@ -115,7 +121,7 @@ def run_grid(recipe, pr, pc, out_dir, device=0, timeout=240, fill=False):
     ctx = mp.get_context("spawn")
     world = pr * pc
     port = free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, recipe, str(out_dir), device, fill))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, recipe, str(out_dir), device, fill, solve))
              for r in range(world)]
     for p in procs:
         p.start()

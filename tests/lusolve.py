@@ -94,3 +94,108 @@ def lu_coords_matrix(fx):
     np.add.at(colptr, cols_sorted + 1, 1)
     colptr = np.cumsum(colptr)
     return colptr, rows[order].astype(np.int64), av[order]
+
+
+def _lcol(lu, k, pc):
+    """Local L column block of supernode k on this rank: (values nsupr x w,
+    global rows, number of diagonal-block rows on top)."""
+    ljb = k // pc
+    if ljb >= len(lu.Loff) or lu.Loff[ljb] < 0:
+        return None
+    xs = lu.xsup
+    w = xs[k + 1] - xs[k]
+    idx = lu.Lidx[lu.Loff[ljb]:]
+    ld = idx[1]
+    blk = lu.Lval[lu.Lvoff[ljb]:lu.Lvoff[ljb] + ld * w].reshape(w, ld).T
+    rows, p, top = [], 2, 0
+    for _ in range(idx[0]):
+        gb, nr = idx[p], idx[p + 1]
+        if gb == k:
+            top = nr
+        rows.extend(idx[p + 2:p + 2 + nr])
+        p += 2 + nr
+    return blk, np.array(rows, dtype=np.int64), top
+
+
+def solve_grid_sim(lus, pr, pc, b, fwd_only=False):
+    """The distributed solve of the engine's 2D-grid path (engine.hip
+    sweep_2d; pdgstrs's lsum scheme, SRC/pdgstrs.c) simulated over all ranks'
+    LUstructs with one x vector per rank: block row k's partial sums live on
+    process row k % pr and are added on the diagonal owner; the solved piece
+    goes down the owner's process column.  Elimination order k = 0..ns-1 is
+    one topological order of the engine's levels.  Returns x (full)."""
+    ns = lus[0].nsupers
+    xs = lus[0].xsup
+    P = pr * pc
+    dt = np.result_type(lus[0].Lval.dtype, np.float64)
+    own = lambda k: (k % pr) * pc + k % pc  # noqa: E731
+    x = [np.zeros(len(b), dtype=dt) for _ in range(P)]
+    for k in range(ns):
+        x[own(k)][xs[k]:xs[k + 1]] = b[xs[k]:xs[k + 1]]
+    lcols = [{k: _lcol(lus[p], k, pc) for k in range(ns) if k % pc == p % pc} for p in range(P)]
+
+    def reduce(k):
+        f, l, o = xs[k], xs[k + 1], own(k)
+        for c in range(pc):
+            s = (k % pr) * pc + c
+            if s != o:
+                x[o][f:l] += x[s][f:l]
+
+    def bcast(k):
+        f, l, o = xs[k], xs[k + 1], own(k)
+        for r in range(pr):
+            x[r * pc + k % pc][f:l] = x[o][f:l]
+
+    for k in range(ns):  # L y = b
+        f, l, o = xs[k], xs[k + 1], own(k)
+        w = l - f
+        reduce(k)
+        blk, rows, top = lcols[o][k]
+        x[o][f:l] = solve_triangular(blk[:w], x[o][f:l], lower=True, unit_diagonal=True)
+        bcast(k)
+        for r in range(pr):
+            p = r * pc + k % pc
+            c = lcols[p].get(k)
+            if c is None:
+                continue
+            blk, rows, top = c
+            if len(rows) > top:
+                x[p][rows[top:]] -= blk[top:] @ x[p][f:l]
+    if fwd_only:
+        out = np.empty(len(b), dtype=dt)
+        for k in range(ns):
+            out[xs[k]:xs[k + 1]] = x[own(k)][xs[k]:xs[k + 1]]
+        return out
+    for p in range(P):  # rows a rank does not own start the backward sweep at zero
+        for k in range(ns):
+            if own(k) != p:
+                x[p][xs[k]:xs[k + 1]] = 0
+    for k in range(ns - 1, -1, -1):  # U x = y
+        f, l, o = xs[k], xs[k + 1], own(k)
+        w = l - f
+        for c in range(pc):
+            p = (k % pr) * pc + c
+            lu = lus[p]
+            lb = k // pr
+            if lb >= len(lu.Uoff) or lu.Uoff[lb] < 0:
+                continue
+            idx = lu.Uidx[lu.Uoff[lb]:]
+            v = lu.Uval[lu.Uvoff[lb]:]
+            q, qq = 3, 0
+            for _ in range(idx[0]):
+                jb = idx[q]
+                for cc in range(xs[jb + 1] - xs[jb]):
+                    fst = idx[q + 2 + cc]
+                    seg = l - fst
+                    if seg:
+                        x[p][fst:l] -= v[qq:qq + seg] * x[p][xs[jb] + cc]
+                    qq += seg
+                q += 2 + xs[jb + 1] - xs[jb]
+        reduce(k)
+        blk, rows, top = lcols[o][k]
+        x[o][f:l] = solve_triangular(blk[:w], x[o][f:l], lower=False)
+        bcast(k)
+    out = np.empty(len(b), dtype=dt)
+    for k in range(ns):
+        out[xs[k]:xs[k + 1]] = x[own(k)][xs[k]:xs[k + 1]]
+    return out

@@ -54,5 +54,14 @@ class Fixture:
     def lus(self, tag="pre"):
         return [self.lu(p, tag) for p in range(self.nranks)]
 
+    def full_rhs(self):
+        """b, R, C, perm_r, perm_c, x_norefine, xtrue as full vectors: the
+        reference's distributed B / X (NRformat_loc rows fst_row .. fst_row +
+        m_loc of each rank) put back together."""
+        order = sorted(range(self.nranks), key=lambda p: self.meta["ranks"][p]["fst_row"])
+        cat = lambda k: np.concatenate([self.arr(p, k) for p in order])  # noqa: E731
+        return (cat("b"), self.z.get("r0_R"), self.z.get("r0_C"), self.arr(0, "perm_r"),
+                self.arr(0, "perm_c"), cat("x_norefine"), cat("xtrue"))
+
     def ref_factors(self):
         return [(self.arr(p, "post_Lval"), self.arr(p, "post_Uval")) for p in range(self.nranks)]

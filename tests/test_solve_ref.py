@@ -12,6 +12,10 @@ berr), all from oracle/_ref/ref_dump running p?gssvx.
   device solve and the device refinement reproduce the reference's x within
   the accuracy the reference itself reaches (||x_ref - xtrue||), and the
   refined backward error is at the reference's level.
+* GPU, 2D grids: the distributed device solve (lsum partial sums reduced
+  along process rows to the diagonal owners, solved pieces down the process
+  columns, as pdgstrs) on the engine's factors of the reference's grid
+  LUstructs reproduces the reference's pdgstrs x_norefine on the same grid.
 """
 import numpy as np
 import pytest
@@ -81,3 +85,45 @@ def test_gpu_fill_solve_refine_match_reference(name):
     ref_berr = float(fx.arr(0, "berr")[0])
     assert berr[0] <= max(4 * ref_berr, 4 * EPS[fx.dtype]), (berr[0], ref_berr)
     assert abs(int(steps[0]) - fx.meta["ranks"][0]["refine_steps"]) <= 1
+
+
+GRID_CASES = [n for n in names() if "_1x1_" not in n and not n.startswith("zeropiv")]
+
+
+@pytest.mark.parametrize("name", GRID_CASES)
+def test_grid_fixture_rhs_reassembles(name):
+    """The per-rank pieces of the reference's distributed B / X put back
+    together solve the reference's own factored system (host check)."""
+    fx = Fixture(name)
+    b, R, C, perm_r, perm_c, xnr, xtrue = fx.full_rhs()
+    assert b.shape == xnr.shape == xtrue.shape == (fx.n,)
+    d, tol = _close(xnr, xnr, xtrue, fx.dtype)
+    assert d == 0 and np.isfinite(xnr).all()
+    assert np.abs(xnr - xtrue).max() / np.abs(xtrue).max() < max(1e-6, 1e3 * EPS[fx.dtype])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", GRID_CASES)
+def test_gpu_grid_solve_matches_reference(name, tmp_path):
+    from gridrun import run_grid
+    fx = Fixture(name)
+    out = run_grid(f"refdump:{name}", fx.pr, fx.pc, tmp_path, device=0, solve=True)
+    _, _, _, _, _, xnr, xtrue = fx.full_rhs()
+    for p, o in enumerate(out):  # x comes back replicated on every rank
+        assert int(o["info"]) == fx.info
+        d, tol = _close(o["x"], xnr, xtrue, fx.dtype)
+        assert d < tol, (p, d, tol)
+
+
+@pytest.mark.parametrize("name", GRID_CASES)
+def test_grid_solve_algorithm_reproduces_reference_pdgstrs(name):
+    """The engine's distributed solve scheme (lusolve.solve_grid_sim: partial
+    sums per process row, reduced to the diagonal owner; solved pieces down
+    the owner's process column), run on the reference's own factors of its
+    grid LUstructs, gives the reference's pdgstrs x_norefine (CPU)."""
+    from lusolve import solve_grid_sim
+    fx = Fixture(name)
+    b, R, C, perm_r, perm_c, xnr, xtrue = fx.full_rhs()
+    y = solve_grid_sim(fx.lus("post"), fx.pr, fx.pc, to_lu_coords(b, perm_r, perm_c, R))
+    d, tol = _close(from_lu_coords(y, perm_c, C), xnr, xtrue, fx.dtype)
+    assert d < tol, (d, tol)
