@@ -185,8 +185,10 @@ int slu_plan_solve(slu_plan *p, void *b, int64_t ldb, int nrhs);
  * t_fill_ms in the stats is the device time of the zero + scatter. */
 int slu_plan_set_a_pattern(slu_plan *p, int64_t ncol, const int64_t *xa, const int64_t *asub);
 int slu_plan_fill_a(slu_plan *p, const void *a, int on_device);
-/* Iterative refinement on the device (SRC/pdgsrfs.c:197-253; 1x1 grid, the
- * LUstruct's permuted coordinates): for each of the nrhs columns of b / x
+/* Iterative refinement on the device (SRC/pdgsrfs.c:197-253, the LUstruct's
+ * permuted coordinates; on a 2D grid collective, b and x replicated, the
+ * residual as pdgsmv's: each rank's entries of A give partial rows, reduced
+ * along process rows to the diagonal owners): for each of the nrhs columns of b / x
  * (ld ld, host arrays of the plan's element type), repeat R = b - A x,
  * berr = max_i |R_i| / (|A||x| + |b|)_i (SAFE1/SAFE2 guards), and while
  * berr > eps, berr <= lstres / 2 and fewer than 20 steps, x += solve(R) with

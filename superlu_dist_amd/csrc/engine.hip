@@ -2481,11 +2481,14 @@ struct Plan : PlanBase {
                                    d_sv_lvl.p + sv_d_off[L], d_L.p, xv, (i64)n, 1);
             sv_bcast(L, xv, false);
         }
-        // x replicated on every rank: each owner's pieces to the world
+        sv_gather(xv);
+        HIPCHK(hipGetLastError());
+    }
+    // each diagonal owner's block rows of xv to every rank (xv replicated)
+    void sv_gather(T *xv) {
         for (int k = 0; k < nsupers; ++k)
             X.section(G_WORLD, (k % Pr) * Pc + k % Pc, ~0u, xv + xsup[k], (size_t)W(k) * sizeof(T));
         X.flush();
-        HIPCHK(hipGetLastError());
     }
 
     // right-hand sides in batches of SvNr<T>: every factor element is read once
@@ -2558,8 +2561,70 @@ struct Plan : PlanBase {
     DevBuf<T> d_rf_b, d_rf_x, d_rf_r;
     DevBuf<unsigned long long> d_rf_berr;
 
+    // 2D grids: the same loop with pdgsmv's distributed residual (solve.h
+    // k_resid_part / k_resid_fin): partial rows from each rank's entries of
+    // A, reduced along process rows to the diagonal owners, berr = the max
+    // over the owners, R gathered to every rank, then the 2D solve.
+    vector<RfRow> rf_rows_h;
+    DevBuf<RfRow> d_rf_rows;
+    DevBuf<double> d_rf_s, d_rf_ss;
+    DevBuf<T> d_rf_sr;
+    vector<std::array<i64, 3>> rf_secs; // (block row, sending column, owner slot)
+
+    void build_refine_2d() {
+        rf_rows_h.clear();
+        rf_secs.clear();
+        i64 slot = 0;
+        for (int k = 0; k < nsupers; ++k) {
+            if (k % Pr != myrow) continue;
+            const bool own = k % Pc == mycol;
+            if (own) rf_rows_h.push_back({(i64)xsup[k], slot, W(k), Pc - 1});
+            for (int c = 0; c < Pc; ++c) {
+                if (c == k % Pc) continue;
+                rf_secs.push_back({k, c, own ? slot : -1});
+                if (own) slot += W(k);
+            }
+        }
+        d_rf_rows.upload(rf_rows_h.empty() ? vector<RfRow>(1) : rf_rows_h);
+        d_rf_sr.alloc(std::max<i64>(slot, 1));
+        d_rf_ss.alloc(std::max<i64>(slot, 1));
+        d_rf_s.alloc(std::max(n, 1));
+        HIPCHK(hipDeviceSynchronize());
+    }
+
+    double resid_2d(double safe1, double safe2) {
+        const unsigned rb = (unsigned)((n + 255) / 256);
+        X.s = stream;
+        hipLaunchKernelGGL(k_resid_part<T>, dim3(rb), dim3(256), 0, stream, d_rp.p, d_rc.p, d_re.p,
+                           a_fact, d_rf_x.p, d_rf_r.p, d_rf_s.p, n);
+        for (const auto &q : rf_secs) {
+            const int k = (int)q[0], c = (int)q[1], oc = k % Pc;
+            const size_t w = (size_t)W(k);
+            void *br = mycol == c ? (void *)(d_rf_r.p + xsup[k]) : mycol == oc ? (void *)(d_rf_sr.p + q[2]) : nullptr;
+            void *bs = mycol == c ? (void *)(d_rf_s.p + xsup[k]) : mycol == oc ? (void *)(d_rf_ss.p + q[2]) : nullptr;
+            X.section(G_ROW, c, 1u << oc, br, w * sizeof(T));
+            X.section(G_ROW, c, 1u << oc, bs, w * sizeof(double));
+        }
+        X.flush();
+        HIPCHK(hipMemsetAsync(d_rf_berr.p, 0, sizeof(unsigned long long), stream));
+        if (!rf_rows_h.empty())
+            hipLaunchKernelGGL(k_resid_fin<T>, dim3((unsigned)rf_rows_h.size()), dim3(256), 0, stream,
+                               d_rf_rows.p, d_rf_b.p, d_rf_r.p, d_rf_s.p, d_rf_sr.p, d_rf_ss.p, safe1,
+                               safe2, d_rf_berr.p);
+        HIPCHK(hipGetLastError());
+        unsigned long long bits = 0;
+        HIPCHK(hipMemcpyAsync(&bits, d_rf_berr.p, sizeof bits, hipMemcpyDeviceToHost, stream));
+        HIPCHK(hipStreamSynchronize(stream));
+        // the max over the owners (bit patterns of non-negative doubles, NaN above +Inf)
+        auto all = X.allgatherv(G_WORLD, vector<i64>(1, (i64)bits));
+        unsigned long long m = 0;
+        for (auto &v : all) m = std::max(m, (unsigned long long)v[0]);
+        double be;
+        memcpy(&be, &m, sizeof be);
+        return be;
+    }
+
     void refine(const void *b, void *x, int64_t ld, int nrhs, double *berr, int *steps) override {
-        SLU_REQUIRE(Pr * Pc == 1, "refine: 1x1 grids only");
         SLU_REQUIRE(vstate == 2, "refine: the device storage holds no factors (factor first)");
         SLU_REQUIRE(a_fact != nullptr,
                     "refine needs the values of A the factors came from (slu_plan_fill_a "
@@ -2574,6 +2639,7 @@ struct Plan : PlanBase {
         d_rf_x.alloc(std::max(n, 1));
         d_rf_r.alloc(std::max(n, 1));
         d_rf_berr.alloc(1);
+        if (xmode && rf_rows_h.empty() && rf_secs.empty()) build_refine_2d();
         const unsigned rb = (unsigned)((n + 255) / 256);
         hipEvent_t e0, e1;
         HIPCHK(hipEventCreate(&e0));
@@ -2588,16 +2654,25 @@ struct Plan : PlanBase {
             int count = 0;
             double lstres = 3.0, be = 0.0;
             while (true) {
-                HIPCHK(hipMemsetAsync(d_rf_berr.p, 0, sizeof(unsigned long long), stream));
-                hipLaunchKernelGGL(k_resid<T>, dim3(rb), dim3(256), 0, stream, d_rp.p, d_rc.p, d_re.p,
-                                   a_fact, d_rf_x.p, d_rf_b.p, d_rf_r.p, n, safe1, safe2, d_rf_berr.p);
-                HIPCHK(hipGetLastError());
-                unsigned long long bits = 0;
-                HIPCHK(hipMemcpyAsync(&bits, d_rf_berr.p, sizeof bits, hipMemcpyDeviceToHost, stream));
-                HIPCHK(hipStreamSynchronize(stream));
-                memcpy(&be, &bits, sizeof be);
+                if (xmode) {
+                    be = resid_2d(safe1, safe2);
+                } else {
+                    HIPCHK(hipMemsetAsync(d_rf_berr.p, 0, sizeof(unsigned long long), stream));
+                    hipLaunchKernelGGL(k_resid<T>, dim3(rb), dim3(256), 0, stream, d_rp.p, d_rc.p, d_re.p,
+                                       a_fact, d_rf_x.p, d_rf_b.p, d_rf_r.p, n, safe1, safe2, d_rf_berr.p);
+                    HIPCHK(hipGetLastError());
+                    unsigned long long bits = 0;
+                    HIPCHK(hipMemcpyAsync(&bits, d_rf_berr.p, sizeof bits, hipMemcpyDeviceToHost, stream));
+                    HIPCHK(hipStreamSynchronize(stream));
+                    memcpy(&be, &bits, sizeof be);
+                }
                 if (!(be > eps && be * 2 <= lstres && count < 20)) break;
-                sweep(d_rf_r.p);
+                if (xmode) {
+                    sv_gather(d_rf_r.p); // R from its owners to every rank, then the 2D solve
+                    sweep_2d(d_rf_r.p);
+                } else {
+                    sweep(d_rf_r.p);
+                }
                 hipLaunchKernelGGL(k_axpy1<T>, dim3(rb), dim3(256), 0, stream, d_rf_x.p, d_rf_r.p, n);
                 lstres = be;
                 ++count;
@@ -2681,14 +2756,21 @@ struct Plan : PlanBase {
         d_aval.alloc(std::max<i64>(nnz, 1));
         a_nnz = nnz;
         d_acur = a_fact = snap_acur = nullptr; // the previous pattern's values are gone
-        if (Pr * Pc == 1) { // rows of A for the refinement's residual (k_resid)
-            vector<i64> rp(n + 1, 0), re((size_t)nnz);
-            vector<int> rc((size_t)nnz);
-            for (i64 e = 0; e < nnz; ++e) ++rp[asub[e] + 1];
+        {   // rows of A for the refinement's residual (k_resid): all of A on a
+            // 1x1 grid, this rank's entries (those of its blocks) on a 2D grid
+            auto mine = [&](i64 e, int j) {
+                return !xmode || ((int)supno[j] % Pc == mycol && (int)supno[asub[e]] % Pr == myrow);
+            };
+            vector<i64> rp(n + 1, 0);
+            for (int j = 0; j < n; ++j)
+                for (i64 e = xa[j]; e < xa[j + 1]; ++e)
+                    if (mine(e, j)) ++rp[asub[e] + 1];
             for (int i = 0; i < n; ++i) rp[i + 1] += rp[i];
-            vector<i64> nx(rp.begin(), rp.end() - 1);
+            vector<i64> re((size_t)rp[n]), nx(rp.begin(), rp.end() - 1);
+            vector<int> rc((size_t)rp[n]);
             for (int j = 0; j < n; ++j)
                 for (i64 e = xa[j]; e < xa[j + 1]; ++e) {
+                    if (!mine(e, j)) continue;
                     const i64 q = nx[asub[e]]++;
                     rc[q] = j;
                     re[q] = e;
@@ -2696,6 +2778,7 @@ struct Plan : PlanBase {
             d_rp.upload(rp);
             d_rc.upload(rc.empty() ? vector<int>(1, 0) : rc);
             d_re.upload(re.empty() ? vector<i64>(1, 0) : re);
+            HIPCHK(hipDeviceSynchronize());
         }
     }
 

@@ -283,6 +283,65 @@ __global__ void __launch_bounds__(256) k_sv_add(const SvAdd *items, T *x, const 
     }
 }
 
+// 2D-grid refinement (pdgsrfs with pdgsmv's distributed product,
+// SRC/pdgsrfs.c:197-253, SRC/pdgsmv.c): every entry of A lives on the rank
+// of its block, so a rank forms partial rows r_p = -A_p x and s_p = |A_p||x|
+// from its own entries (rows in CSR over this rank's nonzeros, x replicated).
+template <typename T>
+__global__ void __launch_bounds__(256)
+k_resid_part(const int64_t *rp, const int *rc, const int64_t *re, const T *a, const T *x, T *r,
+             double *s, int n) {
+    using Sx = S<T>;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    T acc = Sx::zero();
+    double tmp = 0.0;
+    for (int64_t e = rp[i]; e < rp[i + 1]; ++e) {
+        const T av = a[re[e]], xv = x[rc[e]];
+        acc = Sx::fms(acc, av, xv);
+        tmp += Sx::abs1(av) * Sx::abs1(xv);
+    }
+    r[i] = acc;
+    s[i] = tmp;
+}
+// The partial rows of a block row go to its diagonal owner along the
+// process row (nslot consecutive slots each), and the owner finishes them:
+// r = b + sum r_p, s = |b| + sum s_p, berr = max |r_i| / s_i with the
+// SAFE1 / SAFE2 guards, NaN winning the max as in k_resid.
+struct RfRow {
+    int64_t fst, src; // first row; first slot (elements) of the block row
+    int len, nslot;
+};
+template <typename T>
+__global__ void __launch_bounds__(256)
+k_resid_fin(const RfRow *items, const T *b, T *r, const double *s, const T *slot_r,
+            const double *slot_s, double safe1, double safe2, unsigned long long *berr) {
+    using Sx = S<T>;
+    const RfRow it = items[blockIdx.x];
+    double mx = 0.0;
+    for (int i = threadIdx.x; i < it.len; i += 256) {
+        const int64_t row = it.fst + i;
+        T rv = Sx::sub(r[row], Sx::neg(b[row]));
+        double sv = s[row] + Sx::abs1(b[row]);
+        for (int q = 0; q < it.nslot; ++q) {
+            rv = Sx::sub(rv, Sx::neg(slot_r[it.src + (int64_t)q * it.len + i]));
+            sv += slot_s[it.src + (int64_t)q * it.len + i];
+        }
+        r[row] = rv;
+        const double ra = Sx::abs1(rv);
+        double e = 0.0;
+        if (sv > safe2) e = ra / sv;
+        else if (sv != 0.0) e = (safe1 + ra) / sv;
+        mx = (mx != mx || e != e) ? __builtin_nan("") : fmax(mx, e);
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        const double o = __shfl_xor(mx, off, 64);
+        mx = (mx != mx || o != o) ? __builtin_nan("") : fmax(mx, o);
+    }
+    if ((threadIdx.x & 63) == 0 && !(mx <= 0.0))
+        atomicMax(berr, (unsigned long long)__double_as_longlong(mx));
+}
+
 // Residual of the iterative refinement (SRC/pdgsrfs.c:209-230) by rows of A
 // (CSR index over the CSC values): r = b - A x, s = |A||x| + |b| (abs1 for
 // complex, as pzgsrfs), berr = max_i |r_i| / s_i with the SAFE1 / SAFE2

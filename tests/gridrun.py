@@ -74,19 +74,28 @@ def _worker(rank, world, port, recipe, out_dir, device, fill=False, solve=False)
         if device is not None:
             comm = Comm.host(pr, pc, rank, device, gg.bcast)
             p = Plan(lu, comm=comm, replace_tiny=tiny)
-            if fill:  # values from A on the device (no LU upload), SamePattern refill
+            if fill and A is not None:  # values from A on the device (no LU upload), SamePattern refill
                 cp, ri, v = A.permuted(S.perm_c).arrays()
+                p.set_a_pattern(cp, ri)
+                p.fill_a(v)
+            elif solve:  # the fixture's A in the LUstruct's coordinates, filled on the device
+                from lusolve import lu_coords_matrix_from_lus
+                cp, ri, v = lu_coords_matrix_from_lus(fx.lus("pre"), pr, pc)
                 p.set_a_pattern(cp, ri)
                 p.fill_a(v)
             else:
                 p.upload()
             info, ntiny = p.factor(anorm)
-            if solve:  # the 2D-grid device solve of the fixture's right-hand side
+            if solve:  # the 2D-grid device solve and refinement of the fixture's right-hand side
                 from lusolve import from_lu_coords, to_lu_coords
                 b, R, C, perm_r, perm_c, _, _ = fx.full_rhs()
-                y = p.solve(to_lu_coords(b, perm_r, perm_c, R).astype(lu.Lval.dtype))
+                bl = to_lu_coords(b, perm_r, perm_c, R).astype(lu.Lval.dtype)
+                y = p.solve(bl)
                 res["x"] = from_lu_coords(y, perm_c, C)
                 res["t_solve_ms"] = p.stats()["t_solve_ms"]
+                yr, berr, steps = p.refine(bl, y)
+                res["xr"] = from_lu_coords(yr, perm_c, C)
+                res["berr"], res["steps"] = float(berr[0]), int(steps[0])
             p.download()
             st = p.stats()
             res.update(info=info, tiny=ntiny, flops=st["schur_flops"] + st["panel_flops"],

@@ -82,12 +82,21 @@ def from_lu_coords(y, perm_c, C=None):
 
 def lu_coords_matrix(fx):
     """CSC (colptr, rowind, values) of Pc Pr diag(R) A diag(C) Pc^T from a
-    1x1 refdump fixture: pdgssvx leaves its local A scaled and with perm_c
-    applied to the column indices (SRC/pdgssvx.c:1140); rows are mapped here."""
-    rp, ci, av = fx.arr(0, "A_rowptr"), fx.arr(0, "A_colind"), fx.arr(0, "A_val")
+    refdump fixture: pdgssvx leaves its local A scaled and with perm_c
+    applied to the column indices (SRC/pdgssvx.c:1140); rows are mapped here.
+    On a grid the ranks' row slices (NRformat_loc, rows fst_row .. fst_row +
+    m_loc) are put back together."""
+    order = sorted(range(fx.nranks), key=lambda p: fx.meta["ranks"][p]["fst_row"])
+    rps, cis, avs, rws = [], [], [], []
+    for p in order:
+        rp = fx.arr(p, "A_rowptr")
+        rws.append(fx.meta["ranks"][p]["fst_row"] + np.repeat(np.arange(len(rp) - 1), np.diff(rp)))
+        cis.append(fx.arr(p, "A_colind"))
+        avs.append(fx.arr(p, "A_val"))
+    ci, av, grow = np.concatenate(cis), np.concatenate(avs), np.concatenate(rws)
     pr, pc = fx.arr(0, "perm_r"), fx.arr(0, "perm_c")
     n = fx.n
-    rows = pc[pr[np.repeat(np.arange(n), np.diff(rp))]]
+    rows = pc[pr[grow]]
     order = np.lexsort((rows, ci))
     cols_sorted = ci[order]
     colptr = np.zeros(n + 1, dtype=np.int64)
@@ -199,3 +208,48 @@ def solve_grid_sim(lus, pr, pc, b, fwd_only=False):
     for k in range(ns):
         out[xs[k]:xs[k + 1]] = x[own(k)][xs[k]:xs[k + 1]]
     return out
+
+
+def lu_coords_matrix_from_lus(lus, pr, pc):
+    """CSC of A in the LUstruct's coordinates read off the pre-factor
+    LUstructs of all ranks of a pr x pc grid (pddistribute scatters A's
+    entries into zero-initialised L and U blocks, so the nonzeros of the
+    pre-factor blocks are A's).  For grid fixtures, whose dumped local A is
+    in pdgsmv's compressed column numbering."""
+    xs = lus[0].xsup
+    ns = lus[0].nsupers
+    R, Cc, V = [], [], []
+    for p, lu in enumerate(lus):
+        myrow, mycol = p // pc, p % pc
+        for ljb in range(len(lu.Loff)):
+            k = ljb * pc + mycol
+            if k >= ns or lu.Loff[ljb] < 0:
+                continue
+            c = _lcol(lu, k, pc)
+            blk, rows, _ = c
+            for j in range(blk.shape[1]):
+                nz = np.nonzero(blk[:, j])[0]
+                R.extend(rows[nz]); Cc.extend([xs[k] + j] * len(nz)); V.extend(blk[nz, j])
+        for lb in range(len(lu.Uoff)):
+            k = lb * pr + myrow
+            if k >= ns or lu.Uoff[lb] < 0:
+                continue
+            idx = lu.Uidx[lu.Uoff[lb]:]
+            v = lu.Uval[lu.Uvoff[lb]:]
+            l = xs[k + 1]
+            q, qq = 3, 0
+            for _ in range(idx[0]):
+                jb = idx[q]
+                for cc in range(xs[jb + 1] - xs[jb]):
+                    fst = idx[q + 2 + cc]
+                    seg = v[qq:qq + l - fst]
+                    nz = np.nonzero(seg)[0]
+                    R.extend(fst + nz); Cc.extend([xs[jb] + cc] * len(nz)); V.extend(seg[nz])
+                    qq += l - fst
+                q += 2 + xs[jb + 1] - xs[jb]
+    R, Cc, V = np.array(R, dtype=np.int64), np.array(Cc, dtype=np.int64), np.array(V)
+    order = np.lexsort((R, Cc))
+    n = len(lus[0].supno) if hasattr(lus[0], "supno") else int(xs[-1])
+    colptr = np.zeros(n + 1, dtype=np.int64)
+    np.add.at(colptr, Cc[order] + 1, 1)
+    return np.cumsum(colptr), R[order], V[order].astype(lus[0].Lval.dtype)

@@ -15,7 +15,10 @@ berr), all from oracle/_ref/ref_dump running p?gssvx.
 * GPU, 2D grids: the distributed device solve (lsum partial sums reduced
   along process rows to the diagonal owners, solved pieces down the process
   columns, as pdgstrs) on the engine's factors of the reference's grid
-  LUstructs reproduces the reference's pdgstrs x_norefine on the same grid.
+  LUstructs (values filled on the device from the reference's A)
+  reproduces the reference's pdgstrs x_norefine on the same grid, and the
+  grid refinement (residual from each rank's entries of A, reduced to the
+  owners, as pdgsmv) the reference's pdgsrfs x, berr and step count.
 """
 import numpy as np
 import pytest
@@ -109,10 +112,18 @@ def test_gpu_grid_solve_matches_reference(name, tmp_path):
     fx = Fixture(name)
     out = run_grid(f"refdump:{name}", fx.pr, fx.pc, tmp_path, device=0, solve=True)
     _, _, _, _, _, xnr, xtrue = fx.full_rhs()
+    xref = np.concatenate([fx.arr(p, "x") for p in sorted(range(fx.nranks),
+                                                        key=lambda q: fx.meta["ranks"][q]["fst_row"])])
+    ref_berr = float(fx.arr(0, "berr")[0])
     for p, o in enumerate(out):  # x comes back replicated on every rank
         assert int(o["info"]) == fx.info
         d, tol = _close(o["x"], xnr, xtrue, fx.dtype)
-        assert d < tol, (p, d, tol)
+        assert d < tol, ("solve", p, d, tol)
+        # refinement on the grid (pdgsrfs + the distributed residual of pdgsmv)
+        d, tol = _close(o["xr"], xref, xtrue, fx.dtype)
+        assert d < tol, ("refine", p, d, tol)
+        assert o["berr"] <= max(4 * ref_berr, 4 * EPS[fx.dtype]), (o["berr"], ref_berr)
+        assert abs(int(o["steps"]) - fx.meta["ranks"][0]["refine_steps"]) <= 1
 
 
 @pytest.mark.parametrize("name", GRID_CASES)
