@@ -1926,7 +1926,7 @@ struct Plan : PlanBase {
     }
 
     void launch_big(const LevelRange &R, int off, int cnt, hipStream_t st) {
-        hipLaunchKernelGGL(k_schur_big<T>, dim3(cnt), dim3(SB_THREADS), 0, st,
+        hipLaunchKernelGGL(k_schur_big<T>, dim3(cnt), dim3(BigCfg<T>::THREADS), 0, st,
                            d_tiles_big.p + off, d_kinfo.p + R.k_off, d_L.p, d_U.p,
                            d_lblk.p, d_lmap.p, d_ublk.p, d_ucol_voff.p, d_ucol_fst.p);
     }

@@ -1010,14 +1010,24 @@ k_trsm_blk(const TrsmItemF<T> *items) {
 // real MFMAs each (Mma<zc>), K staged 8 deep -- the same accumulator VGPRs,
 // MFMAs per stage and LDS per workgroup as the real tile, at twice the
 // MFMAs per LDS operand; the epilogue stages 16 columns per pass.
-constexpr int SB_BM = 128, SB_THREADS = 512;
+constexpr int SB_BM = 128;
+// THREADS / WN: workgroup size and waves along N; MINW: waves per SIMD the
+// register budget must allow (workgroups per CU x waves per workgroup / 4).
 template <typename T> struct BigCfg {
-    static constexpr int BN = 128, BK = 16, FN = 4, PASSW = 64;
+    static constexpr int THREADS = 512, WN = 2, MINW = 4, BN = 128, BK = 16, FN = 4, PASSW = 64;
 };
+#ifdef SLU_SB_NARROW
+// A/B (tools/ab_build.sh narrow "-DSLU_SB_NARROW"): fp64 tiles of 128 x 64 on
+// 4 waves (each 32 x 64 as in the wide tile), three workgroups per CU
+template <> struct BigCfg<double> {
+    static constexpr int THREADS = 256, WN = 1, MINW = 3, BN = 64, BK = 16, FN = 4, PASSW = 32;
+};
+#endif
 template <> struct BigCfg<zc> {
-    static constexpr int BN = 64, BK = 8, FN = 2, PASSW = 16;
+    static constexpr int THREADS = 512, WN = 2, MINW = 4, BN = 64, BK = 8, FN = 2, PASSW = 16;
 };
 constexpr int SB_BN = BigCfg<double>::BN;
+constexpr int SB_THREADS = 512; // the 512-thread configurations (k_schur_big<float>, <zc>)
 constexpr int SB_TB = 4; // epilogue tables: row blocks x column blocks per tile
 #ifndef SLU_SB_AEB
 #define SLU_SB_AEB 4 // atomic scatters formed per batch (A/B builds: -DSLU_SB_AEB=8)
@@ -1039,14 +1049,15 @@ __device__ unsigned slu_stamp_n;
 
 // 2 workgroups (16 waves) per CU need <= 128 VGPRs: ask for 4 waves per SIMD
 template <typename T>
-__global__ void __launch_bounds__(SB_THREADS, 4)
+__global__ void __launch_bounds__(BigCfg<T>::THREADS, BigCfg<T>::MINW)
 k_schur_big(const TileItem *tiles, const KInfo<T> *kinfo, T *Lval, T *Uval,
             const LBlk *lblk, const int *lmap, const UBlk *ublk,
             const int64_t *ucol_voff, const int *ucol_fst) {
     using Sx = S<T>;
     using M = Mma<T>;
     constexpr int SB_BN = BigCfg<T>::BN, SB_BK = BigCfg<T>::BK;
-    constexpr int WN = 2;                   // waves along N
+    constexpr int SB_THREADS = BigCfg<T>::THREADS;
+    constexpr int WN = BigCfg<T>::WN;       // waves along N
     constexpr int FM = 2, FN = BigCfg<T>::FN; // fragments per wave (32 x 16*FN)
     constexpr int PASSW = BigCfg<T>::PASSW; // epilogue columns per pass
     constexpr int LDS_A = SB_BM + 4, LDS_B = SB_BN + 4;
@@ -1055,12 +1066,20 @@ k_schur_big(const TileItem *tiles, const KInfo<T> *kinfo, T *Lval, T *Uval,
     constexpr int AE = SB_BM * SB_BK / SB_THREADS, BE = SB_BN * SB_BK / SB_THREADS;
     static_assert(PASSW * CLD <= 2 * STAGE, "C staging must fit in the stage buffers");
     static_assert(WN * 16 * FN == SB_BN && AE >= 1 && BE >= 1, "tile shape");
+    static_assert((SB_THREADS / 64 / WN) * 16 * FM == SB_BM, "waves along M");
+    constexpr int CPN = SB_TB * SB_BN, RLN = SB_TB * SB_BM;
+    static_assert(CPN <= SB_THREADS && RLN % SB_THREADS == 0, "table entries per thread");
+    // the epilogue tables go in the stage buffers' tail past the C staging
+    // where it is large enough, else in arrays of their own
+    constexpr bool TAIL = (2 * STAGE - PASSW * CLD) * (int)sizeof(T) >= CPN * 8 + RLN * 4;
     __shared__ T smem[2 * STAGE];
     __shared__ int s_rg[SB_BM], s_ra[SB_BM], s_cg[SB_BN], s_cb[SB_BN];
     __shared__ int64_t s_db[SB_TB * SB_TB], s_dmb[SB_TB * SB_TB]; // destination records
     __shared__ int s_dld[SB_TB * SB_TB];                          // ld (L) or -1 (U)
-    __shared__ int64_t s_cp[SB_TB * SB_BN];                       // [row block][column] column parts
-    __shared__ int s_rl[SB_TB * SB_BM];                           // [column block][row] lmap positions
+    __shared__ int64_t s_cpx[TAIL ? 1 : CPN];                     // [row block][column] column parts
+    __shared__ int s_rlx[TAIL ? 1 : RLN];                         // [column block][row] lmap positions
+    int64_t *const s_cp = TAIL ? (int64_t *)(smem + PASSW * CLD) : s_cpx;
+    int *const s_rl = TAIL ? (int *)(s_cp + CPN) : s_rlx;
 
 #ifdef SLU_SB_STAMP
     __shared__ uint64_t s_stamp_[5]; // in LDS: the stamps must not add VGPRs (occupancy)
@@ -1176,10 +1195,11 @@ k_schur_big(const TileItem *tiles, const KInfo<T> *kinfo, T *Lval, T *Uval,
     // half of the destination tables instead): per (row block, column) the
     // column part of the address, tagged with the column block (1 + bl) or
     // 0 for a U destination; per (column block, row) the lmap position.
-    constexpr int CPN = SB_TB * SB_BN, RLN = SB_TB * SB_BM;
-    static_assert(CPN <= SB_THREADS && RLN <= SB_THREADS, "one table entry per thread");
+    constexpr int RLT = RLN / SB_THREADS; // lmap positions per thread
     int64_t t_code = 0, t_uv = 0;
-    int t_fst = 0, t_rl = 0;
+    int t_fst = 0, t_rl[RLT];
+#pragma unroll
+    for (int u = 0; u < RLT; ++u) t_rl[u] = 0;
     if (tbl) {
         if (tid < CPN) {
             const int al = tid / SB_BN, c = tid % SB_BN;
@@ -1194,11 +1214,12 @@ k_schur_big(const TileItem *tiles, const KInfo<T> *kinfo, T *Lval, T *Uval,
                 }
             }
         }
-        {
-            const int bl = tid / SB_BM, rr = tid % SB_BM;
+#pragma unroll
+        for (int u = 0; u < RLT; ++u) {
+            const int e = tid + u * SB_THREADS, bl = e / SB_BM, rr = e % SB_BM;
             if (bl < NB && rr < mrows) {
                 const int rec = (s_ra[rr] - a0) * SB_TB + bl;
-                if (s_dld[rec] >= 0) t_rl = lmap[s_dmb[rec] + s_rg[rr]];
+                if (s_dld[rec] >= 0) t_rl[u] = lmap[s_dmb[rec] + s_rg[rr]];
             }
         }
     }
@@ -1206,7 +1227,8 @@ k_schur_big(const TileItem *tiles, const KInfo<T> *kinfo, T *Lval, T *Uval,
     __syncthreads();
     if (tbl) {
         if (tid < CPN) s_cp[tid] = t_code ? t_code : (t_uv - t_fst) * 8;
-        s_rl[tid] = t_rl;
+#pragma unroll
+        for (int u = 0; u < RLT; ++u) s_rl[tid + u * SB_THREADS] = t_rl[u];
     }
 
     // ---- epilogue: passes of PASSW columns through LDS, column-contiguous.

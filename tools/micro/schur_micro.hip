@@ -150,7 +150,7 @@ int main(int argc, char **argv) {
     double fl = 2.0 * m * n * kw;
     for (int r = 0; r < reps; ++r) {
         CK(hipEventRecord(e0));
-        hipLaunchKernelGGL(k_schur_big<double>, dim3(tiles.size()), dim3(SB_THREADS), 0, 0, dt, dk, dC,
+        hipLaunchKernelGGL(k_schur_big<double>, dim3(tiles.size()), dim3(BigCfg<double>::THREADS), 0, 0, dt, dk, dC,
                            (double *)nullptr, dl, dmap, (const UBlk *)nullptr, (const int64_t *)nullptr,
                            (const int *)nullptr);
         CK(hipEventRecord(e1));
