@@ -1925,6 +1925,16 @@ struct Plan : PlanBase {
         }
     }
 
+    // The rest of a level's Schur tiles go out as two launches, the first
+    // with rest_split %% of them (SLU_REST_SPLIT, SLU_REST_CHUNKS: A/B).  The
+    // next level's diag LU and TRSM workgroups (150 / 85 KB of LDS, up to 256
+    // VGPRs) fit only on a CU that no Schur workgroup holds; inside one
+    // launch every freed slot is refilled with the next Schur tile, so they
+    // would wait for the whole level.  Where the first launch drains they get
+    // CUs and run beside the second (100^3: 363 -> 345 ms; more split points
+    // gain nothing further, tools/ab_env.sh).
+    int rest_split = getenv("SLU_REST_SPLIT") ? atoi(getenv("SLU_REST_SPLIT")) : 30;
+    int rest_chunks = getenv("SLU_REST_CHUNKS") ? atoi(getenv("SLU_REST_CHUNKS")) : 1;
     void launch_big(const LevelRange &R, int off, int cnt, hipStream_t st) {
         hipLaunchKernelGGL(k_schur_big<T>, dim3(cnt), dim3(BigCfg<T>::THREADS), 0, st,
                            d_tiles_big.p + off, d_kinfo.p + R.k_off, d_L.p, d_U.p,
@@ -2058,8 +2068,17 @@ struct Plan : PlanBase {
             // the rest of L on the Schur stream, once the panels of L exist
             HIPCHK(hipStreamWaitEvent(stream, ev_pan[L], 0));
             if (R.big_n > R.bigc_n) {
+                // the first rest_split %% of the rest tiles as a launch of their own
+                const int nrest = R.big_n - R.bigc_n;
+                const int n1 = rest_split > 0 && !opts.serial ? (int)((i64)nrest * rest_split / 100) : 0;
+                const int nch = rest_chunks > 1 && !opts.serial ? rest_chunks : 1;
                 span(2, stream, [&] {
-                    launch_big(R, R.big_off + R.bigc_n, R.big_n - R.bigc_n, stream);
+                    if (n1 > 0) launch_big(R, R.big_off + R.bigc_n, n1, stream);
+                    for (int c = 0; c < nch; ++c) {
+                        const int a0 = n1 + (int)((i64)(nrest - n1) * c / nch);
+                        const int a1 = n1 + (int)((i64)(nrest - n1) * (c + 1) / nch);
+                        if (a1 > a0) launch_big(R, R.big_off + R.bigc_n + a0, a1 - a0, stream);
+                    }
                 });
                 stats.n_schur_launches++;
                 stats.n_schur_big_launches++;
