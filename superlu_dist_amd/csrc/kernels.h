@@ -1427,9 +1427,20 @@ k_trsm_reg(const TrsmItemF<T> *items) {
     const TrsmItemF<T> it = items[blockIdx.x];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int w = it.w, nb = (w + PW - 1) / PW;
+    // sW (each wave's 16 x PW layout-change tile) lives in the first rows of
+    // sT, which the block's MFMAs have read by then (a barrier separates
+    // them): 68 KB of LDS instead of 85, so the kernel fits beside a Schur
+    // workgroup (engine.hip, rest_split)
+#ifdef SLU_TRSM_SEPARATE_W
     __shared__ T sT[FAST_MAXW - PW][PW + 1];
+    __shared__ T sWx[TR_WAVES][16][PW + 1];
+    T (*W)[PW + 1] = sWx[wid];
+#else
+    __shared__ T sT[FAST_MAXW - PW][PW + 1];
+    static_assert(TR_WAVES * 16 <= FAST_MAXW - PW, "sW inside sT");
+    T (*W)[PW + 1] = sT + wid * 16;
+#endif
     __shared__ T sD[PW][PW + 1];
-    __shared__ T sW[TR_WAVES][16][PW + 1];
     const int rl = lane & 15, kq = lane >> 4;
     const int myr = wid * 16 + rl;
     const bool rv = myr < it.nrows;
@@ -1450,7 +1461,6 @@ k_trsm_reg(const TrsmItemF<T> *items) {
         }
         xa[s] = v;
     }
-    T (*W)[PW + 1] = sW[wid];
 #pragma unroll
     for (int b = 0; b < NBMAX; ++b) {
         if (b >= nb) break;
@@ -1477,6 +1487,9 @@ k_trsm_reg(const TrsmItemF<T> *items) {
             M::step(a0, xa[s], b0);
             M::step(a1, xa[s], b1);
         }
+#ifndef SLU_TRSM_SEPARATE_W
+        __syncthreads(); // every wave is done with sT before W (= its first rows) is written
+#endif
         // Z = X_b - acc: acc (C layout) -> LDS, read back in A layout
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
