@@ -875,6 +875,240 @@ k_diag_lu_f(const DiagItemF<T> *items, double thresh, int replace_tiny, int *tin
     }
 }
 
+// Co-resident variant of k_diag_lu_f: the same factorization, arithmetic
+// and outputs, on 4 waves with <= 256 VGPRs and 84 KB of LDS, so that it fits
+// on a CU where one Schur workgroup finished (k_schur_big holds 76 KB and 2
+// waves x 128 VGPRs per SIMD) instead of waiting for a CU no Schur workgroup
+// holds.  What it gives up for that: U11^{-1} and L11^{-1} share one LDS
+// tile (formed one after the other), and U12 / the trailing update go
+// through LDS in chunks of DC_CH columns instead of all at once.
+constexpr int DC_THREADS = 256, DC_CH = 16;
+template <typename T>
+__global__ void __launch_bounds__(DC_THREADS, 2)
+k_diag_lu_c(const DiagItemF<T> *items, double thresh, int replace_tiny, int *tiny_count,
+            int *zpiv) {
+    constexpr int PW = PWOf<T>::v;
+    constexpr int NW = DC_THREADS / 64;
+    using Sx = S<T>;
+    using M = Mma<T>;
+    const DiagItemF<T> it = items[blockIdx.x];
+    T *A = it.a;
+    const int ld = it.ld, w = it.w, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int nb = (w + PW - 1) / PW;
+    T *dinvU = it.dinv, *dinvLT = it.dinv + (int64_t)nb * PW * PW;
+    __shared__ T sP[FAST_MAXW][PW + 1]; // panel rows (row 0 = row p0), PW columns
+    __shared__ T sX[PW][PW + 1];        // U11^{-1}, then L11^{-1}
+    __shared__ T sC[PW][DC_CH + 1];     // a chunk of U12
+    __shared__ T s_rp[PW];
+    __shared__ int s_z[PW];
+    __shared__ int s_anyz;
+    for (int p = 0; p < nb; ++p) {
+        const int p0 = p * PW, pw = min(PW, w - p0), nrow = w - p0, nbl = nrow - pw;
+        T *A11 = A + p0 + (int64_t)p0 * ld;
+        // ---- 0. stage the panel (zero outside pw / below nrow, as k_diag_lu_f)
+        const int nrs = max(nrow, PW);
+        for (int e = tid; e < nrs * PW; e += DC_THREADS) {
+            const int r = e % nrs, c = e / nrs;
+            sP[r][c] = (c < pw && r < nrow) ? A11[r + (int64_t)c * ld] : Sx::zero();
+        }
+        __syncthreads();
+        // ---- 1. A11 = L11 U11 in registers (wave 0), as k_diag_lu_f
+        if (wid == 0) {
+            const int row = lane & (PW - 1);
+            T xr[PW];
+#pragma unroll
+            for (int c = 0; c < PW; ++c) xr[c] = (row < pw) ? sP[row][c] : Sx::zero();
+            int anyz = 0;
+#pragma unroll
+            for (int j = 0; j < PW; ++j) {
+                if (j < pw) {
+                    T piv = rlane(xr[j], j);
+                    if (replace_tiny && Sx::abs1(piv) < thresh) {
+                        piv = Sx::thresh(piv, thresh);
+                        if (lane == 0) atomicAdd(tiny_count, 1);
+                    }
+                    const int z = Sx::iszero(piv);
+                    if (z) {
+                        anyz = 1;
+                        if (lane == 0) atomicMax(&zpiv[it.k], it.fcol + p0 + j + 1);
+                    }
+                    const T rp = z ? Sx::zero() : Sx::recip(piv);
+                    const bool below = row > j;
+                    const T l = below ? (z ? xr[j] : Sx::mul(xr[j], rp)) : Sx::zero();
+                    xr[j] = below ? l : (row == j ? piv : xr[j]);
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int c = j + 1; c < PW; ++c) {
+                        xr[c] = Sx::fms(xr[c], l, rlane(xr[c], j));
+                        if ((c & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                    if (lane == 0) {
+                        s_rp[j] = rp;
+                        s_z[j] = z;
+                    }
+                }
+            }
+            if (lane < pw) {
+#pragma unroll
+                for (int c = 0; c < PW; ++c) sP[lane][c] = xr[c];
+            }
+            if (lane == 0) s_anyz = anyz;
+            if (lane >= pw && lane < PW) {
+                s_rp[lane] = Sx::zero();
+                s_z[lane] = 0;
+            }
+        }
+        __syncthreads();
+        // ---- 1b. U11^{-1} (wave 0, lane = column, column-sweep order)
+        if (wid == 0 && lane < PW) {
+            const int j = lane;
+            T x[PW];
+#pragma unroll
+            for (int i = 0; i < PW; ++i) x[i] = (i == j) ? one_of(Sx::zero()) : Sx::zero();
+#pragma unroll
+            for (int i = PW - 1; i >= 0; --i) {
+                x[i] = Sx::mul(x[i], s_rp[i]);
+#pragma unroll
+                for (int k = 0; k < i; ++k) x[k] = Sx::fms(x[k], sP[k][i], x[i]);
+            }
+#pragma unroll
+            for (int i = 0; i < PW; ++i) sX[i][j] = (i <= j && j < pw) ? x[i] : Sx::zero();
+        }
+        __syncthreads();
+        const bool anyz = s_anyz;
+        // ---- 2a. L21 = A21 U11^{-1} (or the substitution with the zero-pivot semantics)
+        if (!anyz) {
+            const int nfr = (nbl + 15) / 16;
+            for (int f = wid; f < nfr; f += NW) {
+                typename M::acc_t acc0 = M::zero(), acc1 = M::zero();
+                const int r = f * 16 + (lane & 15);
+#pragma unroll
+                for (int ks = 0; ks < PW; ks += M::KSTEP) {
+                    const int k = ks + (lane >> 4);
+                    const T av = r < nbl ? sP[pw + r][k] : Sx::zero();
+                    M::step(acc0, av, sX[k][lane & 15]);
+                    if (PW > 16) M::step(acc1, av, sX[k][16 + (lane & 15)]);
+                }
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int rr = f * 16 + M::row(lane, i), cc = lane & 15;
+                    if (rr < nbl) {
+                        sP[pw + rr][cc] = cc < pw ? M::get(acc0, i) : Sx::zero();
+                        if (PW > 16) sP[pw + rr][16 + cc] = 16 + cc < pw ? M::get(acc1, i) : Sx::zero();
+                    }
+                }
+            }
+        } else {
+            for (int t = tid; t < nbl; t += DC_THREADS) { // row t of L21: x U11 = a, column by column
+                for (int c = 0; c < PW; ++c) {
+                    T v = sP[pw + t][c];
+                    for (int i = 0; i < c; ++i) v = Sx::fms(v, sP[pw + t][i], sP[i][c]);
+                    sP[pw + t][c] = c >= pw ? Sx::zero() : s_z[c] ? v : Sx::mul(v, s_rp[c]);
+                }
+            }
+        }
+        for (int e = tid; e < PW * PW; e += DC_THREADS)
+            dinvU[(int64_t)p * PW * PW + e] = sX[e / PW][e % PW]; // row-major U11^{-1}
+        __syncthreads();
+        // ---- 1c. L11^{-1} into the same tile (wave 0), and the panel to global
+        if (wid == 0 && lane < PW) {
+            const int j = lane;
+            T x[PW];
+#pragma unroll
+            for (int i = 0; i < PW; ++i) x[i] = (i == j) ? one_of(Sx::zero()) : Sx::zero();
+#pragma unroll
+            for (int i = 0; i < PW; ++i)
+#pragma unroll
+                for (int k = i + 1; k < PW; ++k) x[k] = Sx::fms(x[k], sP[k][i], x[i]);
+#pragma unroll
+            for (int i = 0; i < PW; ++i) sX[i][j] = (i >= j && i < pw && j < pw) ? x[i] : Sx::zero();
+        }
+        for (int e = tid; e < nrow * pw; e += DC_THREADS) {
+            const int r = e % nrow, c = e / nrow;
+            A11[r + (int64_t)c * ld] = sP[r][c];
+        }
+        __syncthreads();
+        for (int e = tid; e < PW * PW; e += DC_THREADS) {
+            const int i = e / PW, jj = e % PW;
+            dinvLT[(int64_t)p * PW * PW + e] = sX[jj][i]; // row-major (L11^{-1})^T
+        }
+        // ---- 2b/3. per chunk of DC_CH columns right of the panel:
+        // U12 = L11^{-1} A12 (LDS), back to global, A22(:, chunk) -= L21 U12
+        for (int q0 = 0; q0 < nbl; q0 += DC_CH) {
+            const int qn = min(DC_CH, nbl - q0);
+            T *A12 = A11 + (int64_t)(pw + q0) * ld;
+            for (int e = tid; e < PW * DC_CH; e += DC_THREADS) {
+                const int i = e % PW, c = e / PW;
+                sC[i][c] = (i < pw && c < qn) ? A12[i + (int64_t)c * ld] : Sx::zero();
+            }
+            __syncthreads();
+            if (!anyz) {
+                constexpr int NG = DC_CH / 16;
+                if (wid < NG) {
+                    const int g = wid, c = g * 16 + (lane & 15);
+                    typename M::acc_t acc0 = M::zero(), acc1 = M::zero();
+#pragma unroll
+                    for (int ks = 0; ks < PW; ks += M::KSTEP) {
+                        const int k = ks + (lane >> 4);
+                        const T bv = sC[k][c];
+                        M::step(acc0, sX[lane & 15][k], bv);
+                        if (PW > 16) M::step(acc1, sX[16 + (lane & 15)][k], bv);
+                    }
+                    // each wave owns its 16 columns of the chunk: no other wave reads them meanwhile
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int ii = M::row(lane, i), cc = g * 16 + (lane & 15);
+                        sC[ii][cc] = ii < pw ? M::get(acc0, i) : Sx::zero();
+                        if (PW > 16) sC[16 + ii][cc] = 16 + ii < pw ? M::get(acc1, i) : Sx::zero();
+                    }
+                }
+            } else {
+                for (int cc = tid; cc < qn; cc += DC_THREADS) { // column cc: L11 y = a
+                    for (int i = 0; i < PW; ++i) {
+                        T v = sC[i][cc];
+                        for (int k = 0; k < i; ++k) v = Sx::fms(v, sP[i][k], sC[k][cc]);
+                        sC[i][cc] = i < pw ? v : Sx::zero();
+                    }
+                }
+            }
+            __syncthreads();
+            for (int e = tid; e < pw * qn; e += DC_THREADS) {
+                const int i = e % pw, c = e / pw;
+                A12[i + (int64_t)c * ld] = sC[i][c];
+            }
+            // A22(:, chunk) -= L21 U12(:, chunk): 16 x 16 fragments over the waves
+            const int nf = (nbl + 15) / 16, nfc = (qn + 15) / 16, nff = nf * nfc;
+            T *A22 = A11 + pw + (int64_t)(pw + q0) * ld;
+            for (int f = wid; f < nff; f += NW) {
+                const int fr = f % nf, fc = f / nf;
+                T cv[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int r = fr * 16 + M::row(lane, i), c = fc * 16 + (lane & 15);
+                    cv[i] = (r < nbl && c < qn) ? A22[r + (int64_t)c * ld] : Sx::zero();
+                }
+                typename M::acc_t acc = M::zero();
+                const int r = fr * 16 + (lane & 15), c = fc * 16 + (lane & 15);
+#pragma unroll
+                for (int ks = 0; ks < PW; ks += M::KSTEP) {
+                    const int k = ks + (lane >> 4);
+                    const T av = (r < nbl) ? sP[pw + r][k] : Sx::zero();
+                    M::step(acc, av, sC[k][c]);
+                }
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int rr = fr * 16 + M::row(lane, i), cc = fc * 16 + (lane & 15);
+                    if (rr < nbl && cc < qn)
+                        A22[rr + (int64_t)cc * ld] = Sx::fms(cv[i], M::get(acc, i), one_of(cv[i]));
+                }
+            }
+            __syncthreads();
+        }
+        __syncthreads();
+    }
+}
+
 // Blocked TRSM with inverted PW x PW diagonal blocks, RB rows per workgroup:
 //   MODE 0 (L panel):  X := X U_kk^{-1}      (SRC/pdgstrf2.c:311,352 dtrsm R,U,N,N)
 //   MODE 1 (U panel):  Y := L_kk^{-1} Y as Y^T := Y^T (L_kk^T)^{-1}, rows of
