@@ -1260,6 +1260,10 @@ template <> struct BigCfg<double> {
 template <> struct BigCfg<zc> {
     static constexpr int THREADS = 512, WN = 2, MINW = 4, BN = 64, BK = 8, FN = 2, PASSW = 16;
 };
+// fp32: three workgroups per CU (6 waves per SIMD, <= 80 VGPRs; 42 KB LDS each)
+template <> struct BigCfg<float> {
+    static constexpr int THREADS = 512, WN = 2, MINW = 6, BN = 128, BK = 16, FN = 4, PASSW = 64;
+};
 constexpr int SB_BN = BigCfg<double>::BN;
 constexpr int SB_THREADS = 512; // the 512-thread configurations (k_schur_big<float>, <zc>)
 constexpr int SB_TB = 4; // epilogue tables: row blocks x column blocks per tile
