@@ -56,6 +56,22 @@ def log(msg):
     print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
+class _StdoutToStderr:
+    """Route fd 1 to fd 2 for the duration (gloo prints its connection
+    messages to stdout; the driver reads rank 0's stdout for the one JSON
+    line)."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+
+
 def grid_shape(n):
     return {1: (1, 1), 2: (1, 2), 4: (2, 2), 8: (2, 4), 16: (4, 4)}.get(n, (1, n))
 
@@ -253,11 +269,13 @@ def main():
         # system one libslu_mi355x.so links; the first loaded is shared.
         import torch
         import torch.distributed as dist
-        dist.init_process_group("gloo")
+        with _StdoutToStderr():
+            dist.init_process_group("gloo")
         if args.host_transport:
             sys.path.insert(0, os.path.join(ROOT, "tests"))
             from gridrun import GlooGrid
-            grid = GlooGrid(rank, pr, pc)
+            with _StdoutToStderr():
+                grid = GlooGrid(rank, pr, pc)
             local = 0
         else:
             buf = torch.zeros(128, dtype=torch.uint8)
