@@ -1,0 +1,575 @@
+// Column ordering post-pass and symbolic factorization:
+// the two serial steps pdgssvx runs between the column ordering and
+// pddistribute (SRC/pdgssvx.c:1046-1076):
+//
+//   sp_colorder  SRC/sp_colorder.c:81-221   etree of Pc(A'+A)Pc' (or the
+//                column etree of A Pc'), its postorder folded into perm_c,
+//                A's columns permuted to A Pc'
+//   symbfact     SRC/symbfact.c:81-215      supernodal symbolic LU without
+//                pivoting: relaxed leaf supernodes, per-column depth-first
+//                search over the pruned graph of L, fundamental supernode
+//                detection, symmetric pruning; L subscripts per supernode,
+//                U segments ("skeleton") per column
+//
+// Both give the reference's arrays exactly (tests/test_symbolic.py against
+// goldens of the reference run on the same inputs): the depth-first search
+// order decides the order of each supernode's L subscripts, and pddistribute
+// lays the factor blocks out in that order.
+#include <algorithm>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "common.h"
+#include "slu_abi.h"
+
+namespace slu {
+namespace symb {
+
+using I = int64_t;
+using std::vector;
+constexpr I NONE = -1;
+
+// ---------------------------------------------------------------- etree ---
+// Elimination tree of a symmetric pattern given column by column through
+// `cols(k, f)` calling f(i) for the (permuted) row indices of column k;
+// entries with i >= k are ignored (SRC/etree.c:156-200 uses the upper
+// triangle the same way).  The tree is unique; ancestor path compression
+// instead of the reference's disjoint sets.
+template <class Cols>
+static void etree_liu(I n, Cols cols, I *parent) {
+    vector<I> anc(n, NONE);
+    for (I k = 0; k < n; ++k) {
+        parent[k] = n;
+        cols(k, [&](I i) {
+            if (i >= k) return;
+            I r = i;
+            while (anc[r] != NONE && anc[r] != k) {
+                const I nx = anc[r];
+                anc[r] = k;
+                r = nx;
+            }
+            if (anc[r] == NONE) {
+                anc[r] = k;
+                parent[r] = k;
+            }
+        });
+    }
+}
+
+// Postorder of a forest given by parent pointers (roots point at n), children
+// visited in increasing order: post[v] = position of v (SRC/etree.c:393-430
+// returns the same inverse numbering).  post has n + 1 entries, post[n] = n.
+static vector<I> postorder(I n, const I *parent) {
+    vector<I> head(n + 1, NONE), next(n + 1, NONE), post(n + 1, 0), stack;
+    for (I v = n - 1; v >= 0; --v) {
+        next[v] = head[parent[v]];
+        head[parent[v]] = v;
+    }
+    I num = 0;
+    stack.reserve(64);
+    stack.push_back(n);
+    while (!stack.empty()) {
+        const I v = stack.back();
+        if (head[v] != NONE) {
+            const I c = head[v];
+            head[v] = next[c]; // next child of v on the next visit
+            stack.push_back(c);
+        } else {
+            post[v] = num++;
+            stack.pop_back();
+        }
+    }
+    return post;
+}
+
+// sp_colorder (SRC/sp_colorder.c:81-221).  colbeg / colend receive A Pc''s
+// column pointers; with recompute (Fact = DOFACT or SamePattern) the etree
+// is recomputed and perm_c / etree / colbeg / colend follow its postorder.
+static void colorder(I m, I n, const I *colptr, const I *rowind, bool ata, bool recompute,
+                     I *perm_c, I *etree, I *colbeg, I *colend) {
+    for (I i = 0; i < n; ++i) {
+        colbeg[perm_c[i]] = colptr[i];
+        colend[perm_c[i]] = colptr[i + 1];
+    }
+    if (!recompute) return;
+    if (m != n || ata) {
+        // column etree of A Pc' (SRC/etree.c:223-286): row r's edges replaced
+        // by a star centred at its first column
+        vector<I> first(m, n);
+        for (I c = 0; c < n; ++c)
+            for (I p = colbeg[c]; p < colend[c]; ++p) first[rowind[p]] = std::min(first[rowind[p]], c);
+        etree_liu(n, [&](I k, auto f) {
+            for (I p = colbeg[k]; p < colend[k]; ++p) f(first[rowind[p]]);
+        }, etree);
+    } else {
+        // etree of Pc (A' + A) Pc': column k of the sum = column c = iperm[k]
+        // of A and row c of A (A' column c), both relabelled by perm_c
+        vector<I> iperm(n), tptr(n + 1, 0), tind(colptr[n]);
+        for (I i = 0; i < n; ++i) iperm[perm_c[i]] = i;
+        for (I p = 0; p < colptr[n]; ++p) tptr[rowind[p] + 1]++;
+        for (I r = 0; r < n; ++r) tptr[r + 1] += tptr[r];
+        {
+            vector<I> at(tptr.begin(), tptr.end() - 1);
+            for (I c = 0; c < n; ++c)
+                for (I p = colptr[c]; p < colptr[c + 1]; ++p) tind[at[rowind[p]]++] = c;
+        }
+        etree_liu(n, [&](I k, auto f) {
+            const I c = iperm[k];
+            for (I p = colptr[c]; p < colptr[c + 1]; ++p) f(perm_c[rowind[p]]);
+            for (I p = tptr[c]; p < tptr[c + 1]; ++p) f(perm_c[tind[p]]);
+        }, etree);
+    }
+    const vector<I> post = postorder(n, etree);
+    vector<I> w(n);
+    for (I i = 0; i < n; ++i) w[post[i]] = post[etree[i]];
+    std::copy(w.begin(), w.end(), etree);
+    for (I i = 0; i < n; ++i) w[post[i]] = colbeg[i];
+    std::copy(w.begin(), w.end(), colbeg);
+    for (I i = 0; i < n; ++i) w[post[i]] = colend[i];
+    std::copy(w.begin(), w.end(), colend);
+    for (I i = 0; i < n; ++i) perm_c[i] = post[perm_c[i]];
+}
+
+// ------------------------------------------------------------ symbfact ---
+// Last column of the relaxed supernode starting at each column, NONE
+// elsewhere: maximal subtrees of the postordered etree with fewer than
+// `relax` descendants (SRC/symbfact.c:227-271).
+static vector<I> relaxed_ends(I n, const I *et, I relax) {
+    vector<I> desc(n + 1, 0), end(n, NONE);
+    for (I j = 0; j < n; ++j)
+        if (et[j] != n) desc[et[j]] += desc[j] + 1;
+    for (I j = 0; j < n;) {
+        const I f = j;
+        while (et[j] != n && desc[et[j]] < relax) j = et[j];
+        end[f] = j;
+        ++j;
+        while (j < n && desc[j] != 0) ++j;
+    }
+    return end;
+}
+
+struct Result {
+    I n = 0;
+    vector<I> xsup, supno, xlsub, lsub, xusub, usub;
+    I nnzL = 0, nnzU = 0, nnzLU = 0, lsub_size = 0;
+};
+
+// The symbolic factorization state: the reference's Glu_persist /
+// Glu_freeable arrays and its work arrays (SRC/symbfact.c:115-131).
+struct Walker {
+    // input: A Pc' with rows relabelled by perm_c (NCP)
+    const I *cb, *ce, *ri;
+    I maxsuper;
+    I *xsup, *supno, *xlsub, *xusub, *xprune, *perm_r;
+    I *marker, *repfnz, *parent, *xplore, *segrep;
+    vector<I> lsub, usub;
+    I nextu = 0;
+
+    void lput(I at, I v) {
+        if (at >= (I)lsub.size()) lsub.resize(std::max<I>(2 * lsub.size(), at + 1024));
+        lsub[at] = v;
+    }
+
+    // relaxed supernode j..k: union of the columns' row structures, a copy
+    // of it for pruning when k > j (SRC/symbfact.c:291-370)
+    void relaxed(I j, I k) {
+        const I ns = ++supno[j];
+        I nextl = xlsub[j];
+        for (I i = j; i <= k; ++i) {
+            for (I p = cb[i]; p < ce[i]; ++p) {
+                const I r = ri[p];
+                if (marker[r] != k) {
+                    marker[r] = k;
+                    lput(nextl++, r);
+                }
+            }
+            supno[i] = ns;
+            xusub[i + 1] = nextu;
+        }
+        if (j < k) {
+            I to = nextl;
+            for (I f = xlsub[j]; f < nextl; ++f) lput(to++, lsub[f]);
+            for (I i = j + 1; i <= k; ++i) xlsub[i] = nextl;
+            nextl = to;
+        }
+        xsup[ns + 1] = k + 1;
+        supno[k + 1] = ns;
+        xprune[k] = nextl;
+        xlsub[k + 1] = nextl;
+    }
+
+    // depth-first search of column j over the pruned graph; returns the
+    // number of U segments (representatives in segrep, in the order the
+    // search finishes them) and decides whether j extends j-1's supernode
+    // (SRC/symbfact.c:458-671)
+    I column(I j) {
+        I ns = supno[j], js = ns, nextl = xlsub[j], nseg = 0;
+        for (I p = cb[j]; p < ce[j]; ++p) {
+            const I r = ri[p], km = marker[r];
+            if (km == j) continue;
+            marker[r] = j;
+            if (perm_r[r] == NONE) { // row below the diagonal: in L(:, j)
+                lput(nextl++, r);
+                if (km != j - 1) js = NONE;
+                continue;
+            }
+            const I kp = perm_r[r];
+            I rep = xsup[supno[kp] + 1] - 1;
+            if (repfnz[rep] != NONE) {
+                if (kp < repfnz[rep]) repfnz[rep] = kp;
+                continue;
+            }
+            parent[rep] = NONE;
+            repfnz[rep] = kp;
+            I x = xlsub[rep], xe = xprune[rep];
+            for (;;) {
+                while (x < xe) {
+                    const I c = lsub[x++], cm = marker[c];
+                    if (cm == j) continue;
+                    marker[c] = j;
+                    const I cp = perm_r[c];
+                    if (cp == NONE) {
+                        lput(nextl++, c);
+                        if (cm != j - 1) js = NONE;
+                        continue;
+                    }
+                    const I crep = xsup[supno[cp] + 1] - 1;
+                    if (repfnz[crep] != NONE) {
+                        if (cp < repfnz[crep]) repfnz[crep] = cp;
+                        continue;
+                    }
+                    xplore[rep] = x; // descend
+                    parent[crep] = rep;
+                    rep = crep;
+                    repfnz[rep] = cp;
+                    x = xlsub[rep];
+                    xe = xprune[rep];
+                }
+                segrep[nseg++] = rep; // finished: back to the parent
+                const I up = parent[rep];
+                if (up == NONE) break;
+                rep = up;
+                x = xplore[rep];
+                xe = xprune[rep];
+            }
+        }
+        if (j == 0) {
+            ns = supno[0] = 0;
+        } else {
+            const I fs = xsup[ns], jp = xlsub[j], jm1p = xlsub[j - 1];
+            // fundamental supernodes: |L(:,j)| = |L(:,j-1)| - 1 besides the
+            // subset test (T2_SUPER, SRC/symbfact.c:39,633-635), and at most
+            // maxsuper columns
+            if (nextl - jp != jp - jm1p - 1) js = NONE;
+            if (j - fs >= maxsuper) js = NONE;
+            if (js == NONE) {
+                if (fs < j - 2) { // >= 3 columns: keep only the first and last lists
+                    I to = xlsub[fs + 1];
+                    xlsub[j - 1] = to;
+                    const I stop = to + jp - jm1p;
+                    xprune[j - 1] = stop;
+                    xlsub[j] = stop;
+                    for (I f = jm1p; f < nextl; ++f, ++to) lsub[to] = lsub[f];
+                    nextl = to;
+                }
+                ++ns;
+                supno[j] = ns;
+            }
+        }
+        xsup[ns + 1] = j + 1;
+        supno[j + 1] = ns;
+        xprune[j] = nextl;
+        xlsub[j + 1] = nextl;
+        return nseg;
+    }
+
+    // U segments of column j, in topological order (SRC/symbfact.c:763-820)
+    void set_usub(I j, I nseg) {
+        const I js = supno[j];
+        for (I s = nseg - 1; s >= 0; --s) {
+            const I rep = segrep[s];
+            if (supno[rep] == js || repfnz[rep] == NONE) continue;
+            if (nextu >= (I)usub.size()) usub.resize(std::max<I>(2 * usub.size(), nextu + 1024));
+            usub[nextu++] = repfnz[rep];
+        }
+        xusub[j + 1] = nextu;
+    }
+
+    // diagonal row of column j to position j - fsupc of its supernode's
+    // first list; pivots are diagonal (SRC/symbfact.c:684-742)
+    void pivot(I j) {
+        const I fs = xsup[supno[j]], lp = xlsub[fs], nr = xlsub[fs + 1] - lp, d0 = j - fs;
+        I d = NONE;
+        for (I s = d0; s < nr; ++s)
+            if (lsub[lp + s] == j) {
+                d = s;
+                break;
+            }
+        if (d == NONE) throw Error("symbfact: zero diagonal at column " + std::to_string(j));
+        perm_r[j] = j;
+        if (d != d0) std::swap(lsub[lp + d], lsub[lp + d0]);
+    }
+
+    // symmetric pruning of the supernodes column j's search reached
+    // (SRC/symbfact.c:824-906)
+    void prune(I j, I nseg) {
+        const I js = supno[j];
+        for (I s = 0; s < nseg; ++s) {
+            const I rep = segrep[s];
+            if (repfnz[rep] == NONE || supno[rep] == js) continue;
+            if (xprune[rep] < xlsub[rep + 1]) continue; // pruned before
+            I lo = xlsub[rep], hi = xlsub[rep + 1] - 1;
+            bool hit = false;
+            for (I q = lo; q <= hi; ++q)
+                if (lsub[q] == j) {
+                    hit = true;
+                    break;
+                }
+            if (!hit) continue;
+            while (lo <= hi) {
+                if (perm_r[lsub[hi]] == NONE)
+                    --hi;
+                else if (perm_r[lsub[lo]] != NONE)
+                    ++lo;
+                else {
+                    std::swap(lsub[lo], lsub[hi]);
+                    ++lo;
+                    --hi;
+                }
+            }
+            xprune[rep] = lo;
+        }
+    }
+
+    // columns [a, b) with the relaxed supernode ends `rend`
+    void run(I a, I b, const I *rend) {
+        for (I j = a; j < b;) {
+            if (rend[j] != NONE) {
+                const I k = rend[j];
+                relaxed(j, k);
+                for (I i = j; i <= k; ++i) pivot(i);
+                j = k + 1;
+            } else {
+                const I nseg = column(j);
+                set_usub(j, nseg);
+                pivot(j);
+                prune(j, nseg);
+                for (I s = 0; s < nseg; ++s) repfnz[segrep[s]] = NONE;
+                ++j;
+            }
+        }
+    }
+};
+
+// symbfact (SRC/symbfact.c:81-215).  m x n matrix, columns [cb[j], ce[j])
+// of ri (A Pc', rows relabelled by perm_c); etree postordered.
+static Result symbfact(I m, I n, const I *cb, const I *ce, const I *ri, const I *etree, I relax,
+                       I maxsuper) {
+    Result R;
+    R.n = n;
+    const I mn = std::min(m, n);
+    R.xsup.assign(n + 2, 0);
+    R.supno.assign(n + 1, 0);
+    R.xlsub.assign(n + 1, 0);
+    R.xusub.assign(n + 1, 0);
+    vector<I> xprune(n, 0), perm_r(m, NONE), marker(m, NONE), repfnz(m, NONE), parent(m, 0),
+        xplore(m, 0), segrep(m, 0);
+    R.supno[0] = NONE;
+    const vector<I> rend = relaxed_ends(n, etree, relax);
+
+    Walker w;
+    w.cb = cb;
+    w.ce = ce;
+    w.ri = ri;
+    w.maxsuper = maxsuper;
+    w.xsup = R.xsup.data();
+    w.supno = R.supno.data();
+    w.xlsub = R.xlsub.data();
+    w.xusub = R.xusub.data();
+    w.xprune = xprune.data();
+    w.perm_r = perm_r.data();
+    w.marker = marker.data();
+    w.repfnz = repfnz.data();
+    w.parent = parent.data();
+    w.xplore = xplore.data();
+    w.segrep = segrep.data();
+    I annz = 0;
+    for (I c = 0; c < n; ++c) annz += ce[c] - cb[c];
+    w.lsub.resize(std::max<I>(4 * annz, 1024));
+    w.usub.resize(std::max<I>(annz, 1024));
+    w.run(0, mn, rend.data());
+    R.lsub = std::move(w.lsub);
+    R.usub = std::move(w.usub);
+    R.usub.resize(R.xusub[mn]);
+
+    // ---- counts (SRC/util.c:95-152) and the final L subscripts: the first
+    // column's list of each supernode, in supernode order (SRC/util.c:163-199)
+    const I nsup = R.supno[n];
+    for (I s = 0; s <= nsup; ++s) {
+        const I f = R.xsup[s];
+        I len = R.xlsub[f + 1] - R.xlsub[f];
+        for (I c = f; c < R.xsup[s + 1]; ++c) {
+            R.nnzL += len;
+            R.nnzU += c - f + 1;
+            --len;
+        }
+    }
+    for (I c = 0; c < n; ++c)
+        for (I p = R.xusub[c]; p < R.xusub[c + 1]; ++p) {
+            const I f = R.usub[p];
+            R.nnzU += R.xsup[R.supno[f] + 1] - f;
+        }
+    R.nnzLU = R.nnzL + R.nnzU - mn;
+    if (n > 1) {
+        R.lsub_size = R.xlsub[n];
+        I out = 0;
+        for (I s = 0; s <= nsup; ++s) {
+            const I f = R.xsup[s], a = R.xlsub[f], b = R.xlsub[f + 1];
+            R.xlsub[f] = out;
+            for (I p = a; p < b; ++p) R.lsub[out++] = perm_r[R.lsub[p]];
+            for (I c = f + 1; c < R.xsup[s + 1]; ++c) R.xlsub[c] = out;
+        }
+        R.xlsub[n] = out;
+    }
+    R.lsub.resize(R.xlsub[n]);
+    return R;
+}
+
+// sp_ienv_dist(2) / (3) (SRC/sp_ienv.c:85-112): environment first, then
+// the options; relax not above maxsup
+static I env_or(const char *a, const char *b, I dflt, bool cap) {
+    const char *s = getenv(a);
+    if (!s) s = getenv(b);
+    if (!s) return dflt;
+    const I k = atoi(s);
+    return cap ? std::min<I>(k, 512) : k; // MAX_SUPER_SIZE, SRC/superlu_defs.h:139
+}
+static I maxsup_of(const superlu_dist_options_t *o) {
+    return env_or("SUPERLU_MAXSUP", "NSUP", o->superlu_maxsup, true);
+}
+static I relax_of(const superlu_dist_options_t *o) {
+    return std::min(env_or("SUPERLU_RELAX", "NREL", o->superlu_relax, false), maxsup_of(o));
+}
+
+template <class T>
+static T *copy_out(const vector<I> &v, size_t n) {
+    T *p = (T *)malloc(std::max<size_t>(n, 1) * sizeof(T));
+    if (!p) throw Error("symbfact: out of host memory");
+    if (n) memcpy(p, v.data(), n * sizeof(T));
+    return p;
+}
+
+} // namespace symb
+} // namespace slu
+
+using namespace slu::symb;
+
+extern "C" {
+
+int slu_colorder(int64_t m, int64_t n, const int64_t *colptr, const int64_t *rowind, int ata,
+                 int recompute, int64_t *perm_c, int64_t *etree, int64_t *colbeg, int64_t *colend) {
+    try {
+        colorder(m, n, colptr, rowind, ata != 0, recompute != 0, perm_c, etree, colbeg, colend);
+        return 0;
+    } catch (const std::exception &e) {
+        slu::set_last_error(e.what());
+        return -1;
+    }
+}
+
+void *slu_symbfact(int64_t m, int64_t n, const int64_t *colbeg, const int64_t *colend,
+                   const int64_t *rowind, const int64_t *etree, int64_t relax, int64_t maxsuper) {
+    try {
+        return new Result(symbfact(m, n, colbeg, colend, rowind, etree, relax, maxsuper));
+    } catch (const std::exception &e) {
+        slu::set_last_error(e.what());
+        return nullptr;
+    }
+}
+
+void slu_symbfact_sizes(const void *h, int64_t *out) {
+    const Result &R = *(const Result *)h;
+    out[0] = R.n ? R.supno[R.n] + 1 : 0;
+    out[1] = (int64_t)R.lsub.size();
+    out[2] = (int64_t)R.usub.size();
+    out[3] = R.nnzL;
+    out[4] = R.nnzU;
+    out[5] = R.nnzLU;
+    out[6] = R.lsub_size;
+}
+
+void slu_symbfact_arrays(const void *h, int64_t *xsup, int64_t *supno, int64_t *xlsub,
+                         int64_t *lsub, int64_t *xusub, int64_t *usub) {
+    const Result &R = *(const Result *)h;
+    const size_t n1 = R.n + 1;
+    memcpy(xsup, R.xsup.data(), n1 * sizeof(int64_t));
+    memcpy(supno, R.supno.data(), n1 * sizeof(int64_t));
+    memcpy(xlsub, R.xlsub.data(), n1 * sizeof(int64_t));
+    memcpy(xusub, R.xusub.data(), n1 * sizeof(int64_t));
+    if (!R.lsub.empty()) memcpy(lsub, R.lsub.data(), R.lsub.size() * sizeof(int64_t));
+    if (!R.usub.empty()) memcpy(usub, R.usub.data(), R.usub.size() * sizeof(int64_t));
+}
+
+void slu_symbfact_free(void *h) { delete (Result *)h; }
+
+// ---- drop-in entry points with the reference's prototypes
+
+// SRC/sp_colorder.c:81 (prototype SRC/superlu_defs.h).  AC's store and its
+// colbeg / colend are malloc'ed as in the reference; rowind / nzval shared
+// with A.
+void sp_colorder(superlu_dist_options_t *options, SuperMatrix *A, int_t *perm_c, int_t *etree,
+                 SuperMatrix *AC) {
+    const NCformat *As = (const NCformat *)A->Store;
+    const I n = A->ncol;
+    NCPformat *S = (NCPformat *)malloc(sizeof(NCPformat));
+    S->nnz = As->nnz;
+    S->nzval = As->nzval;
+    S->rowind = As->rowind;
+    S->colbeg = (int_t *)malloc(std::max<I>(n, 1) * sizeof(int_t));
+    S->colend = (int_t *)malloc(std::max<I>(n, 1) * sizeof(int_t));
+    AC->Stype = SLU_NCP;
+    AC->Dtype = A->Dtype;
+    AC->Mtype = A->Mtype;
+    AC->nrow = A->nrow;
+    AC->ncol = A->ncol;
+    AC->Store = S;
+    const bool recompute = options->Fact == SLU_DOFACT || options->Fact == SLU_SAMEPATTERN;
+    colorder(A->nrow, n, As->colptr, As->rowind, options->ColPerm == SLU_MMD_ATA, recompute, perm_c,
+             etree, S->colbeg, S->colend);
+}
+
+// SRC/symbfact.c:81: returns -(the reference's lsub size), 0 for n <= 1.
+// Glu_persist->xsup / supno and the Glu_freeable arrays are malloc'ed
+// (freed by the reference's symbfact_SubFree / LU destructors with free()).
+int_t symbfact(superlu_dist_options_t *options, int pnum, SuperMatrix *A, int_t *perm_c,
+               int_t *etree, Glu_persist_t *Glu_persist, Glu_freeable_t *Glu_freeable) {
+    (void)pnum;
+    (void)perm_c;
+    const NCPformat *S = (const NCPformat *)A->Store;
+    try {
+        const Result R = symbfact(A->nrow, A->ncol, S->colbeg, S->colend, S->rowind, etree,
+                                  relax_of(options), maxsup_of(options));
+        const size_t n1 = A->ncol + 1;
+        Glu_persist->xsup = copy_out<int_t>(R.xsup, n1);
+        Glu_persist->supno = copy_out<int_t>(R.supno, n1);
+        Glu_freeable->xlsub = copy_out<int_t>(R.xlsub, n1);
+        Glu_freeable->xusub = copy_out<int_t>(R.xusub, n1);
+        Glu_freeable->lsub = copy_out<int_t>(R.lsub, R.lsub.size());
+        Glu_freeable->usub = copy_out<int_t>(R.usub, R.usub.size());
+        Glu_freeable->nzlmax = std::max<I>((I)R.lsub.size(), 1);
+        Glu_freeable->nzumax = std::max<I>((I)R.usub.size(), 1);
+        Glu_freeable->MemModel = 0; // SYSTEM
+        Glu_freeable->nnzLU = R.nnzLU;
+        return -R.lsub_size;
+    } catch (const std::exception &e) {
+        // the reference ABORTs here (SRC/symbfact.c:724-727)
+        fprintf(stderr, "symbfact: %s\n", e.what());
+        abort();
+    }
+}
+
+} // extern "C"

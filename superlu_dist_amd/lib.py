@@ -88,6 +88,13 @@ def lib():
         "slu_csc_create": (C.POINTER(SluCsc), [C.c_int64, C.c_int64, c_i64p, c_i64p, P, C.c_int]),
         "slu_csc_free": (None, [C.POINTER(SluCsc)]),
         "slu_order_nd_grid": (C.c_int, [C.c_int, C.c_int, C.c_int, c_i64p]),
+        "slu_colorder": (C.c_int, [C.c_int64, C.c_int64, c_i64p, c_i64p, C.c_int, C.c_int,
+                                   c_i64p, c_i64p, c_i64p, c_i64p]),
+        "slu_symbfact": (P, [C.c_int64, C.c_int64, c_i64p, c_i64p, c_i64p, c_i64p, C.c_int64,
+                             C.c_int64]),
+        "slu_symbfact_sizes": (None, [P, c_i64p]),
+        "slu_symbfact_arrays": (None, [P, c_i64p, c_i64p, c_i64p, c_i64p, c_i64p, c_i64p]),
+        "slu_symbfact_free": (None, [P]),
         "slu_symbolic": (P, [C.POINTER(SluCsc), c_i64p, C.c_int, C.c_int]),
         "slu_symb_free": (None, [P]),
         "slu_symb_nsupers": (C.c_int64, [P]),

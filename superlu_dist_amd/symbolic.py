@@ -1,0 +1,101 @@
+"""Column ordering post-pass and symbolic factorization,
+mirroring the reference's functions of the same names:
+
+* ``sp_colorder`` -- SRC/sp_colorder.c:81-221: etree of Pc(A'+A)Pc' (or
+  the column etree of A Pc' for MMD_ATA / rectangular A), postorder folded
+  into perm_c, column pointers of A Pc'.
+* ``symbfact`` -- SRC/symbfact.c:81-215 on A Pc' with rows relabelled by
+  perm_c (pdgssvx does the relabelling, SRC/pdgssvx.c:1048-1058): supernode
+  partition, L subscripts per supernode, U segments per column.
+
+Both run the C++ code in ``csrc/symbolic.cpp`` (host code: the symbolic
+factorization is integer graph search on the host cores, sized by nnz(A)),
+the same code the drop-in ``sp_colorder`` / ``symbfact`` symbols of
+libslu_mi355x.so run for the reference's pdgssvx.
+"""
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from .lib import as_i64p, lib
+
+NATURAL, MMD_ATA, MMD_AT_PLUS_A, MY_PERMC = 0, 1, 2, 7
+
+
+def last_error():
+    e = lib().slu_last_error()
+    return e.decode() if e else "unknown error"
+
+
+@dataclass
+class ColOrder:
+    perm_c: np.ndarray  # postordered column permutation (perm_c[i] = new position of column i)
+    etree: np.ndarray   # postordered etree, roots = n
+    colbeg: np.ndarray  # A Pc' column j = rowind[colbeg[j]:colend[j]]
+    colend: np.ndarray
+
+
+def sp_colorder(m, n, colptr, rowind, perm_c, colperm=MMD_AT_PLUS_A, fact_dofact=True):
+    colptr = np.ascontiguousarray(colptr, np.int64)
+    rowind = np.ascontiguousarray(rowind, np.int64)
+    pc = np.array(perm_c, np.int64)
+    et = np.zeros(n, np.int64)
+    cb = np.zeros(n, np.int64)
+    ce = np.zeros(n, np.int64)
+    if lib().slu_colorder(m, n, as_i64p(colptr), as_i64p(rowind), int(colperm == MMD_ATA),
+                          int(fact_dofact), as_i64p(pc), as_i64p(et), as_i64p(cb), as_i64p(ce)):
+        raise RuntimeError(last_error())
+    return ColOrder(pc, et, cb, ce)
+
+
+@dataclass
+class Symb:
+    xsup: np.ndarray
+    supno: np.ndarray
+    xlsub: np.ndarray
+    lsub: np.ndarray
+    xusub: np.ndarray
+    usub: np.ndarray
+    nnzL: int
+    nnzU: int
+    nnzLU: int
+    ret: int  # symbfact's return value: -(lsub size before compression)
+
+    @property
+    def nsupers(self):
+        return len(self.xsup) - 1
+
+
+def symbfact(m, n, colbeg, colend, rowind, etree, relax, maxsuper):
+    """rowind: A Pc''s row indices already relabelled by perm_c."""
+    cb = np.ascontiguousarray(colbeg, np.int64)
+    ce = np.ascontiguousarray(colend, np.int64)
+    ri = np.ascontiguousarray(rowind, np.int64)
+    et = np.ascontiguousarray(etree, np.int64)
+    L = lib()
+    h = L.slu_symbfact(m, n, as_i64p(cb), as_i64p(ce), as_i64p(ri), as_i64p(et), relax, maxsuper)
+    if not h:
+        raise RuntimeError(last_error())
+    try:
+        sz = np.zeros(7, np.int64)
+        L.slu_symbfact_sizes(h, as_i64p(sz))
+        ns, nl, nu = int(sz[0]), int(sz[1]), int(sz[2])
+        xsup = np.zeros(n + 1, np.int64)
+        supno = np.zeros(n + 1, np.int64)
+        xlsub = np.zeros(n + 1, np.int64)
+        xusub = np.zeros(n + 1, np.int64)
+        lsub = np.zeros(max(nl, 1), np.int64)
+        usub = np.zeros(max(nu, 1), np.int64)
+        L.slu_symbfact_arrays(h, as_i64p(xsup), as_i64p(supno), as_i64p(xlsub), as_i64p(lsub),
+                              as_i64p(xusub), as_i64p(usub))
+    finally:
+        L.slu_symbfact_free(h)
+    return Symb(xsup[:ns + 1], supno, xlsub, lsub[:nl], xusub, usub[:nu], int(sz[3]),
+                int(sz[4]), int(sz[5]), -int(sz[6]))
+
+
+def relabel_rows(rowind, perm_c):
+    """pdgssvx's Pc relabelling of A Pc''s rows (SRC/pdgssvx.c:1053-1058);
+    every entry of A lies in one column of A Pc', so all are relabelled."""
+    return np.asarray(perm_c, np.int64)[np.asarray(rowind, np.int64)]
