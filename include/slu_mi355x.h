@@ -14,6 +14,10 @@
  *        exported because the reference's pdgstrf.c.o defines them
  *        (SRC/pdgstrf.c:171 #includes SRC/dscatter.c) and dscatter3d.c.o
  *        still references them after pdgstrf.c.o is removed.
+ *      sp_colorder -- SRC/superlu_defs.h:1079, implemented at SRC/sp_colorder.c:81
+ *      symbfact    -- SRC/superlu_defs.h:1091, implemented at SRC/symbfact.c:81
+ *        (the column ordering post-pass and symbolic factorization pdgssvx
+ *        runs before pddistribute; declared with group 3 below)
  *    On multi-rank grids pdgstrf uses the MPI communicators in gridinfo_t to
  *    bootstrap RCCL (or, when ranks share a GPU, to carry the host-staged
  *    panel broadcasts) and for the final info reduction; the MPI symbols are
@@ -282,6 +286,43 @@ void slu_symb_arrays(const slu_symb *s, int64_t *xsup, int64_t *supno,
 void slu_symb_counts(const slu_symb *s, double *nnzL, double *nnzU);
 /* |struct(L_s)| (rows incl. the diagonal block) per supernode */
 void slu_symb_struct_sizes(const slu_symb *s, int64_t *sizes);
+
+/* ---- Column ordering post-pass + symbolic factorization,
+ * the reference's arrays bit for bit (csrc/symbolic.cpp, tests/test_symbolic.py).
+ *
+ * slu_colorder replaces sp_colorder (SRC/sp_colorder.c:81): colbeg / colend
+ * (n each) get A Pc''s column pointers; with recompute (Fact = DOFACT or
+ * SamePattern) etree (n) gets the etree of Pc(A'+A)Pc' (ata != 0 or m != n:
+ * the column etree of A Pc'), postordered, and perm_c follows the postorder.
+ * Returns 0, or -1 (slu_last_error). */
+int slu_colorder(int64_t m, int64_t n, const int64_t *colptr, const int64_t *rowind, int ata,
+                 int recompute, int64_t *perm_c, int64_t *etree, int64_t *colbeg,
+                 int64_t *colend);
+/* slu_symbfact replaces symbfact (SRC/symbfact.c:81) on A Pc' (colbeg / colend
+ * from slu_colorder, rowind relabelled by perm_c as SRC/pdgssvx.c:1053-1058
+ * does) with the postordered etree.  NULL on a structurally zero diagonal
+ * (the reference ABORTs).  sizes: [nsupers, |lsub|, |usub|, nnzL, nnzU,
+ * nnzLU, lsub size before compression (symbfact returns its negative)]. */
+void *slu_symbfact(int64_t m, int64_t n, const int64_t *colbeg, const int64_t *colend,
+                   const int64_t *rowind, const int64_t *etree, int64_t relax,
+                   int64_t maxsuper);
+void slu_symbfact_sizes(const void *h, int64_t *sizes);
+/* xsup (nsupers+1 of n+1 written), supno / xlsub / xusub (n+1), lsub, usub */
+void slu_symbfact_arrays(const void *h, int64_t *xsup, int64_t *supno, int64_t *xlsub,
+                         int64_t *lsub, int64_t *xusub, int64_t *usub);
+void slu_symbfact_free(void *h);
+/* Drop-in: the reference's own prototypes (SRC/superlu_defs.h:1079, 1091;
+ * types in slu_abi.h).  A program linked against libslu_mi355x.so ahead of
+ * the reference archive runs these in pdgssvx (SRC/pdgssvx.c:1046, 1075).
+ * sp_colorder replaces SRC/sp_colorder.c:81 (AC's store and colbeg / colend
+ * malloc'ed, rowind / nzval shared with A); symbfact replaces
+ * SRC/symbfact.c:81 (xsup / supno and the Glu_freeable arrays malloc'ed,
+ * freed by the reference's symbfact_SubFree / LU destructors), returning
+ * -(lsub size) as the reference does. */
+void sp_colorder(superlu_dist_options_t *options, SuperMatrix *A, int_t *perm_c,
+                 int_t *etree, SuperMatrix *AC);
+int_t symbfact(superlu_dist_options_t *options, int pnum, SuperMatrix *A, int_t *perm_c,
+               int_t *etree, Glu_persist_t *Glu_persist, Glu_freeable_t *Glu_freeable);
 
 /* Build this rank's LUstruct (dtype-typed dLUstruct_t/sLUstruct_t/zLUstruct_t
  * allocated by the library) holding P*A*P^T in the layout of

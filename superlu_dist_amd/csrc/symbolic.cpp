@@ -159,17 +159,30 @@ struct Result {
 };
 
 // The symbolic factorization state: the reference's Glu_persist /
-// Glu_freeable arrays and its work arrays (SRC/symbfact.c:115-131).
+// Glu_freeable arrays and its work arrays (SRC/symbfact.c:115-131).  Row and
+// column indices in T (int32 when n fits: the search is bound by random
+// accesses into marker / supno / lsub), positions in lsub / usub in I.
+// Pivots are diagonal (pivotL, SRC/symbfact.c:729-731), so the reference's
+// perm_r is the identity on the columns done so far: "row r pivoted" is
+// r < j while column j is searched, r <= j while it prunes.
+template <class T>
 struct Walker {
     // input: A Pc' with rows relabelled by perm_c (NCP)
-    const I *cb, *ce, *ri;
+    const I *cb, *ce;
+    const T *ri;
     I maxsuper;
-    I *xsup, *supno, *xlsub, *xusub, *xprune, *perm_r;
-    I *marker, *repfnz, *parent, *xplore, *segrep;
-    vector<I> lsub, usub;
+    vector<T> xsup, supno, marker, repfnz, parent, segrep, lsub, usub;
+    vector<I> xlsub, xusub, xprune, xplore;
     I nextu = 0;
 
-    void lput(I at, I v) {
+    Walker(I m, I n, I cap) : xsup(n + 2, 0), supno(n + 1, 0), marker(m, (T)NONE),
+                              repfnz(m, (T)NONE), parent(m, 0), segrep(m, 0), lsub(cap),
+                              usub(cap / 2 + 1024), xlsub(n + 1, 0), xusub(n + 1, 0),
+                              xprune(n, 0), xplore(m, 0) {
+        supno[0] = (T)NONE;
+    }
+
+    void lput(I at, T v) {
         if (at >= (I)lsub.size()) lsub.resize(std::max<I>(2 * lsub.size(), at + 1024));
         lsub[at] = v;
     }
@@ -177,13 +190,13 @@ struct Walker {
     // relaxed supernode j..k: union of the columns' row structures, a copy
     // of it for pruning when k > j (SRC/symbfact.c:291-370)
     void relaxed(I j, I k) {
-        const I ns = ++supno[j];
+        const T ns = ++supno[j];
         I nextl = xlsub[j];
         for (I i = j; i <= k; ++i) {
             for (I p = cb[i]; p < ce[i]; ++p) {
-                const I r = ri[p];
-                if (marker[r] != k) {
-                    marker[r] = k;
+                const T r = ri[p];
+                if (marker[r] != (T)k) {
+                    marker[r] = (T)k;
                     lput(nextl++, r);
                 }
             }
@@ -196,7 +209,7 @@ struct Walker {
             for (I i = j + 1; i <= k; ++i) xlsub[i] = nextl;
             nextl = to;
         }
-        xsup[ns + 1] = k + 1;
+        xsup[ns + 1] = (T)(k + 1);
         supno[k + 1] = ns;
         xprune[k] = nextl;
         xlsub[k + 1] = nextl;
@@ -207,51 +220,51 @@ struct Walker {
     // search finishes them) and decides whether j extends j-1's supernode
     // (SRC/symbfact.c:458-671)
     I column(I j) {
-        I ns = supno[j], js = ns, nextl = xlsub[j], nseg = 0;
+        const T tj = (T)j, tj1 = (T)(j - 1);
+        I ns = supno[j], nextl = xlsub[j], nseg = 0;
+        bool js = true; // j joins j-1's supernode
         for (I p = cb[j]; p < ce[j]; ++p) {
-            const I r = ri[p], km = marker[r];
-            if (km == j) continue;
-            marker[r] = j;
-            if (perm_r[r] == NONE) { // row below the diagonal: in L(:, j)
+            const T r = ri[p], km = marker[r];
+            if (km == tj) continue;
+            marker[r] = tj;
+            if (r >= tj) { // row not pivoted yet: in L(:, j)
                 lput(nextl++, r);
-                if (km != j - 1) js = NONE;
+                if (km != tj1) js = false;
                 continue;
             }
-            const I kp = perm_r[r];
-            I rep = xsup[supno[kp] + 1] - 1;
-            if (repfnz[rep] != NONE) {
-                if (kp < repfnz[rep]) repfnz[rep] = kp;
+            T rep = xsup[supno[r] + 1] - 1;
+            if (repfnz[rep] != (T)NONE) {
+                if (r < repfnz[rep]) repfnz[rep] = r;
                 continue;
             }
-            parent[rep] = NONE;
-            repfnz[rep] = kp;
+            parent[rep] = (T)NONE;
+            repfnz[rep] = r;
             I x = xlsub[rep], xe = xprune[rep];
             for (;;) {
                 while (x < xe) {
-                    const I c = lsub[x++], cm = marker[c];
-                    if (cm == j) continue;
-                    marker[c] = j;
-                    const I cp = perm_r[c];
-                    if (cp == NONE) {
+                    const T c = lsub[x++], cm = marker[c];
+                    if (cm == tj) continue;
+                    marker[c] = tj;
+                    if (c >= tj) {
                         lput(nextl++, c);
-                        if (cm != j - 1) js = NONE;
+                        if (cm != tj1) js = false;
                         continue;
                     }
-                    const I crep = xsup[supno[cp] + 1] - 1;
-                    if (repfnz[crep] != NONE) {
-                        if (cp < repfnz[crep]) repfnz[crep] = cp;
+                    const T crep = xsup[supno[c] + 1] - 1;
+                    if (repfnz[crep] != (T)NONE) {
+                        if (c < repfnz[crep]) repfnz[crep] = c;
                         continue;
                     }
                     xplore[rep] = x; // descend
                     parent[crep] = rep;
                     rep = crep;
-                    repfnz[rep] = cp;
+                    repfnz[rep] = c;
                     x = xlsub[rep];
                     xe = xprune[rep];
                 }
                 segrep[nseg++] = rep; // finished: back to the parent
-                const I up = parent[rep];
-                if (up == NONE) break;
+                const T up = parent[rep];
+                if (up == (T)NONE) break;
                 rep = up;
                 x = xplore[rep];
                 xe = xprune[rep];
@@ -264,9 +277,9 @@ struct Walker {
             // fundamental supernodes: |L(:,j)| = |L(:,j-1)| - 1 besides the
             // subset test (T2_SUPER, SRC/symbfact.c:39,633-635), and at most
             // maxsuper columns
-            if (nextl - jp != jp - jm1p - 1) js = NONE;
-            if (j - fs >= maxsuper) js = NONE;
-            if (js == NONE) {
+            if (nextl - jp != jp - jm1p - 1) js = false;
+            if (j - fs >= maxsuper) js = false;
+            if (!js) {
                 if (fs < j - 2) { // >= 3 columns: keep only the first and last lists
                     I to = xlsub[fs + 1];
                     xlsub[j - 1] = to;
@@ -277,11 +290,11 @@ struct Walker {
                     nextl = to;
                 }
                 ++ns;
-                supno[j] = ns;
+                supno[j] = (T)ns;
             }
         }
-        xsup[ns + 1] = j + 1;
-        supno[j + 1] = ns;
+        xsup[ns + 1] = (T)(j + 1);
+        supno[j + 1] = (T)ns;
         xprune[j] = nextl;
         xlsub[j + 1] = nextl;
         return nseg;
@@ -289,10 +302,10 @@ struct Walker {
 
     // U segments of column j, in topological order (SRC/symbfact.c:763-820)
     void set_usub(I j, I nseg) {
-        const I js = supno[j];
+        const T js = supno[j];
         for (I s = nseg - 1; s >= 0; --s) {
-            const I rep = segrep[s];
-            if (supno[rep] == js || repfnz[rep] == NONE) continue;
+            const T rep = segrep[s];
+            if (supno[rep] == js || repfnz[rep] == (T)NONE) continue;
             if (nextu >= (I)usub.size()) usub.resize(std::max<I>(2 * usub.size(), nextu + 1024));
             usub[nextu++] = repfnz[rep];
         }
@@ -300,40 +313,39 @@ struct Walker {
     }
 
     // diagonal row of column j to position j - fsupc of its supernode's
-    // first list; pivots are diagonal (SRC/symbfact.c:684-742)
+    // first list (SRC/symbfact.c:684-742)
     void pivot(I j) {
         const I fs = xsup[supno[j]], lp = xlsub[fs], nr = xlsub[fs + 1] - lp, d0 = j - fs;
         I d = NONE;
         for (I s = d0; s < nr; ++s)
-            if (lsub[lp + s] == j) {
+            if (lsub[lp + s] == (T)j) {
                 d = s;
                 break;
             }
         if (d == NONE) throw Error("symbfact: zero diagonal at column " + std::to_string(j));
-        perm_r[j] = j;
         if (d != d0) std::swap(lsub[lp + d], lsub[lp + d0]);
     }
 
     // symmetric pruning of the supernodes column j's search reached
-    // (SRC/symbfact.c:824-906)
+    // (SRC/symbfact.c:824-906); rows <= j are pivoted now
     void prune(I j, I nseg) {
-        const I js = supno[j];
+        const T js = supno[j], tj = (T)j;
         for (I s = 0; s < nseg; ++s) {
-            const I rep = segrep[s];
-            if (repfnz[rep] == NONE || supno[rep] == js) continue;
+            const T rep = segrep[s];
+            if (repfnz[rep] == (T)NONE || supno[rep] == js) continue;
             if (xprune[rep] < xlsub[rep + 1]) continue; // pruned before
             I lo = xlsub[rep], hi = xlsub[rep + 1] - 1;
             bool hit = false;
             for (I q = lo; q <= hi; ++q)
-                if (lsub[q] == j) {
+                if (lsub[q] == tj) {
                     hit = true;
                     break;
                 }
             if (!hit) continue;
             while (lo <= hi) {
-                if (perm_r[lsub[hi]] == NONE)
+                if (lsub[hi] > tj)
                     --hi;
-                else if (perm_r[lsub[lo]] != NONE)
+                else if (lsub[lo] <= tj)
                     ++lo;
                 else {
                     std::swap(lsub[lo], lsub[hi]);
@@ -358,7 +370,7 @@ struct Walker {
                 set_usub(j, nseg);
                 pivot(j);
                 prune(j, nseg);
-                for (I s = 0; s < nseg; ++s) repfnz[segrep[s]] = NONE;
+                for (I s = 0; s < nseg; ++s) repfnz[segrep[s]] = (T)NONE;
                 ++j;
             }
         }
@@ -367,44 +379,34 @@ struct Walker {
 
 // symbfact (SRC/symbfact.c:81-215).  m x n matrix, columns [cb[j], ce[j])
 // of ri (A Pc', rows relabelled by perm_c); etree postordered.
-static Result symbfact(I m, I n, const I *cb, const I *ce, const I *ri, const I *etree, I relax,
-                       I maxsuper) {
+template <class T>
+static Result symbfact_t(I m, I n, const I *cb, const I *ce, const I *ri64, const I *etree,
+                         I relax, I maxsuper) {
     Result R;
     R.n = n;
     const I mn = std::min(m, n);
-    R.xsup.assign(n + 2, 0);
-    R.supno.assign(n + 1, 0);
-    R.xlsub.assign(n + 1, 0);
-    R.xusub.assign(n + 1, 0);
-    vector<I> xprune(n, 0), perm_r(m, NONE), marker(m, NONE), repfnz(m, NONE), parent(m, 0),
-        xplore(m, 0), segrep(m, 0);
-    R.supno[0] = NONE;
+    I annz = 0, top = 0;
+    for (I c = 0; c < n; ++c) {
+        annz += ce[c] - cb[c];
+        top = std::max(top, ce[c]);
+    }
+    vector<T> ri(top);
+    for (I c = 0; c < n; ++c)
+        for (I p = cb[c]; p < ce[c]; ++p) ri[p] = (T)ri64[p];
     const vector<I> rend = relaxed_ends(n, etree, relax);
 
-    Walker w;
+    Walker<T> w(m, n, std::max<I>(4 * annz, 1024));
     w.cb = cb;
     w.ce = ce;
-    w.ri = ri;
+    w.ri = ri.data();
     w.maxsuper = maxsuper;
-    w.xsup = R.xsup.data();
-    w.supno = R.supno.data();
-    w.xlsub = R.xlsub.data();
-    w.xusub = R.xusub.data();
-    w.xprune = xprune.data();
-    w.perm_r = perm_r.data();
-    w.marker = marker.data();
-    w.repfnz = repfnz.data();
-    w.parent = parent.data();
-    w.xplore = xplore.data();
-    w.segrep = segrep.data();
-    I annz = 0;
-    for (I c = 0; c < n; ++c) annz += ce[c] - cb[c];
-    w.lsub.resize(std::max<I>(4 * annz, 1024));
-    w.usub.resize(std::max<I>(annz, 1024));
     w.run(0, mn, rend.data());
-    R.lsub = std::move(w.lsub);
-    R.usub = std::move(w.usub);
-    R.usub.resize(R.xusub[mn]);
+
+    R.xsup.assign(w.xsup.begin(), w.xsup.end());
+    R.supno.assign(w.supno.begin(), w.supno.end());
+    R.xlsub = std::move(w.xlsub);
+    R.xusub = std::move(w.xusub);
+    R.usub.assign(w.usub.begin(), w.usub.begin() + R.xusub[mn]);
 
     // ---- counts (SRC/util.c:95-152) and the final L subscripts: the first
     // column's list of each supernode, in supernode order (SRC/util.c:163-199)
@@ -427,16 +429,28 @@ static Result symbfact(I m, I n, const I *cb, const I *ce, const I *ri, const I 
     if (n > 1) {
         R.lsub_size = R.xlsub[n];
         I out = 0;
+        I total = 0;
+        for (I s = 0; s <= nsup; ++s) total += R.xlsub[R.xsup[s] + 1] - R.xlsub[R.xsup[s]];
+        R.lsub.resize(total);
         for (I s = 0; s <= nsup; ++s) {
             const I f = R.xsup[s], a = R.xlsub[f], b = R.xlsub[f + 1];
             R.xlsub[f] = out;
-            for (I p = a; p < b; ++p) R.lsub[out++] = perm_r[R.lsub[p]];
+            // the reference applies perm_r here: the identity on pivoted
+            // rows, EMPTY on rows past min(m, n)
+            for (I p = a; p < b; ++p) R.lsub[out++] = (I)w.lsub[p] < mn ? (I)w.lsub[p] : NONE;
             for (I c = f + 1; c < R.xsup[s + 1]; ++c) R.xlsub[c] = out;
         }
         R.xlsub[n] = out;
+    } else {
+        R.lsub.assign(w.lsub.begin(), w.lsub.begin() + R.xlsub[n]);
     }
-    R.lsub.resize(R.xlsub[n]);
     return R;
+}
+
+static Result symbfact(I m, I n, const I *cb, const I *ce, const I *ri, const I *etree, I relax,
+                       I maxsuper) {
+    if (std::max(m, n) + 2 < (I)INT32_MAX) return symbfact_t<int32_t>(m, n, cb, ce, ri, etree, relax, maxsuper);
+    return symbfact_t<int64_t>(m, n, cb, ce, ri, etree, relax, maxsuper);
 }
 
 // sp_ienv_dist(2) / (3) (SRC/sp_ienv.c:85-112): environment first, then

@@ -2,14 +2,16 @@
 EXAMPLE/p[dsz]drive.c, linked against libslu_mi355x.so FIRST and then the
 reference library with pdgstrf.o / psgstrf.o / pzgstrf.o removed
 (oracle/_ref/p?drive_mi355x, built by `make -C oracle dropin`), run the
-reference's whole pipeline -- matrix read, equilibration, MC64, MMD, symbfact,
-pddistribute, OUR p?gstrf, the reference pdgstrs / pdgsrfs -- and must solve
+reference's whole pipeline -- matrix read, equilibration, MC64, MMD, OUR
+sp_colorder / symbfact (csrc/symbolic.cpp), the reference pddistribute, OUR
+p?gstrf, the reference pdgstrs / pdgsrfs -- and must solve
 as accurately as the same drivers linked with the reference factorization
 (oracle/_ref/p?drive_ref).
 
 GPU: 1 rank (1x1 grid), and 4 ranks on a 2x2 grid sharing the box's one GPU
 (the library then carries the panel broadcasts over MPI instead of RCCL).
-CPU: the link itself (our pdgstrf is the one the binary binds).
+CPU: the link itself (our pdgstrf, symbfact and sp_colorder are the ones the
+binary binds).
 """
 import os
 import re
@@ -51,9 +53,10 @@ def test_dropin_driver_binds_our_pdgstrf():
     assert "libslu_mi355x.so" in dyn
     und = subprocess.run(["nm", "-D", "--undefined-only", exe], capture_output=True,
                          text=True).stdout.split()
-    assert "pdgstrf" in und            # resolved at load time from libslu_mi355x.so
     defined = subprocess.run(["nm", "--defined-only", exe], capture_output=True, text=True).stdout
-    assert not re.search(r"\bT pdgstrf\b", defined)   # no reference pdgstrf inside
+    for sym in ("pdgstrf", "symbfact", "sp_colorder"):
+        assert sym in und                  # resolved at load time from libslu_mi355x.so
+        assert not re.search(rf"\bT {sym}\b", defined)   # no reference copy inside
 
 
 CASES = [
