@@ -76,13 +76,21 @@ def grid_shape(n):
     return {1: (1, 1), 2: (1, 2), 4: (2, 2), 8: (2, 4), 16: (4, 4)}.get(n, (1, n))
 
 
-def build_lu(workload, nx, pr, pc, myrow, mycol):
+def build_lu(workload, nx, pr, pc, myrow, mycol, ordering="grid"):
     from superlu_dist_amd.frontend import STENCIL_2D5, STENCIL_3D7, STENCIL_3D27, Csc, Symbolic, nd_order
     kind, dims, dtype, diag, diag_im = WORKLOADS[workload][:5]
     kind = {"2d5": STENCIL_2D5, "3d7": STENCIL_3D7, "3d27": STENCIL_3D27}[kind]
     d = dims(nx)
     A = Csc.stencil(kind, *d, diag=diag, diag_im=diag_im, dtype=dtype)
-    S = Symbolic(A, nd_order(*d), 60, 256)
+    if ordering == "graph":
+        # the library's METIS_NodeND on A'+A (csrc/ordering.cpp), as
+        # get_perm_c_dist's METIS_AT_PLUS_A would call it
+        from superlu_dist_amd.symbolic import at_plus_a, metis_nodend
+        cp, ri, _ = A.arrays()
+        perm = metis_nodend(A.n, *at_plus_a(A.n, cp, ri))[0]
+    else:
+        perm = nd_order(*d)
+    S = Symbolic(A, perm, 60, 256)
     lu = S.distribute(pr, pc, myrow, mycol)
     return A, S, lu
 
@@ -231,6 +239,9 @@ def main():
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="lap3d",
                     help="lap3d = C3 (headline), lap2d = C2, helm3d = C4 (complex), st27 = C5 (fp32)")
     ap.add_argument("--nx", type=int, default=None, help="grid points per dimension")
+    ap.add_argument("--ordering", choices=["grid", "graph"], default="grid",
+                    help="grid: geometric nested dissection of the stencil grid (the headline "
+                         "configuration); graph: the library's METIS_NodeND on A'+A")
     ap.add_argument("--cpu-sample", type=int, default=100)
     ap.add_argument("--cpu-ranks", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
@@ -290,7 +301,7 @@ def main():
 
     t0 = time.time()
     log(f"front-end {args.workload} nx={args.nx} grid {pr}x{pc}")
-    A, S, lu = build_lu(args.workload, args.nx, pr, pc, myrow, mycol)
+    A, S, lu = build_lu(args.workload, args.nx, pr, pc, myrow, mycol, args.ordering)
     t_front = time.time() - t0
     log(f"front-end {t_front:.1f} s, {S.nsupers} supernodes")
     if world == 1:
@@ -419,7 +430,7 @@ def main():
             "dtype": W[7],
             "data": f"synthetic (generated {W[0]} stencil matrix, ||A||_1 = {anorm:g})",
             "config": {"workload": f"{args.workload}: {W[0]} stencil {'x'.join(map(str, W[1](args.nx)))} "
-                                   f"(n={A.n}), nested dissection, relax 60, maxsup 256, {W[6]}",
+                                   f"(n={A.n}), {'graph nested dissection (METIS_NodeND)' if args.ordering == 'graph' else 'nested dissection'}, relax 60, maxsup 256, {W[6]}",
                        "grid": f"{pr}x{pc}", "nsupers": int(S.nsupers),
                        "flops_per_factorization": flops_all,
                        "nnz_L": S.nnzL, "parallelism": f"2D block-cyclic {pr}x{pc}",

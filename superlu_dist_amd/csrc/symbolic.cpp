@@ -182,16 +182,20 @@ struct Walker {
         supno[0] = (T)NONE;
     }
 
-    void lput(I at, T v) {
-        if (at >= (I)lsub.size()) lsub.resize(std::max<I>(2 * lsub.size(), at + 1024));
-        lsub[at] = v;
+    I m = 0;
+    // room for `more` entries past `at`: checked once per column (a column's
+    // list has at most m entries), not per entry
+    void reserve(I at, I more) {
+        if (at + more > (I)lsub.size()) lsub.resize(std::max<I>(2 * lsub.size(), at + more + 1024));
     }
+    void lput(I at, T v) { lsub[at] = v; }
 
     // relaxed supernode j..k: union of the columns' row structures, a copy
     // of it for pruning when k > j (SRC/symbfact.c:291-370)
     void relaxed(I j, I k) {
         const T ns = ++supno[j];
         I nextl = xlsub[j];
+        reserve(nextl, 2 * m);
         for (I i = j; i <= k; ++i) {
             for (I p = cb[i]; p < ce[i]; ++p) {
                 const T r = ri[p];
@@ -223,6 +227,7 @@ struct Walker {
         const T tj = (T)j, tj1 = (T)(j - 1);
         I ns = supno[j], nextl = xlsub[j], nseg = 0;
         bool js = true; // j joins j-1's supernode
+        reserve(nextl, m);
         for (I p = cb[j]; p < ce[j]; ++p) {
             const T r = ri[p], km = marker[r];
             if (km == tj) continue;
@@ -396,6 +401,7 @@ static Result symbfact_t(I m, I n, const I *cb, const I *ce, const I *ri64, cons
     const vector<I> rend = relaxed_ends(n, etree, relax);
 
     Walker<T> w(m, n, std::max<I>(4 * annz, 1024));
+    w.m = m;
     w.cb = cb;
     w.ce = ce;
     w.ri = ri.data();

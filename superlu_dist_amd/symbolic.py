@@ -28,6 +28,39 @@ def last_error():
     return e.decode() if e else "unknown error"
 
 
+def at_plus_a(n, colptr, rowind):
+    """Pattern of A'+A without the diagonal as CSR (xadj, adjncy), the graph
+    get_perm_c_dist hands to METIS (at_plus_a_dist, SRC/get_perm_c.c:305)."""
+    colptr = np.asarray(colptr, np.int64)
+    rowind = np.asarray(rowind, np.int64)
+    col = np.repeat(np.arange(n, dtype=np.int64), np.diff(colptr))
+    r = np.concatenate([rowind, col])
+    c = np.concatenate([col, rowind])
+    keep = r != c
+    key = np.unique(c[keep] * n + r[keep])
+    cc, rr = key // n, key % n
+    xadj = np.zeros(n + 1, np.int64)
+    np.add.at(xadj, cc + 1, 1)
+    return np.cumsum(xadj), rr
+
+
+def metis_nodend(n, xadj, adjncy):
+    """The library's METIS_NodeND (nested dissection, csrc/ordering.cpp):
+    returns perm_c = iperm (perm_c[i] = new position of column i), as
+    get_metis does (SRC/get_perm_c.c:91-97)."""
+    xadj = np.ascontiguousarray(xadj, np.int64)
+    adjncy = np.ascontiguousarray(adjncy, np.int64)
+    nn = np.array([n], np.int64)
+    perm = np.zeros(max(n, 1), np.int64)
+    iperm = np.zeros(max(n, 1), np.int64)
+    null = C.cast(None, C.POINTER(C.c_int64))
+    rc = lib().METIS_NodeND(as_i64p(nn), as_i64p(xadj), as_i64p(adjncy) if len(adjncy) else null,
+                            null, null, as_i64p(perm), as_i64p(iperm))
+    if rc != 1:
+        raise RuntimeError(f"METIS_NodeND returned {rc}")
+    return iperm[:n], perm[:n]
+
+
 @dataclass
 class ColOrder:
     perm_c: np.ndarray  # postordered column permutation (perm_c[i] = new position of column i)
