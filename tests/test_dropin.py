@@ -54,7 +54,7 @@ def test_dropin_driver_binds_our_pdgstrf():
     und = subprocess.run(["nm", "-D", "--undefined-only", exe], capture_output=True,
                          text=True).stdout.split()
     defined = subprocess.run(["nm", "--defined-only", exe], capture_output=True, text=True).stdout
-    for sym in ("pdgstrf", "symbfact", "sp_colorder"):
+    for sym in ("pdgstrf", "symbfact", "sp_colorder", "METIS_NodeND"):
         assert sym in und                  # resolved at load time from libslu_mi355x.so
         assert not re.search(rf"\bT {sym}\b", defined)   # no reference copy inside
 
@@ -80,3 +80,18 @@ def test_reference_driver_with_our_factorization(drv, matrix, extra, nprocs, gri
     print(f"{drv} {matrix} {nprocs} ranks: ||x-xtrue||/||x|| ref {ref_err:.3e} mi355x {my_err:.3e}; "
           f"FACTOR time ref {ref_t} s, mi355x {my_t} s")
     assert my_err <= max(10 * ref_err, tol), (my_err, ref_err)
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not _have("pddrive_mi355x", "pddrive_ref"), reason="drivers not built")
+@pytest.mark.parametrize("drv,matrix", [("pddrive", "g20.rua"), ("pddrive", "big.rua"),
+                                        ("pzdrive", "cg20.cua")])
+def test_reference_driver_default_ordering_through_our_metis(drv, matrix):
+    """No -q: the drivers' default ColPerm = METIS_AT_PLUS_A, which calls
+    METIS_NodeND (SRC/get_perm_c.c:524-541).  METIS is not in the image, so
+    only the library's nested dissection can serve it; the all-reference
+    driver runs MMD (-q 2) for the accuracy yardstick."""
+    ref_err, _, _ = _run(f"{drv}_ref", 1, ["-r", "1", "-c", "1", "-q", "2"], matrix)
+    my_err, _, out = _run(f"{drv}_mi355x", 1, ["-r", "1", "-c", "1"], matrix)
+    print(f"{drv} {matrix} METIS_AT_PLUS_A via the library: {my_err:.3e} (reference, MMD: {ref_err:.3e})")
+    assert my_err <= max(10 * ref_err, 1e-12), (my_err, ref_err)
