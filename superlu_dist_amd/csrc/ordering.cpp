@@ -16,7 +16,7 @@
 //   * the separator thinned to the vertices that touch the far side (the
 //     others join the near side);
 //   * near side, far side, then the separator, recursively, down to parts of
-//     at most LEAF vertices, which keep their BFS order;
+//     at most LEAF (32) vertices, which keep their BFS order;
 //   * the two sides of the top splits on host threads.
 //
 // Not METIS's multilevel algorithm: its quality on 3D grids is measured
@@ -50,7 +50,9 @@ struct Work {
     vector<int> &part;
 };
 
-constexpr I LEAF = 128;
+// leaf size (SLU_ND_LEAF for A/B): 32 -- 128 gave 2.5x the supernodes on the
+// 3D Laplacian at the same factor time
+static const I LEAF = getenv("SLU_ND_LEAF") ? atoll(getenv("SLU_ND_LEAF")) : 32;
 
 // part[] is read for neighbours that belong to parts other threads are
 // splitting: relaxed atomic accesses (the value read is never this part's id)

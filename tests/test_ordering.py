@@ -93,16 +93,15 @@ def test_nodend_returns_a_permutation(kind):
 
 def test_nodend_fill_against_reference_mmd():
     """3D 7-point 12^3 (the golden's pattern and the reference's MMD perm_c):
-    at this size minimum degree still fills slightly less (152 k vs 140 k);
-    from 40^3 on nested dissection fills less (60^3: 0.49x, 100^3: 0.40x of
-    MMD)."""
+    nested dissection fills no more than the reference's MMD (137 k vs
+    140 k; 60^3: 0.48x)."""
     z = np.load(os.path.join(GOLDEN, "symb_lap3d12_mmd.npz"), allow_pickle=False)
     n = int(z["meta"][0])
     colptr, rowind = z["colptr"], z["rowind"]
     mmd = _nnzl(n, colptr, rowind, z["perm_c_in"])
     xadj, adj = S.at_plus_a(n, colptr, rowind)
     nd = _nnzl(n, colptr, rowind, S.metis_nodend(n, xadj, adj)[0])
-    assert nd <= 1.15 * mmd, (nd, mmd)
+    assert nd <= mmd, (nd, mmd)
 
 
 def test_nodend_fill_scales_like_nested_dissection():
