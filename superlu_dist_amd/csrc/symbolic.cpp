@@ -16,6 +16,8 @@
 // order decides the order of each supernode's L subscripts, and pddistribute
 // lays the factor blocks out in that order.
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
@@ -400,6 +402,7 @@ static Result symbfact_t(I m, I n, const I *cb, const I *ce, const I *ri64, cons
         for (I p = cb[c]; p < ce[c]; ++p) ri[p] = (T)ri64[p];
     const vector<I> rend = relaxed_ends(n, etree, relax);
 
+    const auto t0 = std::chrono::steady_clock::now();
     Walker<T> w(m, n, std::max<I>(4 * annz, 1024));
     w.m = m;
     w.cb = cb;
@@ -407,6 +410,7 @@ static Result symbfact_t(I m, I n, const I *cb, const I *ce, const I *ri64, cons
     w.ri = ri.data();
     w.maxsuper = maxsuper;
     w.run(0, mn, rend.data());
+    const auto t1 = std::chrono::steady_clock::now();
 
     R.xsup.assign(w.xsup.begin(), w.xsup.end());
     R.supno.assign(w.supno.begin(), w.supno.end());
@@ -450,6 +454,10 @@ static Result symbfact_t(I m, I n, const I *cb, const I *ce, const I *ri64, cons
     } else {
         R.lsub.assign(w.lsub.begin(), w.lsub.begin() + R.xlsub[n]);
     }
+    if (getenv("SLU_SYMB_TIME"))
+        fprintf(stderr, "symbfact: search %.3f s, total %.3f s\n",
+                std::chrono::duration<double>(t1 - t0).count(),
+                std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
     return R;
 }
 
