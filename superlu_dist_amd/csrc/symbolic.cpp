@@ -230,51 +230,57 @@ struct Walker {
         I ns = supno[j], nextl = xlsub[j], nseg = 0;
         bool js = true; // j joins j-1's supernode
         reserve(nextl, m);
+        // local copies of the arrays the search touches (registers, no reloads)
+        T *const L = lsub.data(), *const mk = marker.data(), *const rf = repfnz.data(),
+                 *const par = parent.data(), *const sg = segrep.data();
+        const T *const xs = xsup.data(), *const sn = supno.data();
+        const I *const xl = xlsub.data(), *const xp = xprune.data();
+        I *const xo = xplore.data();
         for (I p = cb[j]; p < ce[j]; ++p) {
-            const T r = ri[p], km = marker[r];
+            const T r = ri[p], km = mk[r];
             if (km == tj) continue;
-            marker[r] = tj;
+            mk[r] = tj;
             if (r >= tj) { // row not pivoted yet: in L(:, j)
-                lput(nextl++, r);
+                L[nextl++] = r;
                 if (km != tj1) js = false;
                 continue;
             }
-            T rep = xsup[supno[r] + 1] - 1;
-            if (repfnz[rep] != (T)NONE) {
-                if (r < repfnz[rep]) repfnz[rep] = r;
+            T rep = xs[sn[r] + 1] - 1;
+            if (rf[rep] != (T)NONE) {
+                if (r < rf[rep]) rf[rep] = r;
                 continue;
             }
-            parent[rep] = (T)NONE;
-            repfnz[rep] = r;
-            I x = xlsub[rep], xe = xprune[rep];
+            par[rep] = (T)NONE;
+            rf[rep] = r;
+            I x = xl[rep], xe = xp[rep];
             for (;;) {
                 while (x < xe) {
-                    const T c = lsub[x++], cm = marker[c];
+                    const T c = L[x++], cm = mk[c];
                     if (cm == tj) continue;
-                    marker[c] = tj;
+                    mk[c] = tj;
                     if (c >= tj) {
-                        lput(nextl++, c);
+                        L[nextl++] = c;
                         if (cm != tj1) js = false;
                         continue;
                     }
-                    const T crep = xsup[supno[c] + 1] - 1;
-                    if (repfnz[crep] != (T)NONE) {
-                        if (c < repfnz[crep]) repfnz[crep] = c;
+                    const T crep = xs[sn[c] + 1] - 1;
+                    if (rf[crep] != (T)NONE) {
+                        if (c < rf[crep]) rf[crep] = c;
                         continue;
                     }
-                    xplore[rep] = x; // descend
-                    parent[crep] = rep;
+                    xo[rep] = x; // descend
+                    par[crep] = rep;
                     rep = crep;
-                    repfnz[rep] = c;
-                    x = xlsub[rep];
-                    xe = xprune[rep];
+                    rf[rep] = c;
+                    x = xl[rep];
+                    xe = xp[rep];
                 }
-                segrep[nseg++] = rep; // finished: back to the parent
-                const T up = parent[rep];
+                sg[nseg++] = rep; // finished: back to the parent
+                const T up = par[rep];
                 if (up == (T)NONE) break;
                 rep = up;
-                x = xplore[rep];
-                xe = xprune[rep];
+                x = xo[rep];
+                xe = xp[rep];
             }
         }
         if (j == 0) {
