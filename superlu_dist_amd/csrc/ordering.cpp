@@ -238,7 +238,10 @@ int METIS_NodeND(int_t *nvtxs, int_t *xadj, int_t *adjncy, int_t *vwgt, int_t *o
     (void)options;
     try {
         const int64_t n = *nvtxs;
-        if (n < 0 || !xadj || !perm || !iperm) return -4;
+        if (n < 0 || !xadj || !perm || !iperm || (n > 0 && xadj[0] != 0)) return -4;
+        for (int64_t i = 0; i < n; ++i)
+            if (xadj[i + 1] < xadj[i]) return -4;
+        if (n > 0 && xadj[n] > 0 && !adjncy) return -4;
         for (int64_t i = 0; i < n; ++i)
             for (int64_t q = xadj[i]; q < xadj[i + 1]; ++q)
                 if (adjncy[q] < 0 || adjncy[q] >= n) return -4;

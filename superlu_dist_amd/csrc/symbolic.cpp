@@ -560,11 +560,19 @@ void sp_colorder(superlu_dist_options_t *options, SuperMatrix *A, int_t *perm_c,
     const NCformat *As = (const NCformat *)A->Store;
     const I n = A->ncol;
     NCPformat *S = (NCPformat *)malloc(sizeof(NCPformat));
+    if (!S) {
+        fprintf(stderr, "sp_colorder: out of host memory\n");
+        abort(); // the reference ABORTs (SRC/sp_colorder.c:106)
+    }
     S->nnz = As->nnz;
     S->nzval = As->nzval;
     S->rowind = As->rowind;
     S->colbeg = (int_t *)malloc(std::max<I>(n, 1) * sizeof(int_t));
     S->colend = (int_t *)malloc(std::max<I>(n, 1) * sizeof(int_t));
+    if (!S->colbeg || !S->colend) {
+        fprintf(stderr, "sp_colorder: out of host memory\n");
+        abort();
+    }
     AC->Stype = SLU_NCP;
     AC->Dtype = A->Dtype;
     AC->Mtype = A->Mtype;

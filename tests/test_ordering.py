@@ -123,3 +123,6 @@ def test_nodend_rejects_bad_input():
     adj = np.array([1, 5], np.int64)      # 5 out of range
     with pytest.raises(RuntimeError):
         S.metis_nodend(2, xadj, adj)
+    xadj = np.array([0, 2, 1], np.int64)  # decreasing pointers
+    with pytest.raises(RuntimeError):
+        S.metis_nodend(2, xadj, np.array([1, 0], np.int64))
