@@ -48,6 +48,34 @@ class Options(C.Structure):
                                          "SymPattern", "Use_TensorCore", "Algo3d")]
 
 
+class SuperMatrix(C.Structure):
+    """SRC/supermatrix.h:54-63."""
+    _fields_ = [("Stype", C.c_int), ("Dtype", C.c_int), ("Mtype", C.c_int),
+                ("nrow", C.c_int64), ("ncol", C.c_int64), ("Store", C.c_void_p)]
+
+
+class NCformat(C.Structure):
+    _fields_ = [("nnz", C.c_int64), ("nzval", C.c_void_p), ("rowind", C.POINTER(C.c_int64)),
+                ("colptr", C.POINTER(C.c_int64))]
+
+
+class NCPformat(C.Structure):
+    _fields_ = [("nnz", C.c_int64), ("nzval", C.c_void_p), ("rowind", C.POINTER(C.c_int64)),
+                ("colbeg", C.POINTER(C.c_int64)), ("colend", C.POINTER(C.c_int64))]
+
+
+class GluPersist(C.Structure):
+    _fields_ = [("xsup", C.POINTER(C.c_int64)), ("supno", C.POINTER(C.c_int64))]
+
+
+class GluFreeable(C.Structure):
+    """SRC/superlu_defs.h:494-505."""
+    _fields_ = [("lsub", C.POINTER(C.c_int64)), ("xlsub", C.POINTER(C.c_int64)),
+                ("usub", C.POINTER(C.c_int64)), ("xusub", C.POINTER(C.c_int64)),
+                ("nzlmax", C.c_int64), ("nzumax", C.c_int64), ("MemModel", C.c_int),
+                ("nnzLU", C.c_int64)]
+
+
 class Stat(C.Structure):
     _fields_ = [("panel_histo", C.POINTER(C.c_int)), ("utime", C.POINTER(C.c_double)),
                 ("ops", C.POINTER(C.c_float)), ("TinyPivots", C.c_int), ("RefineSteps", C.c_int),
