@@ -293,7 +293,13 @@ slu_symb *slu_symbolic(const slu_csc *A, const int64_t *perm_c_in, int relax,
     for (int64_t j = 0; j < n; ++j)
         if (parent[j] >= 0) { nchild[parent[j]]++; size[parent[j]] += size[j]; }
 
-    // supernode partition: relaxed subtrees, then fundamental chains
+    // supernode partition: relaxed subtrees, then fundamental chains.
+    // SLU_AMALG_MULTICHILD=1 (A/B): a chain may also continue through a
+    // column with several children (their structures are nested in it)
+    static const bool multichild =
+        getenv("SLU_AMALG_MULTICHILD") && atoi(getenv("SLU_AMALG_MULTICHILD"));
+    static const double AMALG_ZERO_FRAC =
+        getenv("SLU_AMALG_ZERO") ? atof(getenv("SLU_AMALG_ZERO")) : 0.10;
     vector<int64_t> xsup;
     xsup.reserve(n / 4 + 2);
     int64_t j = 0;
@@ -316,12 +322,11 @@ slu_symb *slu_symbolic(const slu_csc *A, const int64_t *perm_c_in, int relax,
         // introduces stay below AMALG_ZERO_FRAC of the stored entries.  Along
         // a chain struct(L_c)\{c} is contained in struct(L_{c+1}), so the
         // supernode's structure is [f..l] u struct(L_l): exact bookkeeping.
-        const double AMALG_ZERO_FRAC = 0.10;
         xsup.push_back(j);
         int64_t f = j, len = 1;
         double sumcc = (double)cc[j];
         while (j + 1 < n && len < maxsup && parent[j] == j + 1 &&
-               nchild[j + 1] == 1 && size[j + 1] > relax) {
+               (nchild[j + 1] == 1 || multichild) && size[j + 1] > relax) {
             double w = (double)(len + 1), c1 = (double)cc[j + 1];
             double zeros = w * (w - 1) / 2 + w * c1 - (sumcc + c1);
             double stored = w * (w + 1) / 2 + w * c1;
