@@ -88,6 +88,11 @@ def build_lu(workload, nx, pr, pc, myrow, mycol, ordering="grid"):
         from superlu_dist_amd.symbolic import at_plus_a, metis_nodend
         cp, ri, _ = A.arrays()
         perm = metis_nodend(A.n, *at_plus_a(A.n, cp, ri))[0]
+        # chains through multi-child columns in the front-end's partition:
+        # the level-set separators hang their far-side components along the
+        # chain (100^3: 277 -> 182 ms); read at the first
+        # slu_symbolic call of the process
+        os.environ.setdefault("SLU_AMALG_MULTICHILD", "1")
     else:
         perm = nd_order(*d)
     S = Symbolic(A, perm, 60, 256)
