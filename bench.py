@@ -1,7 +1,12 @@
 """Benchmark: pdgstrf fp64 GFLOP/s + factor time, 3D 7-point Laplacian n = 1M.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--n 100]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--nx 100]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+With --gpus N > 1 and no WORLD_SIZE in the environment, bench.py starts the N
+ranks itself (spawn_ranks); a WORLD_SIZE that differs from --gpus, fewer
+visible GPUs than ranks, or communicators that see a different number of ranks
+end the run with a non-zero status instead of measuring another grid.
 
 One process per GPU; N GPUs form the near-square 2D process grid of the
 reference (1x1, 1x2, 2x2, 2x4).  A step is one numeric factorization
@@ -88,14 +93,12 @@ def build_lu(workload, nx, pr, pc, myrow, mycol, ordering="grid"):
         from superlu_dist_amd.symbolic import at_plus_a, metis_nodend
         cp, ri, _ = A.arrays()
         perm = metis_nodend(A.n, *at_plus_a(A.n, cp, ri))[0]
-        # chains through multi-child columns in the front-end's partition:
-        # the level-set separators hang their far-side components along the
-        # chain (100^3: 277 -> 182 ms); read at the first
-        # slu_symbolic call of the process
-        os.environ.setdefault("SLU_AMALG_MULTICHILD", "1")
     else:
         perm = nd_order(*d)
-    S = Symbolic(A, perm, 60, 256)
+    # graph ordering: chains through multi-child columns in the front-end's
+    # partition (the level-set separators hang their far-side components
+    # along the chain; 100^3: 277 -> 182 ms)
+    S = Symbolic(A, perm, 60, 256, multichild=ordering == "graph")
     lu = S.distribute(pr, pc, myrow, mycol)
     return A, S, lu
 
@@ -260,7 +263,8 @@ def main():
                     help="only the serialized (single-stream) profiling step: for rocprofv3 runs")
     ap.add_argument("--host-transport", action="store_true",
                     help="REHEARSAL ONLY: several ranks on one GPU through the host-staged "
-                         "test transport (RCCL refuses duplicate devices); not a measurement")
+                         "point-to-point test transport (the RCCL send / receive pairs over "
+                         "gloo; RCCL refuses duplicate devices); not a measurement")
     args = ap.parse_args()
     W = WORKLOADS[args.workload]
     if args.nx is None:
@@ -268,11 +272,16 @@ def main():
     if args.workload != "lap3d":
         args.no_cpu = True  # the CPU baseline is the reference on the headline workload
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # `bench.py --gpus N` without a launcher: start the N ranks here,
+        # before anything touches the GPU (torch.distributed.run does the same)
+        sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        world = max(world, 1)
+        log(f"WORLD_SIZE={world} but --gpus {args.gpus}: refusing to measure a different grid")
+        sys.exit(2)
     pr, pc = grid_shape(world)
     myrow, mycol = rank // pc, rank % pc
 
@@ -294,6 +303,11 @@ def main():
                 grid = GlooGrid(rank, pr, pc)
             local = 0
         else:
+            ndev = torch.cuda.device_count()
+            if ndev < world:
+                log(f"{world} ranks but {ndev} visible GPUs: RCCL needs one GPU per rank "
+                    f"(--host-transport rehearses several ranks on one GPU)")
+                sys.exit(2)
             buf = torch.zeros(128, dtype=torch.uint8)
             if rank == 0:
                 buf[:] = torch.tensor(list(Comm.unique_id()), dtype=torch.uint8)
@@ -312,9 +326,17 @@ def main():
     if world == 1:
         comm = None
     elif grid is not None:
-        comm = Comm.host(pr, pc, rank, 0, grid.bcast)
+        # the RCCL transport's send / receive pairs, host-staged over gloo
+        comm = Comm.host_p2p(pr, pc, rank, 0, grid.p2p)
     else:
         comm = Comm(pr, pc, rank, device=local, uid=uid)
+    if comm is not None:
+        sizes = (comm.size(0), comm.size(1), comm.size(2))
+        if sizes != (world, pc, pr):
+            log(f"the communicators see {sizes} ranks (grid, row, column), expected "
+                f"{(world, pc, pr)}")
+            sys.exit(3)
+        log(f"communicators: grid {sizes[0]}, row {sizes[1]}, column {sizes[2]} ranks")
     t0 = time.time()
     plan = Plan(lu, comm=comm, timing=2 if args.level_log else 1)
     t_plan = time.time() - t0
@@ -439,7 +461,7 @@ def main():
                        "grid": f"{pr}x{pc}", "nsupers": int(S.nsupers),
                        "flops_per_factorization": flops_all,
                        "nnz_L": S.nnzL, "parallelism": f"2D block-cyclic {pr}x{pc}",
-                       "transport": ("host-staged gloo (REHEARSAL, not a measurement)"
+                       "transport": ("host-staged gloo point-to-point (REHEARSAL, not a measurement)"
                                      if grid is not None else
                                      (f"rccl ({world} ranks, row/column communicators)"
                                       if world > 1 else "none")),
@@ -460,6 +482,26 @@ def main():
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def spawn_ranks(n):
+    """One child process per rank with the torch.distributed.run environment
+    (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT); rank 0's
+    stdout is ours (the one JSON line), the others' goes to stderr.  Returns
+    the first non-zero exit status (0 if all ranks succeeded)."""
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable] + sys.argv, env=env,
+                                      stdout=None if r == 0 else sys.stderr))
+    codes = [p.wait() for p in procs]
+    log(f"ranks exited with {codes}")
+    return next((c for c in codes if c != 0), 0)
 
 
 def pmc_traffic(workload, nx, pr, pc, kernel):

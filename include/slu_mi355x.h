@@ -125,6 +125,27 @@ typedef int (*slu_host_bcast_fn)(void *ctx, int group, int root, void *buf,
                                  int64_t bytes);
 slu_comm *slu_comm_create_host(slu_host_bcast_fn fn, void *ctx, int nprow,
                                int npcol, int iam, int device);
+/* Point-to-point test transport: every exchange phase hands fn the list of
+ * sends and receives (peer = rank within group, as ncclSend / ncclRecv get
+ * it) that the RCCL transport issues inside one ncclGroupStart / End, in the
+ * same order, with host-staged buffers; fn must post all of them before
+ * waiting for any (e.g. torch.distributed isend / irecv + wait) and return 0
+ * once all completed.  Sends and receives between one pair of ranks match in
+ * order, as in RCCL.  device = -1: no GPU (schedule-only plans). */
+typedef struct {
+    int group;     /* 0 whole grid, 1 my process row, 2 my process column */
+    int peer;      /* rank within that group */
+    int send;      /* 1 send, 0 receive */
+    int reserved;
+    void *buf;
+    int64_t bytes;
+} slu_host_p2p_op;
+typedef int (*slu_host_p2p_fn)(void *ctx, int nops, const slu_host_p2p_op *ops);
+slu_comm *slu_comm_create_host_p2p(slu_host_p2p_fn fn, void *ctx, int nprow,
+                                   int npcol, int iam, int device);
+/* Ranks in group 0 / 1 / 2 of c (for RCCL: ncclCommCount of the world / row /
+ * column communicator), -1 on error. */
+int slu_comm_size(const slu_comm *c, int group);
 void slu_comm_destroy(slu_comm *c);
 
 /* Engine options (everything the kernels need beyond the LUstruct). */
@@ -141,7 +162,11 @@ typedef struct {
                                while later levels are factored (the
                                factors are final once their level's panels
                                are done); slu_plan_download is then a no-op */
-    int reserved[3];
+    int schedule_only;      /* 1: host-only plan (no HIP call at all): layout,
+                               index exchange, levels and exchange sections,
+                               for slu_plan_check_exchange; a grid needs the
+                               point-to-point host transport */
+    int reserved[2];
 } slu_engine_opts;
 
 /* A plan = device-resident factors + every index table the kernels use.
@@ -203,6 +228,11 @@ int slu_plan_fill_a(slu_plan *p, const void *a, int on_device);
  * (stat->RefineSteps).  t_refine_ms in the stats = device time of the call. */
 int slu_plan_refine(slu_plan *p, const void *b, void *x, int64_t ld, int nrhs, double *berr,
                     int *steps);
+/* Schedule-only plans: replay every level's exchange phases of
+ * slu_plan_factor through the communicator on host buffers; each received
+ * section is checked byte for byte against what its root wrote.  Collective;
+ * returns 0 and the number / bytes of sections this rank received. */
+int slu_plan_check_exchange(slu_plan *p, int64_t *nsections, int64_t *nbytes);
 void slu_plan_destroy(slu_plan *p);
 
 /* Plan statistics (algorithmic work of one factorization on this rank). */
@@ -273,10 +303,14 @@ int slu_order_nd_grid(int nx, int ny, int nz, int64_t *perm_c);
 
 /* Symbolic factorization of P(A+A^T)P^T (structure of the LU factors when A
  * is structurally symmetric; a valid superset otherwise).  perm_c is
- * composed with an etree postorder.  relax / maxsup as sp_ienv_dist(2/3). */
+ * composed with an etree postorder.  relax / maxsup as sp_ienv_dist(2/3).
+ * flags: SLU_SYMB_MULTICHILD lets a chain supernode continue through a
+ * column with several etree children (shorter supernodal trees for
+ * level-set nested dissections). */
+enum { SLU_SYMB_MULTICHILD = 1 };
 typedef struct slu_symb slu_symb;
 slu_symb *slu_symbolic(const slu_csc *A, const int64_t *perm_c, int relax,
-                       int maxsup);
+                       int maxsup, int flags);
 void slu_symb_free(slu_symb *s);
 int64_t slu_symb_nsupers(const slu_symb *s);
 /* copies: xsup (nsupers+1), supno (n), final perm_c (n) */

@@ -13,7 +13,21 @@ import ctypes as C
 
 import numpy as np
 
-from .lib import SLU_D, SLU_S, SLU_Z, lib
+from .lib import DROPIN_PATH, SLU_D, SLU_S, SLU_Z
+
+_dropin = None
+
+
+def dropin():
+    """The drop-in library itself (libslu_mi355x.so: only the p[dsz]gstrf /
+    [dsz]scatter_* symbols of the reference's p?gstrf.c.o)."""
+    global _dropin
+    if _dropin is None:
+        import os
+        if not os.path.exists(DROPIN_PATH):
+            raise RuntimeError(f"{DROPIN_PATH} missing: build with make -C superlu_dist_amd/csrc")
+        _dropin = C.CDLL(DROPIN_PATH)
+    return _dropin
 
 MPI_Comm = C.c_int  # conda MPICH: MPI_Comm is an int (SURVEY 8b ABI layout)
 NPHASES = 22        # PhaseType (SRC/superlu_enum_consts.h)
@@ -121,7 +135,7 @@ def grid_1x1(comm=0x44000000):
 def pxgstrf(lu, anorm, options=None, grid=None, m=None, n=None):
     """Call pdgstrf / psgstrf / pzgstrf on the LUStruct ``lu`` in place, as
     pdgssvx does.  Returns (return value, info, stat dict)."""
-    L = lib()
+    L = dropin()
     fn = {SLU_D: L.pdgstrf, SLU_S: L.psgstrf, SLU_Z: L.pzgstrf}[lu.dtype]
     fn.restype = C.c_int64
     anorm_t = C.c_float if lu.dtype == SLU_S else C.c_double

@@ -30,6 +30,7 @@
 #include <array>
 #include <chrono>
 #include <cstring>
+#include <map>
 #include <memory>
 #include <numeric>
 #include <string>
@@ -105,6 +106,7 @@ struct slu_comm {
     int nprow = 1, npcol = 1, iam = 0, myrow = 0, mycol = 0, device = 0;
     ncclComm_t world = nullptr, row = nullptr, col = nullptr;
     slu_host_bcast_fn host_fn = nullptr;
+    slu_host_p2p_fn host_p2p = nullptr; // point-to-point test transport
     void *host_ctx = nullptr;
 };
 
@@ -146,9 +148,77 @@ struct Xport {
     void section(int g, int root, uint32_t mask, void *buf, size_t bytes) {
         if (bytes && gsize(g) > 1 && (mask & ~(1u << root))) ops.push_back({g, root, buf, bytes, mask});
     }
+    // The point-to-point test transport: exactly the send / receive pairs
+    // the RCCL branch below issues, in the same order (a broadcast becomes
+    // the root's sends to every other member), staged through host memory
+    // and handed to the caller as one group (its sends and receives are all
+    // posted before any completes, as inside ncclGroupStart / End).  A rank
+    // that expects a section its root does not send, or a different order of
+    // sections between one pair, then hangs or fails in the test instead of
+    // on the RCCL node.
+    vector<vector<char>> p2p_bufs;
+    bool host_mem = false; // schedule-only plans: buffers are host memory
+    void flush_p2p() {
+        if (host_mem) {
+            // no staging: the host buffers go to the transport as they are
+            vector<slu_host_p2p_op> q;
+            for (const Op &o : ops) {
+                const int me = grank(o.g), P = gsize(o.g);
+                if (me == o.root) {
+                    for (int m = 0; m < P; ++m)
+                        if (m != me && (o.mask >> m & 1)) {
+                            q.push_back({o.g, m, 1, 0, o.buf, (int64_t)o.bytes});
+                            sent += (double)o.bytes;
+                        }
+                } else if (o.mask >> me & 1) {
+                    SLU_REQUIRE(o.buf, "section of group %d root %d has no buffer", o.g, o.root);
+                    q.push_back({o.g, o.root, 0, 0, o.buf, (int64_t)o.bytes});
+                    recvd += (double)o.bytes;
+                }
+            }
+            if (!q.empty())
+                SLU_REQUIRE(c->host_p2p(c->host_ctx, (int)q.size(), q.data()) == 0,
+                            "host point-to-point group of %zu ops failed", q.size());
+            return;
+        }
+        HIPCHK(hipStreamSynchronize(s));
+        vector<slu_host_p2p_op> q;
+        vector<std::pair<int, size_t>> recv_of; // (op, q index) of each receive
+        p2p_bufs.resize(std::max(p2p_bufs.size(), ops.size()));
+        for (size_t i = 0; i < ops.size(); ++i) {
+            const Op &o = ops[i];
+            const int me = grank(o.g), P = gsize(o.g);
+            vector<char> &hb = p2p_bufs[i];
+            if (me == o.root) {
+                hb.resize(o.bytes);
+                HIPCHK(hipMemcpyAsync(hb.data(), o.buf, o.bytes, hipMemcpyDeviceToHost, s));
+                for (int m = 0; m < P; ++m)
+                    if (m != me && (o.mask >> m & 1)) {
+                        q.push_back({o.g, m, 1, 0, hb.data(), (int64_t)o.bytes});
+                        sent += (double)o.bytes;
+                    }
+            } else if (o.mask >> me & 1) {
+                SLU_REQUIRE(o.buf, "section of group %d root %d has no buffer", o.g, o.root);
+                hb.resize(o.bytes);
+                recv_of.push_back({(int)i, q.size()});
+                q.push_back({o.g, o.root, 0, 0, hb.data(), (int64_t)o.bytes});
+                recvd += (double)o.bytes;
+            }
+        }
+        HIPCHK(hipStreamSynchronize(s));
+        if (!q.empty())
+            SLU_REQUIRE(c->host_p2p(c->host_ctx, (int)q.size(), q.data()) == 0,
+                        "host point-to-point group of %zu ops failed", q.size());
+        for (auto &r : recv_of)
+            HIPCHK(hipMemcpyAsync(ops[r.first].buf, p2p_bufs[r.first].data(), ops[r.first].bytes,
+                                  hipMemcpyHostToDevice, s));
+        HIPCHK(hipStreamSynchronize(s));
+    }
     void flush() {
         if (ops.empty()) return;
-        if (c->host_fn) {
+        if (c->host_p2p) {
+            flush_p2p();
+        } else if (c->host_fn) {
             HIPCHK(hipStreamSynchronize(s));
             for (auto &o : ops) {
                 hbuf.resize(o.bytes);
@@ -201,6 +271,18 @@ struct Xport {
         vector<vector<i64>> out(P);
         if (P == 1) {
             out[0] = mine;
+            return out;
+        }
+        if (host_mem) { // the same broadcasts over host buffers
+            vector<i64> sz(P, 0);
+            sz[me] = (i64)mine.size();
+            for (int r = 0; r < P; ++r) bcast(g, r, &sz[r], sizeof(i64));
+            flush();
+            for (int r = 0; r < P; ++r) {
+                out[r] = r == me ? mine : vector<i64>(sz[r]);
+                bcast(g, r, out[r].data(), sz[r] * sizeof(i64));
+            }
+            flush();
             return out;
         }
         DevBuf<i64> dsz;
@@ -272,6 +354,7 @@ struct PlanBase {
     virtual void set_a_pattern(int64_t ncol, const int64_t *xa, const int64_t *asub) = 0;
     virtual void fill_a(const void *a, int on_device) = 0;
     virtual void refine(const void *b, void *x, int64_t ld, int nrhs, double *berr, int *steps) = 0;
+    virtual void check_exchange(int64_t *nsec, int64_t *nbytes) = 0;
     slu_plan_stats stats{};
 };
 
@@ -387,12 +470,35 @@ struct Plan : PlanBase {
         comm = c;
         if (o) opts = *o;
         xmode = Pr * Pc > 1;
-        SLU_REQUIRE(!xmode || (comm && (comm->world || comm->host_fn)),
+        SLU_REQUIRE(!xmode || (comm && (comm->world || comm->host_fn || comm->host_p2p)),
                     "a %dx%d grid needs a communicator (slu_comm_create)", Pr, Pc);
         if (xmode)
             SLU_REQUIRE(comm->nprow == Pr && comm->npcol == Pc && comm->iam == iam,
                         "communicator is for a %dx%d grid rank %d, plan for %dx%d rank %d",
                         comm->nprow, comm->npcol, comm->iam, Pr, Pc, iam);
+        dry = opts.schedule_only != 0;
+        if (dry)
+            SLU_REQUIRE(!xmode || comm->host_p2p,
+                        "a schedule-only plan of a grid needs the point-to-point host transport");
+        X.c = comm;
+        X.host_mem = dry;
+        if (dry) {
+            // host only (no HIP call): the layout, the index exchange, the
+            // levels and the per-level exchange sections, for
+            // slu_plan_check_exchange
+            int_t *hx = LU->Glu_persist->xsup;
+            nsupers = (int)(LU->Glu_persist->supno[n - 1] + 1);
+            xsup.assign(hx, hx + nsupers + 1);
+            nlc = (nsupers + Pc - 1) / Pc;
+            nlr = (nsupers + Pr - 1) / Pr;
+            value_layout();
+            build_local();
+            exchange_index();
+            exchange_needs();
+            compute_levels();
+            layout_values();
+            return;
+        }
         if (comm) HIPCHK(hipSetDevice(comm->device));
         // the panel stream carries the critical path (critical Schur tiles,
         // next level's diag LU / TRSM / exchanges): higher priority, so its
@@ -401,7 +507,6 @@ struct Plan : PlanBase {
         HIPCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
         HIPCHK(hipStreamCreateWithPriority(&stream, hipStreamNonBlocking, prio_lo));
         HIPCHK(hipStreamCreateWithPriority(&pstream, hipStreamNonBlocking, prio_hi));
-        X.c = comm;
         X.s = pstream;
         int_t *hx = LU->Glu_persist->xsup;
         nsupers = (int)(LU->Glu_persist->supno[n - 1] + 1);
@@ -439,9 +544,12 @@ struct Plan : PlanBase {
             pin_thread = std::thread([this] {
                 try {
                     HIPCHK(hipSetDevice(comm ? comm->device : 0));
+                    // get() frees slots of another size: never while a
+                    // run_d2h (which holds `use`) still copies through them
+                    std::lock_guard<std::mutex> in_use(pinned_pool(1).use);
                     pinned_pool(1).get(D2H_NS, D2H_SLOT);
                 } catch (const std::exception &e) {
-                    up_err = e.what();
+                    pin_err = e.what();
                 }
             });
         }
@@ -470,6 +578,87 @@ struct Plan : PlanBase {
             throw;
         }
         stats.t_plan_ms = ms_since(t0);
+    }
+
+    bool dry = false;  // schedule-only plan (opts.schedule_only): no device state
+
+    // Replays every level's exchange phases of factor() -- the diagonal
+    // packages, then the panels, issue() for issue() -- through the
+    // transport on host arenas.  Each section carries bytes derived from
+    // (level, group, root, mask, position), written by its root and checked
+    // by every receiver, so a section that goes to the wrong rank, in the
+    // wrong order or with the wrong size fails (or, with a missing send,
+    // hangs) here instead of on the RCCL node.
+    void check_exchange(int64_t *nsec, int64_t *nbytes) override {
+        SLU_REQUIRE(dry, "check_exchange needs a schedule-only plan");
+        vector<unsigned char> hd((size_t)std::max<i64>(dpk_total, 1) * sizeof(T)),
+            hp((size_t)std::max<i64>(pan_total, 1) * sizeof(T));
+        // bytes of the k-th section of root rank gr in phase ph of level L
+        // (an owner's diagonal package goes to its column and its row from
+        // one buffer, so the group is not part of it)
+        auto pat = [](size_t L, int ph, int gr, int k, size_t i) {
+            uint64_t h = (uint64_t)(L * 2 + ph) * 0x9E3779B97F4A7C15ull ^
+                         (uint64_t)(gr * 1031 + k) * 0xBF58476D1CE4E5B9ull ^
+                         (uint64_t)i * 0xD6E8FEB86659FD93ull;
+            return (unsigned char)(h ^ (h >> 29) ^ (h >> 43));
+        };
+        auto root_rank = [&](const Sec &sc) { // global rank of the section's root
+            return sc.g == G_ROW ? myrow * Pc + sc.root : sc.root * Pc + mycol;
+        };
+        i64 ns = 0, nb = 0;
+        for (size_t L = 0; L < levels.size(); ++L) {
+            const LevelRange &R = levels[L];
+            for (int ph = 0; ph < 2; ++ph) {
+                const vector<Sec> &secs = ph ? psecs : dsecs;
+                const int off = ph ? R.ps_off : R.ds_off, cnt = ph ? R.ps_n : R.ds_n;
+                unsigned char *arena = ph ? hp.data() : hd.data();
+                // k = position among the level phase's sections of (group, root)
+                vector<int> kth(cnt);
+                {
+                    std::map<std::pair<int, int>, int> seen;
+                    for (int i = 0; i < cnt; ++i) kth[i] = seen[{secs[off + i].g, secs[off + i].root}]++;
+                }
+                for (int i = off; i < off + cnt; ++i) {
+                    const Sec &sc = secs[i];
+                    const int me = sc.g == G_ROW ? mycol : myrow;
+                    const size_t bytes = (size_t)sc.cnt * sizeof(T);
+                    if (me == sc.root) {
+                        SLU_REQUIRE(sc.off >= 0, "root of a section without a buffer");
+                        for (size_t b = 0; b < bytes; ++b)
+                            arena[(size_t)sc.off * sizeof(T) + b] = pat(L, ph, root_rank(sc), kth[i - off], b);
+                    } else if (sc.off >= 0) {
+                        memset(arena + (size_t)sc.off * sizeof(T), 0, bytes);
+                    }
+                }
+                for (int i = off; i < off + cnt; ++i) {
+                    const Sec &sc = secs[i];
+                    X.section(sc.g, sc.root, sc.mask,
+                              sc.off >= 0 ? arena + (size_t)sc.off * sizeof(T) : nullptr,
+                              (size_t)sc.cnt * sizeof(T));
+                }
+                X.flush();
+                for (int i = off; i < off + cnt; ++i) {
+                    const Sec &sc = secs[i];
+                    const int me = sc.g == G_ROW ? mycol : myrow;
+                    if (me == sc.root || !(sc.mask >> me & 1)) continue;
+                    SLU_REQUIRE(sc.off >= 0, "level %zu: a section for this rank has no buffer", L);
+                    const size_t bytes = (size_t)sc.cnt * sizeof(T);
+                    for (size_t b = 0; b < bytes; ++b)
+                        SLU_REQUIRE(arena[(size_t)sc.off * sizeof(T) + b] ==
+                                        pat(L, ph, root_rank(sc), kth[i - off], b),
+                                    "level %zu: section (group %d root %d) byte %zu differs", L, sc.g,
+                                    sc.root, b);
+                    ++ns;
+                    nb += (i64)bytes;
+                }
+            }
+        }
+        // the final info reduction of factor()
+        vector<i64> mine(1, iam);
+        auto all = X.allgatherv(G_WORLD, mine);
+        for (int r = 0; r < Pr * Pc; ++r) SLU_REQUIRE(all[r].size() == 1 && all[r][0] == r, "info all-gather");
+        *nsec = ns;
+        *nbytes = nb;
     }
 
     bool prof = false; // SLU_PROFILE_PLAN: phase times of the plan build on stderr
@@ -1616,7 +1805,7 @@ struct Plan : PlanBase {
 
     // ---- host <-> HBM copies of the values (hostio.h)
     std::thread up_thread, pin_thread;
-    std::string up_err;
+    std::string up_err, pin_err; // one per helper thread (no shared writes)
     double up_ms = 0;
     bool host_current = false; // the host LUstruct holds what the device holds
 
@@ -1653,6 +1842,12 @@ struct Plan : PlanBase {
     void upload() override {
         const auto t0 = std::chrono::steady_clock::now();
         if (pin_thread.joinable()) pin_thread.join();
+        if (!pin_err.empty()) {
+            if (up_thread.joinable()) up_thread.join();
+            std::string e;
+            e.swap(pin_err);
+            throw Error(e);
+        }
         if (up_thread.joinable()) {
             up_thread.join();
             if (!up_err.empty()) {
@@ -2953,6 +3148,38 @@ slu_comm *slu_comm_create_host(slu_host_bcast_fn fn, void *ctx, int nprow, int n
     }
 }
 
+slu_comm *slu_comm_create_host_p2p(slu_host_p2p_fn fn, void *ctx, int nprow, int npcol, int iam,
+                                   int device) {
+    try {
+        SLU_REQUIRE(fn != nullptr, "point-to-point host transport needs a callback");
+        auto *c = new slu_comm;
+        c->nprow = nprow;
+        c->npcol = npcol;
+        c->iam = iam;
+        c->myrow = iam / npcol;
+        c->mycol = iam % npcol;
+        c->device = device;
+        c->host_p2p = fn;
+        c->host_ctx = ctx;
+        if (device >= 0) HIPCHK(hipSetDevice(device)); // -1: schedule-only plans, no GPU
+        return c;
+    } catch (const std::exception &e) {
+        set_last_error(e.what());
+        return nullptr;
+    }
+}
+
+int slu_comm_size(const slu_comm *c, int group) {
+    if (!c) return -1;
+    if (c->world) { // what RCCL itself reports for the communicator
+        int n = -1;
+        ncclComm_t cm = group == 0 ? c->world : group == 1 ? c->row : c->col;
+        if (ncclCommCount(cm, &n) != ncclSuccess) return -1;
+        return n;
+    }
+    return group == 0 ? c->nprow * c->npcol : group == 1 ? c->npcol : c->nprow;
+}
+
 void slu_comm_destroy(slu_comm *c) {
     if (!c) return;
     if (c->row) ncclCommDestroy(c->row);
@@ -3074,6 +3301,16 @@ int slu_plan_snapshot(slu_plan *p) {
 int slu_plan_restore(slu_plan *p) {
     try {
         p->impl->restore();
+        return 0;
+    } catch (const std::exception &e) {
+        set_last_error(e.what());
+        return -1;
+    }
+}
+
+int slu_plan_check_exchange(slu_plan *p, int64_t *nsections, int64_t *nbytes) {
+    try {
+        p->impl->check_exchange(nsections, nbytes);
         return 0;
     } catch (const std::exception &e) {
         set_last_error(e.what());

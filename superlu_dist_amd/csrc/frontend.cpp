@@ -258,7 +258,7 @@ int slu_order_nd_grid(int nx, int ny, int nz, int64_t *perm_c) {
 }
 
 slu_symb *slu_symbolic(const slu_csc *A, const int64_t *perm_c_in, int relax,
-                       int maxsup) {
+                       int maxsup, int flags) {
     int64_t n = A->n;
     if (maxsup < 1) maxsup = 256;
     if (relax > maxsup) relax = maxsup;
@@ -294,10 +294,9 @@ slu_symb *slu_symbolic(const slu_csc *A, const int64_t *perm_c_in, int relax,
         if (parent[j] >= 0) { nchild[parent[j]]++; size[parent[j]] += size[j]; }
 
     // supernode partition: relaxed subtrees, then fundamental chains.
-    // SLU_AMALG_MULTICHILD=1 (A/B): a chain may also continue through a
-    // column with several children (their structures are nested in it)
-    static const bool multichild =
-        getenv("SLU_AMALG_MULTICHILD") && atoi(getenv("SLU_AMALG_MULTICHILD"));
+    // SLU_SYMB_MULTICHILD: a chain may also continue through a column with
+    // several children (their structures are nested in it)
+    const bool multichild = (flags & SLU_SYMB_MULTICHILD) != 0;
     static const double AMALG_ZERO_FRAC =
         getenv("SLU_AMALG_ZERO") ? atof(getenv("SLU_AMALG_ZERO")) : 0.10;
     vector<int64_t> xsup;

@@ -231,8 +231,10 @@ extern "C" {
 
 // METIS_NodeND as SRC/get_perm_c.c:49-50 declares it (int_t arguments;
 // vwgt / options unused, as the reference passes NULL).  Returns 1
-// (METIS_OK), or -4 (METIS_ERROR) on bad input.
-int METIS_NodeND(int_t *nvtxs, int_t *xadj, int_t *adjncy, int_t *vwgt, int_t *options,
+// (METIS_OK), or -4 (METIS_ERROR) on bad input.  Exported only by the
+// opt-in libslu_mi355x_full.so (never by the drop-in libslu_mi355x.so),
+// and weak: a METIS linked statically into the program binds first.
+__attribute__((weak)) int METIS_NodeND(int_t *nvtxs, int_t *xadj, int_t *adjncy, int_t *vwgt, int_t *options,
                  int_t *perm, int_t *iperm) {
     (void)vwgt;
     (void)options;

@@ -589,12 +589,18 @@ void sp_colorder(superlu_dist_options_t *options, SuperMatrix *A, int_t *perm_c,
 // (freed by the reference's symbfact_SubFree / LU destructors with free()).
 int_t symbfact(superlu_dist_options_t *options, int pnum, SuperMatrix *A, int_t *perm_c,
                int_t *etree, Glu_persist_t *Glu_persist, Glu_freeable_t *Glu_freeable) {
-    (void)pnum;
     (void)perm_c;
     const NCPformat *S = (const NCPformat *)A->Store;
     try {
         const Result R = symbfact(A->nrow, A->ncol, S->colbeg, S->colend, S->rowind, etree,
                                   relax_of(options), maxsup_of(options));
+        if (!pnum && options->PrintStat == SLU_YES) { // SRC/symbfact.c:187-194
+            printf("\tMatrix size min_mn  %lld\n", (long long)std::min<I>(A->nrow, A->ncol));
+            printf("\tNonzeros in L       %lld\n", (long long)R.nnzL);
+            printf("\tNonzeros in U       %lld\n", (long long)R.nnzU);
+            printf("\tnonzeros in L+U     %lld\n", (long long)R.nnzLU);
+            printf("\tnonzeros in LSUB    %lld\n", (long long)R.lsub_size);
+        }
         const size_t n1 = A->ncol + 1;
         Glu_persist->xsup = copy_out<int_t>(R.xsup, n1);
         Glu_persist->supno = copy_out<int_t>(R.supno, n1);

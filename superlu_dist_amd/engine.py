@@ -10,7 +10,7 @@ import ctypes as C
 
 import numpy as np
 
-from .lib import HOST_BCAST_FN, EngineOpts, PlanStats, as_i64p, lib
+from .lib import HOST_BCAST_FN, HOST_P2P_FN, EngineOpts, PlanStats, as_i64p, lib
 
 SMACH_EPS = 5.9604644775390625e-08  # smach_dist("Epsilon"), SRC/smach_dist.c:64
 
@@ -55,6 +55,40 @@ class Comm:
             raise RuntimeError(lib().slu_last_error().decode())
         return self
 
+    @classmethod
+    def host_p2p(cls, nprow, npcol, iam, device, p2p):
+        """Point-to-point test transport: ``p2p(ops)`` receives the list of
+        (group, peer, is_send, uint8 numpy buffer) of one exchange phase --
+        exactly the ncclSend / ncclRecv pairs the RCCL transport issues, in
+        its order -- and must post them all before waiting for any."""
+        self = cls.__new__(cls)
+        self.nprow, self.npcol, self.iam = nprow, npcol, iam
+
+        def _cb(_ctx, nops, ops):
+            try:
+                lst = []
+                for i in range(nops):
+                    o = ops[i]
+                    arr = np.ctypeslib.as_array((C.c_uint8 * o.bytes).from_address(o.buf))
+                    lst.append((o.group, o.peer, bool(o.send), arr))
+                p2p(lst)
+                return 0
+            except Exception as e:  # noqa: BLE001 -- reported through the C status
+                import sys
+                print(f"host p2p group failed: {e!r}", file=sys.stderr)
+                return 1
+
+        self._cb = HOST_P2P_FN(_cb)
+        self.ptr = lib().slu_comm_create_host_p2p(self._cb, None, nprow, npcol, iam, device)
+        if not self.ptr:
+            raise RuntimeError(lib().slu_last_error().decode())
+        return self
+
+    def size(self, group=0):
+        """Ranks in the grid (0), my process row (1) or column (2); for RCCL
+        what ncclCommCount reports."""
+        return lib().slu_comm_size(self.ptr, group)
+
     @staticmethod
     def unique_id():
         buf = C.create_string_buffer(128)
@@ -70,17 +104,20 @@ class Comm:
 
 class Plan:
     def __init__(self, lu, comm=None, replace_tiny=False, timing=False, overlap_upload=False,
-                 overlap_download=False):
+                 overlap_download=False, schedule_only=False):
         """overlap_upload: the H2D copy of the values starts inside the
         constructor, beside the plan build (upload() waits for it);
         overlap_download: factor() writes each finished level back into the
-        host LUstruct while later levels run (download() is then a no-op)."""
+        host LUstruct while later levels run (download() is then a no-op);
+        schedule_only: host-only plan (no GPU needed) whose exchange schedule
+        check_exchange() replays through the communicator."""
         self.lu = lu
         o = EngineOpts()
         o.replace_tiny_pivot = int(bool(replace_tiny))
         o.timing = int(timing)
         o.overlap_upload = int(bool(overlap_upload))
         o.overlap_download = int(bool(overlap_download))
+        o.schedule_only = int(bool(schedule_only))
         err = C.create_string_buffer(1024)
         iam = lu.myrow * lu.npcol + lu.mycol
         self.comm = comm
@@ -164,6 +201,14 @@ class Plan:
                                         berr.ctypes.data_as(C.POINTER(C.c_double)),
                                         steps.ctypes.data_as(C.POINTER(C.c_int))))
         return xx, berr[:nrhs], steps[:nrhs]
+
+    def check_exchange(self):
+        """Schedule-only plans: replay every level's exchange phases of
+        factor() through the communicator, each received section checked
+        byte for byte (collective).  Returns (sections, bytes) received."""
+        ns, nb = C.c_int64(), C.c_int64()
+        self._chk(lib().slu_plan_check_exchange(self.ptr, C.byref(ns), C.byref(nb)))
+        return ns.value, nb.value
 
     def stats(self):
         st = PlanStats()

@@ -73,14 +73,21 @@ def nd_order(nx, ny, nz=1):
     return perm
 
 
+SLU_SYMB_MULTICHILD = 1
+
+
 class Symbolic:
-    def __init__(self, A, perm_c=None, relax=60, maxsup=256):
+    def __init__(self, A, perm_c=None, relax=60, maxsup=256, multichild=False):
+        """multichild: chain supernodes continue through columns with several
+        etree children (csrc/frontend.cpp; shortens the supernodal tree of
+        level-set nested dissections such as the library's METIS_NodeND)."""
         self.A = A
         pc = None
         if perm_c is not None:
             self._perm_in = np.ascontiguousarray(perm_c, dtype=np.int64)
             pc = as_i64p(self._perm_in)
-        self.ptr = lib().slu_symbolic(A.ptr, pc, relax, maxsup)
+        self.ptr = lib().slu_symbolic(A.ptr, pc, relax, maxsup,
+                                      SLU_SYMB_MULTICHILD if multichild else 0)
         self.n = A.n
         self.nsupers = lib().slu_symb_nsupers(self.ptr)
         self.xsup = np.empty(self.nsupers + 1, dtype=np.int64)

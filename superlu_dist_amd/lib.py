@@ -1,8 +1,12 @@
-"""ctypes binding of libslu_mi355x.so (include/slu_mi355x.h).
+"""ctypes binding of libslu_mi355x_full.so (include/slu_mi355x.h).
 
-The shared library is built in-tree by ``make -C superlu_dist_amd/csrc``
-(``__graft_entry__.build()``).  Nothing here falls back to Python or the CPU:
-a missing library raises immediately.
+Two libraries are built in-tree by ``make -C superlu_dist_amd/csrc``
+(``__graft_entry__.build()``) from the same objects: libslu_mi355x.so, the
+drop-in with exactly the reference pdgstrf.c.o symbol set (bound by
+``capi.dropin()``), and libslu_mi355x_full.so, which also exports the engine
+API, the front-end helpers and the opt-in reference-prototype extras.  This
+module binds the latter.  Nothing here falls back to Python or the CPU: a
+missing library raises immediately.
 """
 import ctypes as C
 import os
@@ -11,7 +15,8 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # SLU_LIB overrides the in-tree library (A/B comparisons of engine builds)
-LIB_PATH = os.environ.get("SLU_LIB") or os.path.join(_HERE, "lib", "libslu_mi355x.so")
+LIB_PATH = os.environ.get("SLU_LIB") or os.path.join(_HERE, "lib", "libslu_mi355x_full.so")
+DROPIN_PATH = os.path.join(os.path.dirname(LIB_PATH), "libslu_mi355x.so")
 
 SLU_D, SLU_S, SLU_Z = 0, 1, 2
 DTYPES = {SLU_D: np.float64, SLU_S: np.float32, SLU_Z: np.complex128}
@@ -23,6 +28,16 @@ c_intp = C.POINTER(C.c_int)
 
 # int (*)(void *ctx, int group, int root, void *buf, int64_t bytes)
 HOST_BCAST_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int64)
+
+
+class HostP2POp(C.Structure):
+    """slu_host_p2p_op: one send / receive of an exchange phase."""
+    _fields_ = [("group", C.c_int), ("peer", C.c_int), ("send", C.c_int), ("reserved", C.c_int),
+                ("buf", C.c_void_p), ("bytes", C.c_int64)]
+
+
+# int (*)(void *ctx, int nops, const slu_host_p2p_op *ops)
+HOST_P2P_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.POINTER(HostP2POp))
 
 
 class SluCsc(C.Structure):
@@ -43,7 +58,7 @@ class SluLuView(C.Structure):
 class EngineOpts(C.Structure):
     _fields_ = [("replace_tiny_pivot", C.c_int), ("timing", C.c_int), ("serial", C.c_int),
                 ("overlap_upload", C.c_int), ("overlap_download", C.c_int),
-                ("reserved", C.c_int * 3)]
+                ("schedule_only", C.c_int), ("reserved", C.c_int * 2)]
 
 
 class PlanStats(C.Structure):
@@ -96,7 +111,7 @@ def lib():
         "slu_symbfact_arrays": (None, [P, c_i64p, c_i64p, c_i64p, c_i64p, c_i64p, c_i64p]),
         "slu_symbfact_free": (None, [P]),
         "METIS_NodeND": (C.c_int, [c_i64p, c_i64p, c_i64p, c_i64p, c_i64p, c_i64p, c_i64p]),
-        "slu_symbolic": (P, [C.POINTER(SluCsc), c_i64p, C.c_int, C.c_int]),
+        "slu_symbolic": (P, [C.POINTER(SluCsc), c_i64p, C.c_int, C.c_int, C.c_int]),
         "slu_symb_free": (None, [P]),
         "slu_symb_nsupers": (C.c_int64, [P]),
         "slu_symb_arrays": (None, [P, c_i64p, c_i64p, c_i64p]),
@@ -113,6 +128,8 @@ def lib():
         "slu_comm_unique_id": (C.c_int, [P]),
         "slu_comm_create": (P, [P, C.c_int, C.c_int, C.c_int, C.c_int]),
         "slu_comm_create_host": (P, [HOST_BCAST_FN, P, C.c_int, C.c_int, C.c_int, C.c_int]),
+        "slu_comm_create_host_p2p": (P, [HOST_P2P_FN, P, C.c_int, C.c_int, C.c_int, C.c_int]),
+        "slu_comm_size": (C.c_int, [P, C.c_int]),
         "slu_comm_destroy": (None, [P]),
         "slu_plan_create": (P, [C.c_int, P, C.c_int, C.c_int, C.c_int, C.c_int, P,
                                 C.POINTER(EngineOpts), C.c_char_p, C.c_int]),
@@ -127,6 +144,7 @@ def lib():
         "slu_plan_restore": (C.c_int, [P]),
         "slu_plan_sync": (C.c_int, [P]),
         "slu_plan_set_timing": (C.c_int, [P, C.c_int, C.c_int]),
+        "slu_plan_check_exchange": (C.c_int, [P, c_i64p, c_i64p]),
         "slu_plan_destroy": (None, [P]),
         "slu_plan_get_stats": (C.c_int, [P, C.POINTER(PlanStats)]),
         "slu_last_error": (C.c_char_p, []),

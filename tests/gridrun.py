@@ -48,8 +48,24 @@ class GlooGrid:
         g = None if group == 0 else (self.row if group == 1 else self.col)
         self.dist.broadcast(t, src=self.global_root(group, root), group=g)
 
+    def p2p(self, ops):
+        """One exchange phase of the point-to-point transport: post every
+        send / receive (global ranks, one tag: pairs match in order, as
+        ncclSend / ncclRecv inside a group), then wait for all of them."""
+        import torch
+        works = []
+        for group, peer, send, arr in ops:
+            t = torch.from_numpy(arr)
+            other = self.global_root(group, peer)
+            if other == self.rank:
+                raise RuntimeError(f"p2p op with myself (group {group}, peer {peer})")
+            works.append(self.dist.isend(t, other) if send else self.dist.irecv(t, other))
+        for w in works:
+            w.wait()
 
-def _worker(rank, world, port, recipe, out_dir, device, fill=False, solve=False):
+
+def _worker(rank, world, port, recipe, out_dir, device, fill=False, solve=False,
+            transport="bcast"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     try:
         import torch.distributed as dist
@@ -71,8 +87,19 @@ def _worker(rank, world, port, recipe, out_dir, device, fill=False, solve=False)
             S = Symbolic(A, perm, relax, maxsup)
             lu = S.distribute(pr, pc, rank // pc, rank % pc)
         res = {}
-        if device is not None:
-            comm = Comm.host(pr, pc, rank, device, gg.bcast)
+        if transport == "schedule":  # no GPU: the exchange schedule over the p2p transport
+            comm = Comm.host_p2p(pr, pc, rank, -1, gg.p2p)
+            p = Plan(lu, comm=comm, schedule_only=True)
+            res["nsec"], res["nbytes"] = p.check_exchange()
+            st = p.stats()
+            res["nlevels"] = st["nlevels"]
+            del p
+        elif device is not None:
+            if transport == "p2p":
+                comm = Comm.host_p2p(pr, pc, rank, device, gg.p2p)
+            else:
+                comm = Comm.host(pr, pc, rank, device, gg.bcast)
+            assert comm.size(0) == pr * pc and comm.size(1) == pc and comm.size(2) == pr
             p = Plan(lu, comm=comm, replace_tiny=tiny)
             if fill and A is not None:  # values from A on the device (no LU upload), SamePattern refill
                 cp, ri, v = A.permuted(S.perm_c).arrays()
@@ -118,10 +145,14 @@ def _worker(rank, world, port, recipe, out_dir, device, fill=False, solve=False)
         raise
 
 
-def run_grid(recipe, pr, pc, out_dir, device=0, timeout=240, fill=False, solve=False):
+def run_grid(recipe, pr, pc, out_dir, device=0, timeout=240, fill=False, solve=False,
+             transport="bcast"):
     """Run ``recipe`` (picklable callable returning cases.build()-style
     tuples, or "refdump:<case>" for the per-rank LUstructs of a reference
     dump fixture) on a pr x pc grid; returns the per-rank result dicts.
+    transport: "bcast" (host-staged broadcasts, the drop-in's MPI path when
+    ranks share a GPU) or "p2p" (the RCCL transport's send / receive pairs,
+    host-staged over gloo isend / irecv).
 
     The parent never imports torch: torch bundles its own ROCm runtime, and a
     process that loads libslu_mi355x.so (system ROCm) before torch ends up
@@ -130,7 +161,8 @@ def run_grid(recipe, pr, pc, out_dir, device=0, timeout=240, fill=False, solve=F
     ctx = mp.get_context("spawn")
     world = pr * pc
     port = free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, recipe, str(out_dir), device, fill, solve))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, recipe, str(out_dir), device, fill,
+                                                solve, transport))
              for r in range(world)]
     for p in procs:
         p.start()

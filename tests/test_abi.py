@@ -1,7 +1,8 @@
 """The drop-in boundary: the mirror header reproduces the reference layouts
 byte for byte (tests/golden/abi_layout.json, measured from the reference
-headers by oracle/gen/make_abi_layout.sh), and libslu_mi355x.so exports every
-function include/*.h declares.  CPU only: no compute calls."""
+headers by oracle/gen/make_abi_layout.sh), libslu_mi355x.so exports exactly the
+reference's pdgstrf.c.o symbol set, and libslu_mi355x_full.so every function
+include/*.h declares.  CPU only: no compute calls."""
 import ctypes as C
 import json
 import os
@@ -30,13 +31,39 @@ def _declared_functions():
     return sorted(set(names))
 
 
-def test_library_exports_every_declared_symbol():
-    lib = C.CDLL(os.path.join(ROOT, "superlu_dist_amd", "lib", "libslu_mi355x.so"))
+# the symbol set of the reference's pdgstrf.c.o / psgstrf.c.o / pzgstrf.c.o
+# (measured with nm): the drop-in exports these and nothing else
+DROPIN_SYMBOLS = sorted(["pdgstrf", "psgstrf", "pzgstrf"] +
+                        [f"{t}scatter_{s}" for t in "dsz" for s in ("l", "l_1", "u")])
+
+
+def test_full_library_exports_every_declared_symbol():
+    lib = C.CDLL(os.path.join(ROOT, "superlu_dist_amd", "lib", "libslu_mi355x_full.so"))
     names = _declared_functions()
     assert {"pdgstrf", "psgstrf", "pzgstrf", "dscatter_l", "dscatter_l_1", "dscatter_u",
             "zscatter_u", "sscatter_l", "slu_plan_create", "slu_plan_factor"} <= set(names)
     missing = [n for n in names if not hasattr(lib, n)]
     assert not missing, missing
+
+
+@pytest.mark.skipif(shutil.which("nm") is None, reason="needs binutils nm")
+def test_dropin_library_exports_exactly_the_reference_symbol_set():
+    """libslu_mi355x.so defines exactly p[dsz]gstrf + [dsz]scatter_l/_l_1/_u
+    (SURVEY 8b); symbfact / sp_colorder / METIS_NodeND live only in the
+    opt-in libslu_mi355x_full.so, and there METIS_NodeND is weak."""
+    lib = os.path.join(ROOT, "superlu_dist_amd", "lib")
+    out = subprocess.run(["nm", "-D", "--defined-only", os.path.join(lib, "libslu_mi355x.so")],
+                         check=True, capture_output=True, text=True).stdout.split("\n")
+    syms = sorted(ln.split()[-1] for ln in out if ln.strip())
+    assert syms == DROPIN_SYMBOLS
+    full = subprocess.run(["nm", "-D", "--defined-only",
+                           os.path.join(lib, "libslu_mi355x_full.so")],
+                          check=True, capture_output=True, text=True).stdout
+    kinds = {ln.split()[-1]: ln.split()[-2] for ln in full.split("\n") if ln.strip()}
+    assert kinds["METIS_NodeND"] == "W"
+    assert kinds["symbfact"] == "T" and kinds["sp_colorder"] == "T"
+    assert all(k.startswith("slu_") or k in DROPIN_SYMBOLS or
+               k in ("symbfact", "sp_colorder", "METIS_NodeND") for k in kinds), kinds
 
 
 @pytest.mark.skipif(shutil.which("gcc") is None or not os.path.exists("/opt/conda/include/mpi.h"),

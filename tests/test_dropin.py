@@ -2,16 +2,16 @@
 EXAMPLE/p[dsz]drive.c, linked against libslu_mi355x.so FIRST and then the
 reference library with pdgstrf.o / psgstrf.o / pzgstrf.o removed
 (oracle/_ref/p?drive_mi355x, built by `make -C oracle dropin`), run the
-reference's whole pipeline -- matrix read, equilibration, MC64, MMD, OUR
-sp_colorder / symbfact (csrc/symbolic.cpp), the reference pddistribute, OUR
-p?gstrf, the reference pdgstrs / pdgsrfs -- and must solve
-as accurately as the same drivers linked with the reference factorization
-(oracle/_ref/p?drive_ref).
+reference's whole pipeline -- matrix read, equilibration, MC64, MMD, the
+reference sp_colorder / symbfact / pddistribute, OUR p?gstrf, the reference
+pdgstrs / pdgsrfs -- and must solve as accurately as the same drivers linked
+with the reference factorization (oracle/_ref/p?drive_ref).  The opt-in
+libslu_mi355x_full.so (p?drive_mi355x_full) also replaces sp_colorder /
+symbfact and provides METIS_NodeND for the drivers' default ordering.
 
 GPU: 1 rank (1x1 grid), and 4 ranks on a 2x2 grid sharing the box's one GPU
 (the library then carries the panel broadcasts over MPI instead of RCCL).
-CPU: the link itself (our pdgstrf, symbfact and sp_colorder are the ones the
-binary binds).
+CPU: the links themselves (which symbols each binary binds from where).
 """
 import os
 import re
@@ -46,17 +46,34 @@ def _run(exe, nprocs, args, matrix, timeout=240):
     return max(errs), (float(m.group(1)) if m else None), out
 
 
-@pytest.mark.skipif(not _have("pddrive_mi355x"), reason="drop-in drivers not built")
-def test_dropin_driver_binds_our_pdgstrf():
-    exe = os.path.join(REF, "pddrive_mi355x")
+def _binding(exe):
+    exe = os.path.join(REF, exe)
     dyn = subprocess.run(["readelf", "-d", exe], capture_output=True, text=True).stdout
-    assert "libslu_mi355x.so" in dyn
     und = subprocess.run(["nm", "-D", "--undefined-only", exe], capture_output=True,
                          text=True).stdout.split()
     defined = subprocess.run(["nm", "--defined-only", exe], capture_output=True, text=True).stdout
+    return dyn, und, defined
+
+
+@pytest.mark.skipif(not _have("pddrive_mi355x"), reason="drop-in drivers not built")
+def test_dropin_driver_binds_our_pdgstrf():
+    """Default drop-in: pdgstrf comes from libslu_mi355x.so, the symbolic
+    factorization stays the reference's own (linked from the archive)."""
+    dyn, und, defined = _binding("pddrive_mi355x")
+    assert "libslu_mi355x.so" in dyn and "libslu_mi355x_full.so" not in dyn
+    assert "pdgstrf" in und                          # resolved at load time from the library
+    assert not re.search(r"\bT pdgstrf\b", defined)  # no reference copy inside
+    for sym in ("symbfact", "sp_colorder", "pddistribute"):
+        assert sym not in und and re.search(rf"\bT {sym}\b", defined), sym
+
+
+@pytest.mark.skipif(not _have("pddrive_mi355x_full"), reason="opt-in drivers not built")
+def test_optin_driver_binds_our_symbolic():
+    dyn, und, defined = _binding("pddrive_mi355x_full")
+    assert "libslu_mi355x_full.so" in dyn
     for sym in ("pdgstrf", "symbfact", "sp_colorder", "METIS_NodeND"):
-        assert sym in und                  # resolved at load time from libslu_mi355x.so
-        assert not re.search(rf"\bT {sym}\b", defined)   # no reference copy inside
+        assert sym in und, sym                       # from libslu_mi355x_full.so
+        assert not re.search(rf"\bT {sym}\b", defined)
 
 
 CASES = [
@@ -83,7 +100,7 @@ def test_reference_driver_with_our_factorization(drv, matrix, extra, nprocs, gri
 
 
 @pytest.mark.gpu
-@pytest.mark.skipif(not _have("pddrive_mi355x", "pddrive_ref"), reason="drivers not built")
+@pytest.mark.skipif(not _have("pddrive_mi355x_full", "pddrive_ref"), reason="drivers not built")
 @pytest.mark.parametrize("drv,matrix", [("pddrive", "g20.rua"), ("pddrive", "big.rua"),
                                         ("pzdrive", "cg20.cua")])
 def test_reference_driver_default_ordering_through_our_metis(drv, matrix):
@@ -92,6 +109,6 @@ def test_reference_driver_default_ordering_through_our_metis(drv, matrix):
     only the library's nested dissection can serve it; the all-reference
     driver runs MMD (-q 2) for the accuracy yardstick."""
     ref_err, _, _ = _run(f"{drv}_ref", 1, ["-r", "1", "-c", "1", "-q", "2"], matrix)
-    my_err, _, out = _run(f"{drv}_mi355x", 1, ["-r", "1", "-c", "1"], matrix)
+    my_err, _, out = _run(f"{drv}_mi355x_full", 1, ["-r", "1", "-c", "1"], matrix)
     print(f"{drv} {matrix} METIS_AT_PLUS_A via the library: {my_err:.3e} (reference, MMD: {ref_err:.3e})")
     assert my_err <= max(10 * ref_err, 1e-12), (my_err, ref_err)

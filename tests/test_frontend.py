@@ -87,3 +87,32 @@ def test_bufmax_and_comm_schedule_consistent():
         assert lu.ToRecv.min() >= 0 and lu.ToRecv.max() <= 2
         tsr = lu.to_sendr()
         assert set(np.unique(tsr)) <= {-1, 1}
+
+
+@pytest.mark.parametrize("dims", [(12, 12, 12), (9, 11, 7)])
+def test_multichild_partition_holds_all_fill(dims):
+    """Symbolic(multichild=True) on the library's METIS_NodeND ordering (the
+    bench's --ordering graph): fewer supernodes than the default partition,
+    and a structure that holds every fill entry -- the oracle factorization
+    on it solves A x = b to backward error ~eps (a missing fill position
+    would drop an update and spoil the solution).  CPU only."""
+    import pyoracle
+    from lusolve import backward_error, solve_1x1
+    from superlu_dist_amd.symbolic import at_plus_a, metis_nodend
+    A = Csc.stencil(STENCIL_3D7, *dims)
+    cp, ri, _ = A.arrays()
+    perm = metis_nodend(A.n, *at_plus_a(A.n, cp, ri))[0]
+    S0 = Symbolic(A, perm, 60, 256)
+    S = Symbolic(A, perm, 60, 256, multichild=True)
+    assert S.nsupers <= S0.nsupers
+    lu = S.distribute()
+    o = pyoracle.oracle_factor([lu], 1, 1, A.n, False, cases.anorm(A))
+    assert o["info"] == 0
+    xt = np.random.default_rng(2).standard_normal(A.n)
+    B = A.permuted(S.perm_c)
+    bcp, bri, bv = B.arrays()
+    b = np.zeros(A.n)
+    for j in range(A.n):
+        b[bri[bcp[j]:bcp[j + 1]]] += bv[bcp[j]:bcp[j + 1]] * xt[j]
+    x = solve_1x1(lu, b)
+    assert backward_error(A, S.perm_c, x, b) < 1e-14

@@ -153,3 +153,43 @@ def test_gpu_overlapped_upload_download(slot_kb, dtype, monkeypatch):
     pyoracle.oracle_factor([ref], 1, 1, A.n, False, an)
     err = cases.factor_error([gpu], [(ref.Lval[:-1], ref.Uval[:-1])])
     assert err < TOL[dtype], err
+
+
+def _graph_case(kind, dims, dtype):
+    from superlu_dist_amd.symbolic import at_plus_a, metis_nodend
+    kw = dict(diag=6 - 0.25, diag_im=-0.0025) if dtype == 2 else {}
+    A = Csc.stencil(kind, *dims, dtype=dtype, **kw)
+    cp, ri, _ = A.arrays()
+    return A, metis_nodend(A.n, *at_plus_a(A.n, cp, ri))[0]
+
+
+@pytest.mark.parametrize("kind,dims,dtype", [
+    (STENCIL_3D7, (16, 16, 16), 0),
+    (STENCIL_3D7, (24, 24, 24), 0),    # 128x128 Schur tiles
+    (STENCIL_3D27, (14, 14, 14), 1),
+    (STENCIL_3D7, (12, 12, 12), 2),
+])
+def test_gpu_graph_ordering_multichild_matches_oracle(kind, dims, dtype):
+    """The bench's --ordering graph configuration: the library's
+    METIS_NodeND on A'+A and the multi-child chain partition
+    (Symbolic(multichild=True)); factors against the oracle, then the solve
+    with the GPU factors (backward and forward error)."""
+    A, perm = _graph_case(kind, dims, dtype)
+    S = Symbolic(A, perm, 60, 256, multichild=True)
+    gpu, ref = S.distribute(), S.distribute()
+    an = cases.anorm(A)
+    info, tiny, st = factor_lustruct(gpu, anorm=an)
+    o = pyoracle.oracle_factor([ref], 1, 1, A.n, False, an)
+    assert info == o["info"] == 0
+    err = cases.factor_error([gpu], [(ref.Lval, ref.Uval)])
+    assert err < TOL[dtype], err
+    assert abs(st["schur_flops"] + st["panel_flops"] - o["flops"]) <= 1e-9 * o["flops"] + 10
+    if dtype == 0:
+        xt = np.random.default_rng(3).standard_normal(A.n)
+        cp, ri, v = A.permuted(S.perm_c).arrays()
+        b = np.zeros(A.n)
+        for j in range(A.n):
+            b[ri[cp[j]:cp[j + 1]]] += v[cp[j]:cp[j + 1]] * xt[j]
+        x = solve_1x1(gpu, b)
+        assert backward_error(A, S.perm_c, x, b) < 1e-14
+        assert np.abs(x - xt).max() / np.abs(xt).max() < 1e-10

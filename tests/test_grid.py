@@ -32,6 +32,36 @@ def test_gloo_grid_groups_cpu(tmp_path):
         assert int(o["col_root"]) == 1 * 2 + c       # column broadcast from row 1
 
 
+REFDUMP_GRIDS = ["refdump_big_2x2_d", "refdump_big_1x2_s", "refdump_cd2d_24_2x2_d",
+                 "refdump_cd2d_20_2x1_z", "refdump_g20_2x3_small_d", "refdump_lap3d_12_2x2_d",
+                 "refdump_zeropiv2_2x2_d", "refdump_cg20_2x2_z"]
+
+
+@pytest.mark.parametrize("case", REFDUMP_GRIDS + ["stencil_3d7_12_2x4", "stencil_3d27_8_2x2"])
+def test_exchange_schedule_through_p2p_transport_cpu(case, tmp_path):
+    """No GPU: every rank builds a schedule-only plan over the point-to-point
+    host transport (the RCCL send / receive pairs, gloo isend / irecv) --
+    the plan-time index / need / edge all-gathers go through it -- and then
+    replays every level's diagonal-package and panel exchange of factor()
+    with patterned bytes that each receiver checks.  A section sent to the
+    wrong rank, in the wrong order or with the wrong size fails; one that is
+    never sent hangs until run_grid's timeout."""
+    if case.startswith("refdump_"):
+        name = case[len("refdump_"):]
+        from refdump import Fixture
+        fx = Fixture(name)
+        pr, pc = fx.pr, fx.pc
+        rec = f"refdump:{name}"
+    else:
+        _, kind, nx, g = case.split("_")
+        pr, pc = int(g[0]), int(g[2])
+        kind = STENCIL_3D7 if kind == "3d7" else STENCIL_3D27
+        rec = functools.partial(_stencil_recipe, kind, (int(nx),) * 3, 0, (pr, pc), 60, 256)
+    out = run_grid(rec, pr, pc, tmp_path, device=None, transport="schedule", timeout=120)
+    assert len({int(o["nlevels"]) for o in out}) == 1        # identical levels on every rank
+    assert sum(int(o["nsec"]) for o in out) > 0
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("name,fill", [(n, False) for n in GRID_CASES] +
                          [("lap3d_10_2x4_small_d", True), ("cg20_2x2_small_z", True)])
@@ -57,6 +87,7 @@ def _stencil_recipe(kind, dims, dtype, grid, relax, maxsup):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("transport", ["bcast", "p2p"])
 @pytest.mark.parametrize("kind,dims,dtype,grid,relax,maxsup", [
     (STENCIL_3D7, (16, 16, 16), 0, (2, 2), 60, 256),
     (STENCIL_3D7, (20, 20, 20), 0, (2, 4), 60, 256),   # 128x128 Schur tiles on 8 ranks
@@ -64,10 +95,10 @@ def _stencil_recipe(kind, dims, dtype, grid, relax, maxsup):
     (STENCIL_3D27, (12, 12, 12), 1, (2, 2), 60, 256),
     (STENCIL_3D7, (10, 10, 10), 2, (2, 1), 60, 256),
 ])
-def test_grid_matches_oracle_stencil(kind, dims, dtype, grid, relax, maxsup, tmp_path):
+def test_grid_matches_oracle_stencil(kind, dims, dtype, grid, relax, maxsup, transport, tmp_path):
     rec = functools.partial(_stencil_recipe, kind, dims, dtype, grid, relax, maxsup)
     pr, pc = grid
-    out = run_grid(rec, pr, pc, tmp_path, device=0)
+    out = run_grid(rec, pr, pc, tmp_path, device=0, transport=transport)
     A, perm, dt, _, _, _, _ = rec()
     S = Symbolic(A, perm, relax, maxsup)
     lus = [S.distribute(pr, pc, r, c) for r in range(pr) for c in range(pc)]

@@ -108,11 +108,15 @@ def test_gpu_dropin_pdgstrf_on_reference_lustructs(name):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("transport", ["bcast", "p2p"])
 @pytest.mark.parametrize("name", GRIDS)
-def test_gpu_grid_on_reference_lustructs(name, tmp_path):
+def test_gpu_grid_on_reference_lustructs(name, transport, tmp_path):
+    """bcast: host-staged broadcasts (the drop-in's MPI path when ranks share
+    a GPU); p2p: the RCCL transport's send / receive pairs in its order,
+    host-staged over gloo isend / irecv."""
     from gridrun import run_grid
     fx = Fixture(name)
-    out = run_grid(f"refdump:{name}", fx.pr, fx.pc, tmp_path, device=0)
+    out = run_grid(f"refdump:{name}", fx.pr, fx.pc, tmp_path, device=0, transport=transport)
     assert all(int(o["info"]) == fx.info for o in out)
     assert sum(int(o["tiny"]) for o in out) == fx.tiny
     if fx.info == 0:

@@ -106,11 +106,13 @@ def test_grid_fixture_rhs_reassembles(name):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("transport", ["bcast", "p2p"])
 @pytest.mark.parametrize("name", GRID_CASES)
-def test_gpu_grid_solve_matches_reference(name, tmp_path):
+def test_gpu_grid_solve_matches_reference(name, transport, tmp_path):
     from gridrun import run_grid
     fx = Fixture(name)
-    out = run_grid(f"refdump:{name}", fx.pr, fx.pc, tmp_path, device=0, solve=True)
+    out = run_grid(f"refdump:{name}", fx.pr, fx.pc, tmp_path, device=0, solve=True,
+                   transport=transport)
     _, _, _, _, _, xnr, xtrue = fx.full_rhs()
     xref = np.concatenate([fx.arr(p, "x") for p in sorted(range(fx.nranks),
                                                         key=lambda q: fx.meta["ranks"][q]["fst_row"])])
