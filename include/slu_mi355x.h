@@ -378,6 +378,21 @@ void *slu_lustruct_build(int dtype, int64_t n, int64_t nsupers, const int_t *xsu
                          int64_t Uval_cnt, const int64_t *Uvoff, const int *ToRecv,
                          const int *ToSendD, const int *ToSendR, const int_t *bufmax);
 
+/* The reference's structural pddistribute (the first-time
+ * branch of SRC/pddistribute.c:673-1340, 1460-1509, ToRecv / ToSendD /
+ * ToSendR :767-801, bufmax :2370 as the MAX over the whole grid): this rank's
+ * LUstruct (freed by slu_lustruct_free) from the symbolic factorization
+ * (xsup / supno of Glu_persist; xlsub / lsub / xusub / usub of Glu_freeable,
+ * as symbfact leaves them) and A in the LUstruct's coordinates (CSC of
+ * Pc Pr diag(R) A diag(C) Pc^T; every rank may pass all of A, entries of
+ * other ranks' blocks are skipped).  Index arrays, block order and values
+ * are the reference's bit for bit (tests/test_distribute.py).  NULL on error
+ * (slu_last_error). */
+void *slu_distribute_glu(int dtype, int64_t n, const int_t *xsup, const int_t *supno,
+                         const int_t *xlsub, const int_t *lsub, const int_t *xusub,
+                         const int_t *usub, const int64_t *xa, const int64_t *asub,
+                         const void *a, int nprow, int npcol, int myrow, int mycol);
+
 /* Permuted-matrix helpers for tests: B = P*A*P^T in CSC. */
 slu_csc *slu_permute(const slu_csc *A, const int64_t *perm_c);
 

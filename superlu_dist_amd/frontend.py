@@ -165,6 +165,29 @@ class LUStruct:
         self._wrap(ptr, dtype, n, ns, nprow, npcol, myrow, mycol)
         return self
 
+    @classmethod
+    def from_glu(cls, symb, colptr, rowind, values, dtype, nprow=1, npcol=1, myrow=0, mycol=0):
+        """This rank's LUstruct as the reference's pddistribute builds it
+        (csrc/distribute.cpp) from a reference-exact symbolic factorization
+        ``symb`` (superlu_dist_amd.symbolic.Symb) and A in the LUstruct's
+        coordinates (CSC colptr / rowind / values of Pc Pr A Pc^T)."""
+        self = cls.__new__(cls)
+        self.symb = None
+        i64 = lambda a: np.ascontiguousarray(a, dtype=np.int64)  # noqa: E731
+        xsup, supno = i64(symb.xsup), i64(symb.supno)
+        xl, ls, xu, us = i64(symb.xlsub), i64(symb.lsub), i64(symb.xusub), i64(symb.usub)
+        cp, ri = i64(colptr), i64(rowind)
+        v = np.ascontiguousarray(values, dtype=DTYPES[dtype])
+        n = len(cp) - 1
+        ptr = lib().slu_distribute_glu(dtype, n, as_i64p(xsup), as_i64p(supno), as_i64p(xl),
+                                       as_i64p(ls), as_i64p(xu), as_i64p(us), as_i64p(cp),
+                                       as_i64p(ri), v.ctypes.data_as(C.c_void_p), nprow, npcol,
+                                       myrow, mycol)
+        if not ptr:
+            raise RuntimeError("slu_distribute_glu: " + lib().slu_last_error().decode())
+        self._wrap(ptr, dtype, n, symb.nsupers, nprow, npcol, myrow, mycol)
+        return self
+
     def _wrap(self, ptr, dtype, n, nsupers, nprow, npcol, myrow, mycol):
         self.ptr = ptr
         self.dtype = dtype

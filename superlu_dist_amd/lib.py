@@ -119,6 +119,8 @@ def lib():
         "slu_symb_struct_sizes": (None, [P, c_i64p]),
         "slu_distribute": (P, [P, C.POINTER(SluCsc), C.c_int, C.c_int, C.c_int, C.c_int]),
         "slu_lustruct_free": (None, [P, C.c_int]),
+        "slu_distribute_glu": (P, [C.c_int, C.c_int64, c_i64p, c_i64p, c_i64p, c_i64p, c_i64p,
+                                   c_i64p, c_i64p, c_i64p, P, C.c_int, C.c_int, C.c_int, C.c_int]),
         "slu_lustruct_build": (P, [C.c_int, C.c_int64, C.c_int64, c_i64p, c_i64p, C.c_int,
                                    C.c_int, c_i64p, C.c_int64, c_i64p, P, C.c_int64, c_i64p,
                                    c_i64p, C.c_int64, c_i64p, P, C.c_int64, c_i64p, c_intp,
