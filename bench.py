@@ -81,7 +81,7 @@ def grid_shape(n):
     return {1: (1, 1), 2: (1, 2), 4: (2, 2), 8: (2, 4), 16: (4, 4)}.get(n, (1, n))
 
 
-def build_lu(workload, nx, pr, pc, myrow, mycol, ordering="grid"):
+def build_lu(workload, nx, pr, pc, myrow, mycol, ordering="grid", symbolic="reference"):
     from superlu_dist_amd.frontend import STENCIL_2D5, STENCIL_3D7, STENCIL_3D27, Csc, Symbolic, nd_order
     kind, dims, dtype, diag, diag_im = WORKLOADS[workload][:5]
     kind = {"2d5": STENCIL_2D5, "3d7": STENCIL_3D7, "3d27": STENCIL_3D27}[kind]
@@ -95,12 +95,18 @@ def build_lu(workload, nx, pr, pc, myrow, mycol, ordering="grid"):
         perm = metis_nodend(A.n, *at_plus_a(A.n, cp, ri))[0]
     else:
         perm = nd_order(*d)
-    # graph ordering: chains through multi-child columns in the front-end's
-    # partition (the level-set separators hang their far-side components
-    # along the chain; 100^3: 277 -> 182 ms)
-    S = Symbolic(A, perm, 60, 256, multichild=ordering == "graph")
+    if symbolic == "reference":
+        # what pdgssvx hands pdgstrf for this perm_c (ColPerm = MY_PERMC):
+        # the reference's sp_colorder + symbfact, laid out by its pddistribute
+        # (bit-exact restatements, csrc/symbolic.cpp, csrc/distribute.cpp)
+        S = Symbolic(A, perm, 60, 256, reference=True)
+    else:
+        # the library front-end's amalgamated partition (chains with <= 10 %
+        # explicit zeros; graph ordering: chains through multi-child columns,
+        # DESIGN §11)
+        S = Symbolic(A, perm, 60, 256, multichild=ordering == "graph")
     lu = S.distribute(pr, pc, myrow, mycol)
-    return A, S, lu
+    return A, S, lu, perm
 
 
 def next_rows(plan, A, S, anorm, one_step):
@@ -151,7 +157,7 @@ def next_rows(plan, A, S, anorm, one_step):
                        "fwd_err": float(np.abs(xr - xt).max() / np.abs(xt).max())}}
 
 
-def abi_leg(lu, anorm, factor_ms):
+def abi_leg(lu, anorm, factor_ms, fingerprint=None):
     """utime[FACT] of the drop-in path: pdgstrf called through the C ABI the
     way pdgssvx calls it (SRC/pdgssvx.c:1174-1180) -- plan build, H2D of the
     host LUstruct's values, factorization and D2H of the factors into the
@@ -171,6 +177,9 @@ def abi_leg(lu, anorm, factor_ms):
         rv, info, st = capi.pxgstrf(lu, anorm)
         walls.append((time.perf_counter() - t) * 1e3)
         assert rv == 0 and info == 0, (rv, info)
+    # the drop-in's factors, fingerprinted for the parity check of the
+    # cpu_baseline leg (oracle/blocksum.h) while they are in the host arrays
+    sums = fingerprint(lu) if fingerprint else None
     Lf = lu.Lval.copy()
     lu.Lval[:] = L0
     lu.Uval[:] = U0
@@ -203,7 +212,7 @@ def abi_leg(lu, anorm, factor_ms):
             "pcie_floor_ms": round((st["h2d_bytes"] + st["d2h_bytes"]) / pcie / 1e6, 1),
             "factors_rel_diff_abi_vs_engine": same,
             "note": "factor_ms in bar_ms = ms_per_step (HBM-resident); h2d = staged H2D of the "
-                    "L/U values (hostio.h); D2H rides under the factorization"}
+                    "L/U values (hostio.h); D2H rides under the factorization"}, sums
 
 
 def one_norm(A):
@@ -212,31 +221,50 @@ def one_norm(A):
     return float(np.add.reduceat(np.abs(val).astype(np.float64), colptr[:-1]).max())
 
 
-def cpu_baseline(nx_sample, nranks, timeout):
+def gpu_fingerprints(lu):
+    """cpu_baseline leg, the checker: per-block fingerprints (max |v| and a
+    fixed random projection, oracle/blocksum.h) of the factors in ``lu``'s
+    host arrays, keyed by global block, to compare with the reference's."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+    return pyoracle.blocksums(lu)
+
+
+def cpu_baseline(A, perm, nx, nranks, timeout, flops, symbolic="reference", gpu_sums=None):
     """Reference pdgstrf (oracle/_ref/ref_pdgstrf: /root/reference sources,
-    MPICH + sequential MKL, one rank per core) on the sample problem."""
+    MPICH + sequential MKL, one rank per core) on the same matrix, ordering
+    and LUstruct (the reference's own symbolic stage for symbolic ==
+    "reference"), and -- given the GPU factors' fingerprints -- the parity of
+    the full-size factors: the reference's per-block fingerprints from its
+    own grid against the GPU's (oracle/pyoracle.compare_blocksums)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle
     if not pyoracle.have_reference_harness():
-        return None
-    from superlu_dist_amd.frontend import STENCIL_3D7, Csc, Symbolic, nd_order
+        return None, None
     pr, pc = grid_shape(nranks)
-    A = Csc.stencil(STENCIL_3D7, nx_sample, nx_sample, nx_sample)
-    perm = nd_order(nx_sample, nx_sample, nx_sample)
-    S = Symbolic(A, perm, 60, 256)
-    flops = S.flops()["total"]
     try:
         st, _ = pyoracle.run_reference(A, perm, pr, pc, relax=60, maxsup=256, lookahead=10,
-                                       want_factors=False, timeout=timeout)
+                                       want_factors=False, timeout=timeout,
+                                       symb_flags=2 if symbolic == "reference" else 0,
+                                       want_blocksums=gpu_sums is not None)
     except Exception as e:  # noqa: BLE001
         print(f"[bench] cpu baseline failed: {e}", file=sys.stderr)
-        return None
+        return None, None
     t = st["time_best"]
-    return {"value": round(flops / t / 1e9, 2), "unit": "GFLOP/s", "cores": pr * pc,
-            "kind": "reference",
-            "sample": f"reference pdgstrf (oracle/_ref) on 3D 7-pt Laplacian {nx_sample}^3 "
-                      f"(n={nx_sample**3}, {flops:.3e} flops), {pr}x{pc} MPI ranks x 1 thread, "
-                      f"MKL sequential; factor time {t:.2f} s"}
+    parity = None
+    if gpu_sums is not None:
+        parity = pyoracle.compare_blocksums(gpu_sums, st["blocksums"])
+        parity.update({"tolerance": 1e-12, "ok": bool(parity["match"] and parity["rel_err"] <= 1e-12),
+                       "against": f"reference pdgstrf on a {pr}x{pc} grid (oracle/_ref/ref_pdgstrf)",
+                       "gpu_factors": "drop-in pdgstrf (C ABI) factors, 1x1",
+                       "method": "per-block fingerprints keyed by global (ib, jb): max|v| and a "
+                                 "fixed pseudo-random projection (oracle/blocksum.h); rel_err = "
+                                 "max over blocks of max(|d maxabs|, |d proj|/sqrt(cnt)) / max|ref|"})
+    return ({"value": round(flops / t / 1e9, 2), "unit": "GFLOP/s", "cores": pr * pc,
+             "kind": "reference",
+             "sample": f"reference pdgstrf (oracle/_ref) on the same 3D 7-pt Laplacian {nx}^3 "
+                       f"and LUstruct (n={nx**3}, {flops:.3e} flops), {pr}x{pc} MPI ranks x 1 "
+                       f"thread, MKL sequential; factor time {t:.2f} s"}, parity)
 
 
 def main():
@@ -250,7 +278,10 @@ def main():
     ap.add_argument("--ordering", choices=["grid", "graph"], default="grid",
                     help="grid: geometric nested dissection of the stencil grid (the headline "
                          "configuration); graph: the library's METIS_NodeND on A'+A")
-    ap.add_argument("--cpu-sample", type=int, default=100)
+    ap.add_argument("--symbolic", choices=["reference", "frontend"], default="reference",
+                    help="reference: pdgssvx's own sp_colorder + symbfact + pddistribute (the "
+                         "LUstruct the reference hands pdgstrf for this perm_c; headline); "
+                         "frontend: the library front-end's amalgamated supernodes")
     ap.add_argument("--cpu-ranks", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-next", action="store_true",
@@ -320,7 +351,8 @@ def main():
 
     t0 = time.time()
     log(f"front-end {args.workload} nx={args.nx} grid {pr}x{pc}")
-    A, S, lu = build_lu(args.workload, args.nx, pr, pc, myrow, mycol, args.ordering)
+    A, S, lu, perm = build_lu(args.workload, args.nx, pr, pc, myrow, mycol, args.ordering,
+                              args.symbolic)
     t_front = time.time() - t0
     log(f"front-end {t_front:.1f} s, {S.nsupers} supernodes")
     if world == 1:
@@ -387,12 +419,14 @@ def main():
     if world == 1 and not args.no_next and not args.roofline_only:
         log("next rows (fill / solve / refine)")
         nxt = next_rows(plan, A, S, anorm, one_step)
-    abi = None
+    abi = gpu_sums = None
+    want_cpu = rank == 0 and world == 1 and not args.no_cpu and not args.roofline_only
     if world == 1 and not args.no_abi and not args.roofline_only:
         t_step_local = float(np.mean(times)) * 1e3
         del plan
         log("drop-in pdgstrf leg (utime[FACT])")
-        abi = abi_leg(lu, anorm, t_step_local)
+        abi, gpu_sums = abi_leg(lu, anorm, t_step_local,
+                                fingerprint=gpu_fingerprints if want_cpu else None)
     if args.roofline_only:
         if rank == 0:
             print(json.dumps({"roofline_only": True, "t_schur_big_ms": sst["t_schur_big_ms"],
@@ -439,10 +473,11 @@ def main():
                 "serial_factor_ms": round(sst["t_total_ms"], 3),
                 "all_schur_tflops": round(st["schur_flops"] / (acc["t_schur_ms"] / 1e3 / K) / 1e12,
                                           3) if acc["t_schur_ms"] else None}
-        cpu = None
-        if not args.no_cpu and world == 1:
-            log(f"cpu baseline (reference pdgstrf, {args.cpu_sample}^3, {args.cpu_ranks} ranks)")
-            cpu = cpu_baseline(args.cpu_sample, args.cpu_ranks, timeout=600)
+        cpu = parity = None
+        if want_cpu:
+            log(f"cpu baseline (reference pdgstrf, {args.nx}^3, {args.cpu_ranks} ranks)")
+            cpu, parity = cpu_baseline(A, perm, args.nx, args.cpu_ranks, 900, flops_all,
+                                       args.symbolic, gpu_sums)
         out = {
             "metric": W[5],
             "value": round(flops_all / t_step / 1e9, 2),
@@ -458,6 +493,8 @@ def main():
             "data": f"synthetic (generated {W[0]} stencil matrix, ||A||_1 = {anorm:g})",
             "config": {"workload": f"{args.workload}: {W[0]} stencil {'x'.join(map(str, W[1](args.nx)))} "
                                    f"(n={A.n}), {'graph nested dissection (METIS_NodeND)' if args.ordering == 'graph' else 'nested dissection'}, relax 60, maxsup 256, {W[6]}",
+                       "symbolic": ("reference sp_colorder + symbfact + pddistribute (ColPerm = MY_PERMC)"
+                                    if args.symbolic == "reference" else "library front-end (amalgamated)"),
                        "grid": f"{pr}x{pc}", "nsupers": int(S.nsupers),
                        "flops_per_factorization": flops_all,
                        "nnz_L": S.nnzL, "parallelism": f"2D block-cyclic {pr}x{pc}",
@@ -471,6 +508,7 @@ def main():
                        "comm_volume_gb_rank0": round(st0["comm_bytes"] / 1e9, 3)},
             "roofline": roof,
             "cpu_baseline": cpu,
+            "parity": parity,
             "next_rows": nxt,
             "abi_pdgstrf": abi,
             "phases_ms_per_step_rank0": {k[2:-3]: round(v / K, 3) for k, v in acc.items()},

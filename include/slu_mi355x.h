@@ -306,8 +306,12 @@ int slu_order_nd_grid(int nx, int ny, int nz, int64_t *perm_c);
  * composed with an etree postorder.  relax / maxsup as sp_ienv_dist(2/3).
  * flags: SLU_SYMB_MULTICHILD lets a chain supernode continue through a
  * column with several etree children (shorter supernodal trees for
- * level-set nested dissections). */
-enum { SLU_SYMB_MULTICHILD = 1 };
+ * level-set nested dissections).  SLU_SYMB_REFERENCE instead runs pdgssvx's
+ * own symbolic stage (sp_colorder + symbfact below, SRC/pdgssvx.c:1046-1076,
+ * perm_r = I): supernodes and structure are the reference's, and
+ * slu_distribute then lays them out with the reference's pddistribute
+ * (slu_distribute_glu on Pc A Pc^T). */
+enum { SLU_SYMB_MULTICHILD = 1, SLU_SYMB_REFERENCE = 2 };
 typedef struct slu_symb slu_symb;
 slu_symb *slu_symbolic(const slu_csc *A, const int64_t *perm_c, int relax,
                        int maxsup, int flags);

@@ -9,7 +9,10 @@
  *
  * usage: mpiexec -n P ref_pdgstrf -lib LIB -f MATRIX.bin -r PR -c PC
  *          [-x relax] [-m maxsup] [-l lookaheads] [-t replace_tiny]
- *          [-n reps] [-o outprefix]
+ *          [-n reps] [-o outprefix] [-s symbolic_flags] [-k blocksums_prefix]
+ * -s: slu_symbolic flags (2 = SLU_SYMB_REFERENCE: pdgssvx's own sp_colorder +
+ *     symbfact + pddistribute, restated bit-exact in the library).
+ * -k: per-block checksums of the factors (oracle/blocksum.h) per rank.
  * MATRIX.bin: int64 {n, nnz, dtype, has_perm}, colptr[n+1], rowind[nnz],
  *             values[nnz] (dtype 0=d,1=s,2=z), perm_c[n] if has_perm.
  */
@@ -22,6 +25,20 @@
 #include "superlu_sdefs.h"
 #include "superlu_zdefs.h"
 
+/* the library's flat LUstruct view (include/slu_mi355x.h) */
+typedef struct {
+    int64_t nsupers;
+    int_t *xsup, *supno;
+    int_t *Lidx; int64_t Lidx_cnt; long *Lidx_off;
+    void *Lval; int64_t Lval_cnt; long *Lval_off;
+    int_t *Uidx; int64_t Uidx_cnt; long *Uidx_off;
+    void *Uval; int64_t Uval_cnt; long *Uval_off;
+    int *ToRecv, *ToSendD, **ToSendR;
+    int_t bufmax[5];
+} slu_lu_view;
+#define SLU_ORACLE_BLOCKSUM_WRITE
+#include "../blocksum.h"
+
 typedef struct {
     int64_t n, nnz;
     int64_t *colptr, *rowind;
@@ -30,17 +47,18 @@ typedef struct {
 } fe_csc;
 
 typedef fe_csc *(*csc_create_t)(int64_t, int64_t, const int64_t *, const int64_t *, const void *, int);
-typedef void *(*symbolic_t)(const fe_csc *, const int64_t *, int, int);
+typedef void *(*symbolic_t)(const fe_csc *, const int64_t *, int, int, int);
 typedef void *(*distribute_t)(const void *, const fe_csc *, int, int, int, int);
 typedef void (*lufree_t)(void *, int);
+typedef int (*view_t)(void *, int, slu_lu_view *);
 
 static size_t vsz(int dt) { return dt == 1 ? 4 : dt == 2 ? 16 : 8; }
 
 int main(int argc, char **argv) {
     int prov;
     MPI_Init_thread(&argc, &argv, MPI_THREAD_MULTIPLE, &prov);
-    const char *libpath = NULL, *mfile = NULL, *outp = NULL;
-    int nprow = 1, npcol = 1, relax = 60, maxsup = 256, look = 10, tiny = 0, reps = 1;
+    const char *libpath = NULL, *mfile = NULL, *outp = NULL, *sums = NULL;
+    int nprow = 1, npcol = 1, relax = 60, maxsup = 256, look = 10, tiny = 0, reps = 1, sflags = 0;
     for (int i = 1; i < argc - 1; ++i) {
         if (!strcmp(argv[i], "-lib")) libpath = argv[++i];
         else if (!strcmp(argv[i], "-f")) mfile = argv[++i];
@@ -52,6 +70,8 @@ int main(int argc, char **argv) {
         else if (!strcmp(argv[i], "-l")) look = atoi(argv[++i]);
         else if (!strcmp(argv[i], "-t")) tiny = atoi(argv[++i]);
         else if (!strcmp(argv[i], "-n")) reps = atoi(argv[++i]);
+        else if (!strcmp(argv[i], "-s")) sflags = atoi(argv[++i]);
+        else if (!strcmp(argv[i], "-k")) sums = argv[++i];
     }
     void *h = dlopen(libpath, RTLD_NOW | RTLD_LOCAL);
     if (!h) { fprintf(stderr, "dlopen %s: %s\n", libpath, dlerror()); MPI_Abort(MPI_COMM_WORLD, 1); }
@@ -59,6 +79,7 @@ int main(int argc, char **argv) {
     symbolic_t symbolic = (symbolic_t)dlsym(h, "slu_symbolic");
     distribute_t distribute = (distribute_t)dlsym(h, "slu_distribute");
     lufree_t lufree = (lufree_t)dlsym(h, "slu_lustruct_free");
+    view_t get_view = (view_t)dlsym(h, "slu_lu_get_view");
 
     FILE *fp = fopen(mfile, "rb");
     if (!fp) { fprintf(stderr, "cannot open %s\n", mfile); MPI_Abort(MPI_COMM_WORLD, 1); }
@@ -91,7 +112,7 @@ int main(int argc, char **argv) {
     superlu_gridinit(MPI_COMM_WORLD, nprow, npcol, &grid);
     int iam = grid.iam, myrow = iam / npcol, mycol = iam % npcol;
     fe_csc *A = csc_create(n, nnz, colptr, rowind, val, dtype);
-    void *symb = symbolic(A, perm, relax, maxsup);
+    void *symb = symbolic(A, perm, relax, maxsup, sflags);
 
     double tbest = 1e30, tsum = 0;
     int info = 0, tinyp = 0;
@@ -140,6 +161,17 @@ int main(int argc, char **argv) {
             fp = fopen(fn, "wb"); fwrite(ld, vsz(dtype), lcnt, fp); fclose(fp);
             snprintf(fn, sizeof fn, "%s.rank%d.U.bin", outp, iam);
             fp = fopen(fn, "wb"); fwrite(ud, vsz(dtype), ucnt, fp); fclose(fp);
+        }
+        if (rep == reps - 1 && sums) {
+            slu_lu_view v;
+            get_view(LU, dtype, &v);
+            v.nsupers = n > 0 ? v.supno[n - 1] + 1 : 0;
+            char fn[1024];
+            snprintf(fn, sizeof fn, "%s.rank%d.bin", sums, iam);
+            if (blocksum_write(fn, dtype, &v, nprow, npcol, myrow, mycol)) {
+                fprintf(stderr, "cannot write %s\n", fn);
+                MPI_Abort(MPI_COMM_WORLD, 1);
+            }
         }
         PStatFree(&stat);
         lufree(LU, dtype);

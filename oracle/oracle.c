@@ -142,3 +142,16 @@ int oracle_zfactor(int Pr, int Pc, void **LUs, int n, int rt, double anorm,
                    int *info, int *tiny, double *flops) {
     return z_factor(Pr, Pc, LUs, n, rt, anorm, info, tiny, flops);
 }
+
+/* Per-block fingerprints of one rank's factors (blocksum.h; the checker of
+ * the full-size headline parity in bench.py's cpu_baseline leg).  Returns the
+ * record count; out == NULL counts only. */
+#include "blocksum.h"
+int64_t oracle_blocksums(int dtype, int64_t nsupers, const int64_t *xsup, const int64_t *Lidx,
+                         const long *Loff, const void *Lval, const long *Lvoff,
+                         const int64_t *Uidx, const long *Uoff, const void *Uval,
+                         const long *Uvoff, int nprow, int npcol, int myrow, int mycol,
+                         blocksum_rec *out) {
+    return blocksum_compute(dtype, nsupers, xsup, Lidx, Loff, Lval, Lvoff, Uidx, Uoff, Uval,
+                            Uvoff, nprow, npcol, myrow, mycol, out);
+}

@@ -60,6 +60,63 @@ def oracle_factor(lus, nprow, npcol, n, replace_tiny=False, anorm=1.0):
     return {"info": info.value, "tiny": tiny.value, "flops": flops.value}
 
 
+class BlockSum(C.Structure):
+    """blocksum.h's record: per-block fingerprint keyed by global (ib, jb)."""
+    _fields_ = [("kind", C.c_int64), ("ib", C.c_int64), ("jb", C.c_int64), ("cnt", C.c_int64),
+                ("maxabs", C.c_double), ("wre", C.c_double), ("wim", C.c_double)]
+
+
+BLOCKSUM_DT = np.dtype([("kind", "<i8"), ("ib", "<i8"), ("jb", "<i8"), ("cnt", "<i8"),
+                        ("maxabs", "<f8"), ("wre", "<f8"), ("wim", "<f8")])
+
+
+def blocksums(lu, Lval=None, Uval=None):
+    """Per-block fingerprints (oracle/blocksum.h) of one rank's LUStruct, with
+    its own value arrays or the given ones (e.g. a copy of the factors)."""
+    L = _load()
+    f = L.oracle_blocksums
+    f.restype = C.c_int64
+    Lv = lu.Lval if Lval is None else Lval
+    Uv = lu.Uval if Uval is None else Uval
+    v = lu.view
+    args = [lu.dtype, lu.nsupers, lu.xsup.ctypes.data_as(C.c_void_p),
+            C.cast(v.Lidx, C.c_void_p), C.cast(v.Lidx_off, C.c_void_p),
+            Lv.ctypes.data_as(C.c_void_p), C.cast(v.Lval_off, C.c_void_p),
+            C.cast(v.Uidx, C.c_void_p), C.cast(v.Uidx_off, C.c_void_p),
+            Uv.ctypes.data_as(C.c_void_p), C.cast(v.Uval_off, C.c_void_p),
+            C.c_int(lu.nprow), C.c_int(lu.npcol), C.c_int(lu.myrow), C.c_int(lu.mycol)]
+    f.argtypes = [C.c_int, C.c_int64] + [C.c_void_p] * 9 + [C.c_int] * 4 + [C.c_void_p]
+    n = f(*args, None)
+    out = np.zeros(max(n, 1), BLOCKSUM_DT)
+    f(*args, out.ctypes.data_as(C.c_void_p))
+    return out[:n]
+
+
+def read_blocksums(path):
+    with open(path, "rb") as fh:
+        n = int(np.fromfile(fh, np.int64, 1)[0])
+        return np.fromfile(fh, BLOCKSUM_DT, n)
+
+
+def compare_blocksums(mine, ref):
+    """Factor parity from per-block fingerprints of two factorizations of the
+    same LUstruct (any two process grids): every block present in both, and
+    rel_err = max over blocks of max(|d maxabs|, |d wsum| / sqrt(cnt)) / max|ref|
+    (|d wsum| / sqrt(cnt) estimates the block's RMS elementwise error: w is a
+    fixed pseudo-random projection)."""
+    key = lambda a: (a["kind"] * (1 << 42) + a["ib"]) * (1 << 21) + a["jb"]  # noqa: E731
+    a = np.sort(mine, order=["kind", "ib", "jb"])
+    b = np.sort(ref, order=["kind", "ib", "jb"])
+    if len(a) != len(b) or not np.array_equal(key(a), key(b)) or not np.array_equal(a["cnt"], b["cnt"]):
+        return {"blocks": int(len(b)), "blocks_mine": int(len(a)), "match": False, "rel_err": None}
+    scale = max(float(b["maxabs"].max()), 1e-300)
+    dmax = np.abs(a["maxabs"] - b["maxabs"])
+    dw = np.hypot(a["wre"] - b["wre"], a["wim"] - b["wim"]) / np.sqrt(np.maximum(b["cnt"], 1))
+    return {"blocks": int(len(b)), "values": int(b["cnt"].sum()), "match": True,
+            "rel_err": float(max(dmax.max(), dw.max()) / scale),
+            "rel_err_maxabs": float(dmax.max() / scale), "rel_err_proj": float(dw.max() / scale)}
+
+
 def write_matrix_bin(path, A, perm_c=None):
     colptr, rowind, val = A.arrays()
     with open(path, "wb") as fh:
@@ -78,9 +135,13 @@ def have_reference_harness():
 
 def run_reference(A, perm_c, nprow, npcol, relax=60, maxsup=256, lookahead=10,
                   replace_tiny=False, reps=1, want_factors=True, omp_threads=1,
-                  timeout=3600):
+                  timeout=3600, symb_flags=0, want_blocksums=False):
     """Run the reference factorization on nprow*npcol MPI ranks.
-    Returns (stats_dict, [(Lval, Uval) per rank] or None)."""
+    symb_flags: slu_symbolic flags for the LUstruct the harness builds
+    (2 = the reference's own sp_colorder + symbfact + pddistribute).
+    Returns (stats_dict, [(Lval, Uval) per rank] or None); with
+    want_blocksums, stats_dict["blocksums"] holds every rank's per-block
+    fingerprints (blocksum.h), concatenated."""
     from superlu_dist_amd.lib import DTYPES, LIB_PATH
     tmp = tempfile.mkdtemp(prefix="slu_ref_")
     try:
@@ -94,14 +155,20 @@ def run_reference(A, perm_c, nprow, npcol, relax=60, maxsup=256, lookahead=10,
         cmd = [os.path.join(CONDA, "bin", "mpiexec"), "-n", str(nprow * npcol), REF_BIN,
                "-lib", LIB_PATH, "-f", mfile, "-r", str(nprow), "-c", str(npcol),
                "-x", str(relax), "-m", str(maxsup), "-l", str(lookahead),
-               "-t", str(int(replace_tiny)), "-n", str(reps)]
+               "-t", str(int(replace_tiny)), "-n", str(reps), "-s", str(symb_flags)]
         if outp:
             cmd += ["-o", outp]
+        sums = os.path.join(tmp, "sums") if want_blocksums else None
+        if sums:
+            cmd += ["-k", sums]
         r = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=timeout)
         if r.returncode != 0:
             raise RuntimeError(f"reference harness failed: {r.stderr[-2000:]}")
         line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
         stats = json.loads(line)
+        if sums:
+            stats["blocksums"] = np.concatenate([read_blocksums(f"{sums}.rank{p}.bin")
+                                                 for p in range(nprow * npcol)])
         facs = None
         if want_factors:
             npt = DTYPES[A.dtype]

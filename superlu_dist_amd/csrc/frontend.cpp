@@ -169,6 +169,11 @@ struct slu_symb {
     vector<int64_t> sptr, srows; // struct(L_s) incl. diagonal rows, sorted
     vector<int64_t> sparent;     // supernodal etree
     double nnzL = 0, nnzU = 0;
+    // SLU_SYMB_REFERENCE: the reference's own symbolic factorization
+    // (sp_colorder + symbfact, csrc/symbolic.cpp) -- Glu_freeable's arrays,
+    // distributed by the reference's pddistribute (csrc/distribute.cpp)
+    bool ref = false;
+    vector<int64_t> xlsub, lsub, xusub, usub;
 };
 
 extern "C" {
@@ -257,6 +262,52 @@ int slu_order_nd_grid(int nx, int ny, int nz, int64_t *perm_c) {
     return 0;
 }
 
+// pdgssvx's symbolic stage for a square A with perm_r = I
+// (SRC/pdgssvx.c:1046-1076): sp_colorder's etree postorder folded into perm_c,
+// A Pc''s rows relabelled by perm_c, symbfact with relax / maxsup.  The
+// supernode partition and L / U structure are then exactly what the
+// reference's pdgssvx would hand pddistribute and pdgstrf for this perm_c.
+static slu_symb *symbolic_reference(const slu_csc *A, vector<int64_t> perm, int relax,
+                                    int maxsup) {
+    const int64_t n = A->n;
+    vector<int64_t> etree(n), cb(n), ce(n);
+    if (slu_colorder(n, n, A->colptr, A->rowind, 0, 1, perm.data(), etree.data(), cb.data(),
+                     ce.data()))
+        return nullptr;
+    vector<int64_t> ri(A->nnz);
+    for (int64_t p = 0; p < A->nnz; ++p) ri[p] = perm[A->rowind[p]];
+    void *h = slu_symbfact(n, n, cb.data(), ce.data(), ri.data(), etree.data(), relax, maxsup);
+    if (!h) return nullptr;
+    int64_t sz[7];
+    slu_symbfact_sizes(h, sz);
+    slu_symb *S = new slu_symb;
+    S->ref = true;
+    S->n = n;
+    S->perm = perm;
+    S->nsupers = sz[0];
+    S->xsup.assign(n + 1, 0);
+    S->supno.assign(n + 1, 0);
+    S->xlsub.assign(n + 1, 0);
+    S->xusub.assign(n + 1, 0);
+    S->lsub.assign(std::max<int64_t>(sz[1], 1), 0);
+    S->usub.assign(std::max<int64_t>(sz[2], 1), 0);
+    slu_symbfact_arrays(h, S->xsup.data(), S->supno.data(), S->xlsub.data(), S->lsub.data(),
+                        S->xusub.data(), S->usub.data());
+    slu_symbfact_free(h);
+    S->xsup.resize(S->nsupers + 1);
+    S->supno.resize(n);
+    // |struct(L_s)| (diagonal block rows included): the subscripts of a
+    // supernode are stored once, at its first column (SRC/symbfact.c:81-215)
+    S->sptr.assign(S->nsupers + 1, 0);
+    for (int64_t k = 0; k < S->nsupers; ++k) {
+        const int64_t f = S->xsup[k];
+        S->sptr[k + 1] = S->sptr[k] + (S->xlsub[f + 1] - S->xlsub[f]);
+    }
+    S->nnzL = (double)sz[3];
+    S->nnzU = (double)sz[4];
+    return S;
+}
+
 slu_symb *slu_symbolic(const slu_csc *A, const int64_t *perm_c_in, int relax,
                        int maxsup, int flags) {
     int64_t n = A->n;
@@ -265,6 +316,7 @@ slu_symb *slu_symbolic(const slu_csc *A, const int64_t *perm_c_in, int relax,
     vector<int64_t> perm(n);
     if (perm_c_in) std::copy(perm_c_in, perm_c_in + n, perm.begin());
     else std::iota(perm.begin(), perm.end(), 0);
+    if (flags & SLU_SYMB_REFERENCE) return symbolic_reference(A, std::move(perm), relax, maxsup);
 
     // etree of P(A+A^T)P^T, then compose perm with its postorder
     Graph g = sym_pattern(A, perm);
@@ -395,6 +447,7 @@ void slu_symb_arrays(const slu_symb *s, int64_t *xsup, int64_t *supno,
     if (perm_c) std::copy(s->perm.begin(), s->perm.end(), perm_c);
 }
 void slu_symb_struct_sizes(const slu_symb *s, int64_t *sizes) {
+    // (for SLU_SYMB_REFERENCE: |struct(L_s)| from symbfact's lsub)
     for (int64_t k = 0; k < s->nsupers; ++k) sizes[k] = s->sptr[k + 1] - s->sptr[k];
 }
 void slu_symb_counts(const slu_symb *s, double *nnzL, double *nnzU) {
@@ -810,6 +863,16 @@ extern "C" {
 
 void *slu_distribute(const slu_symb *s, const slu_csc *A, int nprow,
                      int npcol, int myrow, int mycol) {
+    if (s->ref) {
+        // the reference's pddistribute on Pc A Pc^T (csrc/distribute.cpp)
+        slu_csc *B = slu_permute(A, s->perm.data());
+        void *LU = slu_distribute_glu(A->dtype, s->n, s->xsup.data(), s->supno.data(),
+                                      s->xlsub.data(), s->lsub.data(), s->xusub.data(),
+                                      s->usub.data(), B->colptr, B->rowind, B->val, nprow, npcol,
+                                      myrow, mycol);
+        slu_csc_free(B);
+        return LU;
+    }
     switch (A->dtype) {
     case SLU_D: return distribute_t<double, dLocalLU_t, dLUstruct_t>(s, A, nprow, npcol, myrow, mycol);
     case SLU_S: return distribute_t<float, sLocalLU_t, sLUstruct_t>(s, A, nprow, npcol, myrow, mycol);

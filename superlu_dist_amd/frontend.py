@@ -73,21 +73,30 @@ def nd_order(nx, ny, nz=1):
     return perm
 
 
-SLU_SYMB_MULTICHILD = 1
+SLU_SYMB_MULTICHILD, SLU_SYMB_REFERENCE = 1, 2
 
 
 class Symbolic:
-    def __init__(self, A, perm_c=None, relax=60, maxsup=256, multichild=False):
+    def __init__(self, A, perm_c=None, relax=60, maxsup=256, multichild=False, reference=False):
         """multichild: chain supernodes continue through columns with several
         etree children (csrc/frontend.cpp; shortens the supernodal tree of
-        level-set nested dissections such as the library's METIS_NodeND)."""
+        level-set nested dissections such as the library's METIS_NodeND).
+        reference: pdgssvx's own symbolic stage instead (sp_colorder +
+        symbfact, SRC/pdgssvx.c:1046-1076, bit-exact restatements in
+        csrc/symbolic.cpp), distributed by the reference's pddistribute
+        (csrc/distribute.cpp): the supernodes and L/U structure the reference
+        hands pdgstrf for this perm_c."""
         self.A = A
         pc = None
         if perm_c is not None:
             self._perm_in = np.ascontiguousarray(perm_c, dtype=np.int64)
             pc = as_i64p(self._perm_in)
+        self.reference = reference
         self.ptr = lib().slu_symbolic(A.ptr, pc, relax, maxsup,
-                                      SLU_SYMB_MULTICHILD if multichild else 0)
+                                      (SLU_SYMB_MULTICHILD if multichild else 0) |
+                                      (SLU_SYMB_REFERENCE if reference else 0))
+        if not self.ptr:
+            raise RuntimeError("slu_symbolic: " + lib().slu_last_error().decode())
         self.n = A.n
         self.nsupers = lib().slu_symb_nsupers(self.ptr)
         self.xsup = np.empty(self.nsupers + 1, dtype=np.int64)

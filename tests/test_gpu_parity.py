@@ -193,3 +193,45 @@ def test_gpu_graph_ordering_multichild_matches_oracle(kind, dims, dtype):
         x = solve_1x1(gpu, b)
         assert backward_error(A, S.perm_c, x, b) < 1e-14
         assert np.abs(x - xt).max() / np.abs(xt).max() < 1e-10
+
+
+@pytest.mark.parametrize("kind,dims,dtype", [
+    (STENCIL_3D7, (20, 20, 20), 0),
+    (STENCIL_3D7, (24, 24, 24), 0),
+    (STENCIL_3D27, (14, 14, 14), 1),
+    (STENCIL_3D7, (12, 12, 12), 2),
+    (STENCIL_2D5, (60, 60, 1), 0),
+])
+def test_gpu_reference_structure_matches_oracle(kind, dims, dtype):
+    """The LUstruct the reference's pdgssvx builds for a given perm_c (its
+    own sp_colorder + symbfact + pddistribute, bench.py's headline
+    structure): many width-1 supernodes from the separators' borders."""
+    kw = dict(diag=6 - 0.25, diag_im=-0.0025) if dtype == 2 else {}
+    A = Csc.stencil(kind, *dims, dtype=dtype, **kw)
+    S = Symbolic(A, nd_order(*dims), 60, 256, reference=True)
+    gpu, ref = S.distribute(), S.distribute()
+    an = cases.anorm(A)
+    info, tiny, st = factor_lustruct(gpu, anorm=an)
+    o = pyoracle.oracle_factor([ref], 1, 1, A.n, False, an)
+    assert info == o["info"] == 0
+    err = cases.factor_error([gpu], [(ref.Lval, ref.Uval)])
+    assert err < TOL[dtype], err
+    assert abs(st["schur_flops"] + st["panel_flops"] - o["flops"]) <= 1e-9 * o["flops"] + 10
+
+
+@pytest.mark.skipif(not pyoracle.have_reference_harness(), reason="oracle/_ref not built")
+def test_gpu_reference_structure_fingerprints_match_reference_pdgstrf():
+    """bench.py's full-size parity check at a test size: the drop-in pdgstrf's
+    factors against the REFERENCE pdgstrf's (2x2 MPI grid) through the
+    per-block fingerprints (oracle/blocksum.h)."""
+    from superlu_dist_amd import capi
+    A = Csc.stencil(STENCIL_3D7, 24, 24, 24)
+    p = nd_order(24, 24, 24)
+    S = Symbolic(A, p, 60, 256, reference=True)
+    lu = S.distribute()
+    rv, info, _ = capi.pxgstrf(lu, 12.0)
+    assert rv == 0 and info == 0
+    st, _ = pyoracle.run_reference(A, p, 2, 2, symb_flags=2, want_factors=False,
+                                   want_blocksums=True, timeout=300)
+    c = pyoracle.compare_blocksums(pyoracle.blocksums(lu), st["blocksums"])
+    assert c["match"] and c["rel_err"] <= 1e-12, c
