@@ -98,8 +98,12 @@ def build_lu(workload, nx, pr, pc, myrow, mycol, ordering="grid", symbolic="refe
     if symbolic == "reference":
         # what pdgssvx hands pdgstrf for this perm_c (ColPerm = MY_PERMC):
         # the reference's sp_colorder + symbfact, laid out by its pddistribute
-        # (bit-exact restatements, csrc/symbolic.cpp, csrc/distribute.cpp)
-        S = Symbolic(A, perm, 60, 256, reference=True)
+        # (bit-exact restatements, csrc/symbolic.cpp, csrc/distribute.cpp).
+        # 1x1: that LUstruct as is (the plan amalgamates it on the device,
+        # csrc/amalg.h).  Grids: the grid plan has no device relayout, so the
+        # same coarse partition is laid out by pddistribute's rules instead
+        # (SLU_SYMB_COARSE); the rate counts the reference partition's work.
+        S = Symbolic(A, perm, 60, 256, reference=True, coarse=pr * pc > 1)
     else:
         # the library front-end's amalgamated partition (chains with <= 10 %
         # explicit zeros; graph ordering: chains through multi-child columns,
@@ -242,6 +246,14 @@ def cpu_baseline(A, perm, nx, nranks, timeout, flops, symbolic="reference", gpu_
     if not pyoracle.have_reference_harness():
         return None, None
     pr, pc = grid_shape(nranks)
+    import threading
+    done = threading.Event()
+
+    def heartbeat():  # a silent GPU job is taken for hung: say the CPU run is alive
+        t0 = time.time()
+        while not done.wait(30):
+            log(f"  reference pdgstrf running ({time.time() - t0:.0f} s)")
+    threading.Thread(target=heartbeat, daemon=True).start()
     try:
         st, _ = pyoracle.run_reference(A, perm, pr, pc, relax=60, maxsup=256, lookahead=10,
                                        want_factors=False, timeout=timeout,
@@ -250,6 +262,8 @@ def cpu_baseline(A, perm, nx, nranks, timeout, flops, symbolic="reference", gpu_
     except Exception as e:  # noqa: BLE001
         print(f"[bench] cpu baseline failed: {e}", file=sys.stderr)
         return None, None
+    finally:
+        done.set()
     t = st["time_best"]
     parity = None
     if gpu_sums is not None:
@@ -435,6 +449,7 @@ def main():
         return
     t_step = float(np.mean(times))
     flops_all = my_flops
+    ref_work = S.ref_flops() if args.symbolic == "reference" else None
     if dist is not None:
         import torch
         tt = torch.tensor([t_step], dtype=torch.float64)
@@ -443,6 +458,10 @@ def main():
         ff = torch.tensor([my_flops], dtype=torch.float64)
         dist.all_reduce(ff, op=dist.ReduceOp.SUM)
         flops_all = float(ff.item())
+    if ref_work is not None:
+        # the reference partition's algorithmic work (what pdgstrf does on the
+        # LUstruct pdgssvx builds; the coarse partition adds explicit zeros)
+        flops_all = ref_work["total"]
 
     if rank == 0:
         K = args.steps
@@ -495,7 +514,9 @@ def main():
                                    f"(n={A.n}), {'graph nested dissection (METIS_NodeND)' if args.ordering == 'graph' else 'nested dissection'}, relax 60, maxsup 256, {W[6]}",
                        "symbolic": ("reference sp_colorder + symbfact + pddistribute (ColPerm = MY_PERMC)"
                                     if args.symbolic == "reference" else "library front-end (amalgamated)"),
-                       "grid": f"{pr}x{pc}", "nsupers": int(S.nsupers),
+                       "grid": f"{pr}x{pc}",
+                       "nsupers": ref_work["nsupers"] if ref_work else int(S.nsupers),
+                       "nsupers_factored": int(st0["nsupers"]),
                        "flops_per_factorization": flops_all,
                        "nnz_L": S.nnzL, "parallelism": f"2D block-cyclic {pr}x{pc}",
                        "transport": ("host-staged gloo point-to-point (REHEARSAL, not a measurement)"

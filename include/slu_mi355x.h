@@ -267,6 +267,14 @@ typedef struct {
     double h2d_bytes, d2h_bytes;
     int64_t n_d2h_copies;
     double comm_buf_bytes;     /* HBM of the receive ring (diag packages + panels) */
+    /* engine-side amalgamation (csrc/amalg.h, 1x1 grids): nsupers above is
+     * the factored (coarse) partition, nsupers_in the caller's */
+    int64_t nsupers_in;
+    int64_t amalg_groups;      /* merged supernodes of more than one original */
+    double amalg_zeros;        /* explicit zeros the coarse storage adds */
+    double t_amalg_ms;         /* host analysis + programs (part of t_plan_ms) */
+    double t_expand_ms;        /* device relayout caller -> coarse (last upload) */
+    double t_compress_ms;      /* device relayout coarse -> caller (last download) */
 } slu_plan_stats;
 int slu_plan_get_stats(const slu_plan *p, slu_plan_stats *st);
 
@@ -310,8 +318,12 @@ int slu_order_nd_grid(int nx, int ny, int nz, int64_t *perm_c);
  * own symbolic stage (sp_colorder + symbfact below, SRC/pdgssvx.c:1046-1076,
  * perm_r = I): supernodes and structure are the reference's, and
  * slu_distribute then lays them out with the reference's pddistribute
- * (slu_distribute_glu on Pc A Pc^T). */
-enum { SLU_SYMB_MULTICHILD = 1, SLU_SYMB_REFERENCE = 2 };
+ * (slu_distribute_glu on Pc A Pc^T).  SLU_SYMB_REFERENCE | SLU_SYMB_COARSE
+ * then replaces the partition by the engine's coarse one (the amalgamation a
+ * 1x1 plan applies internally, csrc/amalg.h), so that it can be distributed
+ * on any grid; slu_symb_ref_info keeps the reference partition's size and
+ * work. */
+enum { SLU_SYMB_MULTICHILD = 1, SLU_SYMB_REFERENCE = 2, SLU_SYMB_COARSE = 4 };
 typedef struct slu_symb slu_symb;
 slu_symb *slu_symbolic(const slu_csc *A, const int64_t *perm_c, int relax,
                        int maxsup, int flags);
@@ -322,6 +334,10 @@ void slu_symb_arrays(const slu_symb *s, int64_t *xsup, int64_t *supno,
                      int64_t *perm_c);
 /* nnz(L) including the diagonal blocks, nnz(U) excluding them */
 void slu_symb_counts(const slu_symb *s, double *nnzL, double *nnzU);
+/* SLU_SYMB_REFERENCE: [nsupers of the reference's partition, schur, trsm,
+ * trsv, s1, s2, w] -- the algorithmic-work sums of that partition (real
+ * flops; the plan's weights per value type, csrc/amalg.h) */
+void slu_symb_ref_info(const slu_symb *s, double *out);
 /* |struct(L_s)| (rows incl. the diagonal block) per supernode */
 void slu_symb_struct_sizes(const slu_symb *s, int64_t *sizes);
 

@@ -31,6 +31,8 @@
 
 namespace {
 
+using i64 = int64_t;
+
 // MPI is resolved from the host process at run time (no link-time MPI).
 struct Mpi {
     int (*bcast)(void *, int, MPI_Datatype, int, MPI_Comm) = nullptr;
@@ -190,6 +192,57 @@ void reap_later(slu_plan *p) {
     });
 }
 
+// ---- plan cache (1x1 grids).  pdgssvx refactors one pattern with Fact =
+// SamePattern / SamePattern_SameRowPerm (SRC/superlu_defs.h:577-598): the
+// LUstruct's index arrays are the same, only the values differ.  The last
+// plan is kept (with its HBM) and reused when the structure digest matches,
+// so such a call pays upload + factor + download only.  Grids always build
+// afresh (their communicator belongs to grid->comm).  SUPERLU_MI355X_PLAN_CACHE=0
+// frees the plan after every call, as the reference frees its buffers.
+struct CachedPlan {
+    slu_plan *plan = nullptr;
+    uint64_t digest = 0;
+    int dtype = -1, n = -1, replace_tiny = -1;
+};
+CachedPlan g_cache;
+std::mutex g_cache_mu;
+
+inline uint64_t mix(uint64_t h, uint64_t v) {
+    h ^= v + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2);
+    return h * 0xBF58476D1CE4E5B9ull;
+}
+
+// digest of the 1x1 structure: xsup and every L / U index array (host threads)
+template <typename LUS> uint64_t structure_digest(LUS *lu, int n) {
+    const int_t *xsup = lu->Glu_persist->xsup;
+    const int ns = (int)(lu->Glu_persist->supno[n - 1] + 1);
+    std::vector<uint64_t> part(ns);
+    auto idx = [](const int_t *ix, i64 len) {
+        uint64_t h = 0x12345;
+        for (i64 i = 0; i < len; ++i) h = mix(h, (uint64_t)ix[i]);
+        return h;
+    };
+    slu::parallel_for(ns, [&](int s) {
+        uint64_t h = mix((uint64_t)s, (uint64_t)xsup[s + 1]);
+        if (const int_t *ix = lu->Llu->Lrowind_bc_ptr[s]) {
+            i64 p = SLU_BC_HEADER;
+            for (i64 b = 0; b < ix[0]; ++b) p += SLU_LB_DESCRIPTOR + ix[p + 1];
+            h = mix(h, idx(ix, p));
+        }
+        if (const int_t *ux = lu->Llu->Ufstnz_br_ptr[s]) h = mix(h, idx(ux, ux[2]));
+        // and where the values live: a plan keeps host pointers (the D2H
+        // unpack targets), so another LUstruct of the same pattern is a miss
+        h = mix(h, (uint64_t)(uintptr_t)lu->Llu->Lnzval_bc_ptr[s]);
+        h = mix(h, (uint64_t)(uintptr_t)lu->Llu->Unzval_br_ptr[s]);
+        part[s] = h;
+    });
+    uint64_t h = mix((uint64_t)n, (uint64_t)ns);
+    h = mix(h, (uint64_t)(uintptr_t)lu);
+    h = mix(h, (uint64_t)(uintptr_t)lu->Llu);
+    for (uint64_t v : part) h = mix(h, v);
+    return h;
+}
+
 template <typename LUS>
 int_t pxgstrf(int dtype, const char *name, superlu_dist_options_t *options, int m, int n,
               double anorm, LUS *LUstruct, gridinfo_t *grid, SuperLUStat_t *stat, int *info) {
@@ -208,20 +261,39 @@ int_t pxgstrf(int dtype, const char *name, superlu_dist_options_t *options, int 
     stat->num_look_aheads = std::max(0, std::min(options->num_lookaheads, SLU_MAX_LOOKAHEADS - 1));
     slu_plan *plan = nullptr;
     try {
-        reap_join(); // the previous call's device memory is free again
-        slu_comm *c = comm_for_grid(grid);
-        slu_engine_opts eo{};
-        eo.replace_tiny_pivot = options->ReplaceTinyPivot == SLU_YES;
-        // utime[FACT] (SRC/pdgssvx.c:1174-1180) covers the copies too: the
-        // H2D of the values runs beside the plan build, and each level's
-        // finished factors go back to the host arrays while later levels
-        // are factored (SUPERLU_MI355X_OVERLAP=0 turns both off)
-        const char *ov = getenv("SUPERLU_MI355X_OVERLAP");
-        eo.overlap_upload = eo.overlap_download = !(ov && !strcmp(ov, "0"));
-        char err[512] = {0};
-        plan = slu_plan_create(dtype, LUstruct, n, (int)grid->nprow, (int)grid->npcol, grid->iam,
-                               c, &eo, err, sizeof err);
-        if (!plan) throw slu::Error(err);
+        const bool one = grid->nprow * grid->npcol == 1;
+        const char *pc = getenv("SUPERLU_MI355X_PLAN_CACHE");
+        const bool cache = one && !(pc && !strcmp(pc, "0"));
+        const int rt = options->ReplaceTinyPivot == SLU_YES;
+        uint64_t dg = 0;
+        if (cache) {
+            dg = structure_digest(LUstruct, n);
+            std::lock_guard<std::mutex> lk(g_cache_mu);
+            if (g_cache.plan && g_cache.digest == dg && g_cache.dtype == dtype && g_cache.n == n &&
+                g_cache.replace_tiny == rt) {
+                plan = g_cache.plan; // same structure: reuse (values are uploaded again below)
+                g_cache.plan = nullptr;
+            } else if (g_cache.plan) {
+                reap_later(g_cache.plan);
+                g_cache.plan = nullptr;
+            }
+        }
+        if (!plan) {
+            reap_join(); // the previous call's device memory is free again
+            slu_comm *c = comm_for_grid(grid);
+            slu_engine_opts eo{};
+            eo.replace_tiny_pivot = rt;
+            // utime[FACT] (SRC/pdgssvx.c:1174-1180) covers the copies too: the
+            // H2D of the values runs beside the plan build, and each level's
+            // finished factors go back to the host arrays while later levels
+            // are factored (SUPERLU_MI355X_OVERLAP=0 turns both off)
+            const char *ov = getenv("SUPERLU_MI355X_OVERLAP");
+            eo.overlap_upload = eo.overlap_download = !(ov && !strcmp(ov, "0"));
+            char err[512] = {0};
+            plan = slu_plan_create(dtype, LUstruct, n, (int)grid->nprow, (int)grid->npcol,
+                                   grid->iam, c, &eo, err, sizeof err);
+            if (!plan) throw slu::Error(err);
+        }
         int myinfo = 0, tiny = 0;
         if (slu_plan_upload(plan) || slu_plan_factor(plan, anorm, &myinfo, &tiny) ||
             slu_plan_download(plan))
@@ -231,7 +303,16 @@ int_t pxgstrf(int dtype, const char *name, superlu_dist_options_t *options, int 
         stat->ops[SLU_PHASE_FACT] = (float)(st.schur_flops + st.panel_flops);
         stat->TinyPivots += tiny;
         stat->gpu_buffer = (float)(st.lu_bytes + st.index_bytes);
-        reap_later(plan);
+        if (cache) {
+            std::lock_guard<std::mutex> lk(g_cache_mu);
+            g_cache.plan = plan;
+            g_cache.digest = dg;
+            g_cache.dtype = dtype;
+            g_cache.n = n;
+            g_cache.replace_tiny = rt;
+        } else {
+            reap_later(plan);
+        }
         plan = nullptr;
         int gi = myinfo ? myinfo : n + 1;
         if (grid->nprow * grid->npcol > 1) {

@@ -1,0 +1,510 @@
+// Engine-side supernode amalgamation: analysis, coarse LUstruct, expand /
+// compress programs (amalg.h explains what and why).  Host C++, run once per
+// structure by the plan; the host apply() mirrors the device programs for
+// the CPU tests (tests/test_amalg.py).
+#include "amalg.h"
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <complex>
+#include <cstring>
+
+#include "common.h"
+
+namespace slu {
+
+namespace {
+
+using i64 = int64_t;
+
+// One original supernode's structure as the plan needs it.
+struct SnInfo {
+    i64 nsupr = 0, ulen = 0, ucols = 0; // L rows, U values, U column entries
+    double schur = 0, trsv = 0;         // 2 m seglen, seglen (seglen + 1) over U columns
+    int parent = -1;                    // first block row below the diagonal block
+    int b = 0;                          // L rows below the diagonal block
+    bool sym = false, nested = false, ok = false;
+};
+
+// rows of L(:,s) below the diagonal block, in index order
+inline void below_rows(const int_t *ix, int s, std::vector<int32_t> &out) {
+    out.clear();
+    if (!ix) return;
+    i64 p = SLU_BC_HEADER;
+    for (i64 b = 0; b < ix[0]; ++b) {
+        const i64 gb = ix[p], nr = ix[p + 1];
+        if (gb != s)
+            for (i64 i = 0; i < nr; ++i) out.push_back((int32_t)ix[p + 2 + i]);
+        p += SLU_LB_DESCRIPTOR + nr;
+    }
+}
+
+// columns of U(s,:) with a non-empty segment, with their first rows
+template <typename F> inline void for_ucols(const int_t *ux, const int_t *xsup, F &&f) {
+    if (!ux) return;
+    i64 p = SLU_BR_HEADER;
+    for (i64 b = 0; b < ux[0]; ++b) {
+        const i64 jb = ux[p], w = xsup[jb + 1] - xsup[jb];
+        for (i64 c = 0; c < w; ++c) f(xsup[jb] + c, ux[p + SLU_UB_DESCRIPTOR + c]);
+        p += SLU_UB_DESCRIPTOR + w;
+    }
+}
+
+} // namespace
+
+bool Amalg::build(int64_t n_, int ns, const int_t *xsup, const int_t *const *lidx,
+                  const int_t *const *uidx, double zero_frac, int maxw) {
+    n = n_;
+    ns1 = ns;
+    const bool prof = getenv("SLU_AMALG_TIME") != nullptr;
+    auto t0 = std::chrono::steady_clock::now();
+    auto tick = [&](const char *what) {
+        if (!prof) return;
+        const auto t = std::chrono::steady_clock::now();
+        fprintf(stderr, "[slu amalg] %s %.1f ms\n", what,
+                std::chrono::duration<double, std::milli>(t - t0).count());
+        t0 = t;
+    };
+    auto W = [&](i64 k) { return (int)(xsup[k + 1] - xsup[k]); };
+    SLU_REQUIRE(n < (1ll << 31), "amalgamation: n %lld does not fit int32", (long long)n);
+
+    // ---- pass 1: per supernode structure facts (parallel)
+    std::vector<SnInfo> inf(ns);
+    parallel_for(ns, [&](int s) {
+        thread_local std::vector<int32_t> bl, uc, bl2;
+        SnInfo &I = inf[s];
+        const int_t *ux = uidx[s];
+        if (ux) {
+            i64 p = SLU_BR_HEADER;
+            for (i64 b = 0; b < ux[0]; ++b) {
+                I.ucols += W(ux[p]);
+                p += SLU_UB_DESCRIPTOR + W(ux[p]);
+            }
+            I.ulen = ux[1];
+        }
+        const int_t *ix = lidx[s];
+        if (!ix) return;
+        I.nsupr = ix[1];
+        {
+            i64 p = SLU_BC_HEADER;
+            if (ix[0] < 1 || ix[p] != s || ix[p + 1] != W(s)) return; // diagonal block first, full
+        }
+        below_rows(ix, s, bl);
+        I.b = (int)bl.size();
+        SLU_REQUIRE(I.nsupr == W(s) + I.b, "amalgamation: L column %d rows %lld != %d + %d", s,
+                    (long long)I.nsupr, W(s), I.b);
+        {
+            i64 p = SLU_BC_HEADER;
+            if (ix[0] > 1) I.parent = (int)ix[p + SLU_LB_DESCRIPTOR + ix[p + 1]];
+        }
+        const i64 end = xsup[s + 1];
+        uc.clear();
+        for_ucols(ux, xsup, [&](i64 g, i64 fst) {
+            if (fst >= end) return;
+            uc.push_back((int32_t)g);
+            const double seg = (double)(end - fst);
+            I.trsv += seg * (seg + 1);
+            I.schur += 2.0 * I.b * seg;
+        });
+        std::sort(bl.begin(), bl.end());
+        I.sym = bl == uc; // U columns come out ascending (blocks by jb)
+        I.ok = true;
+        // nested into s+1: below(s) within cols(s+1) u below(s+1)
+        if (I.parent == s + 1 && s + 1 < ns) {
+            below_rows(lidx[s + 1], s + 1, bl2);
+            std::sort(bl2.begin(), bl2.end());
+            const i64 f1 = xsup[s + 1], l1 = xsup[s + 2];
+            size_t q = 0;
+            bool nest = true;
+            for (int32_t r : bl) {
+                if (r >= f1 && r < l1) continue;
+                while (q < bl2.size() && bl2[q] < r) ++q;
+                if (q == bl2.size() || bl2[q] != r) { nest = false; break; }
+            }
+            I.nested = nest;
+        }
+    }, 16);
+
+    for (int s = 0; s < ns; ++s) {
+        const double w = W(s);
+        fl_w += w;
+        fl_s1 += w * (w - 1) / 2;
+        fl_s2 += (w - 1) * w * (2 * w - 1) / 6;
+        fl_trsm += w * (w + 1) * inf[s].b;
+        fl_trsv += inf[s].trsv;
+        fl_schur += inf[s].schur;
+    }
+    tick("pass 1 (structure facts)");
+    // ---- pass 2: greedy chains
+    std::vector<int> gstart; // first original supernode of every group
+    {
+        std::vector<int32_t> ff((size_t)n, -1); // first-row of column g in the open chain
+        std::vector<int32_t> touched;
+        int s = 0;
+        while (s < ns) {
+            gstart.push_back(s);
+            int e = s;
+            const SnInfo &I0 = inf[s];
+            int wJ = W(s);
+            i64 orig = (i64)W(s) * I0.nsupr + I0.ulen;
+            touched.clear();
+            if (I0.ok && I0.sym)
+                for_ucols(uidx[s], xsup, [&](i64 g, i64 fst) {
+                    if (fst < xsup[s + 1]) { ff[g] = (int32_t)fst; touched.push_back((int32_t)g); }
+                });
+            while (e + 1 < ns && inf[e].ok && inf[e].sym && inf[e].nested && inf[e].parent == e + 1 &&
+                   inf[e + 1].ok && inf[e + 1].sym && wJ + W(e + 1) <= maxw) {
+                const int c = e + 1;
+                const i64 endc = xsup[c + 1];
+                double S = 0;
+                i64 b = 0;
+                for_ucols(uidx[c], xsup, [&](i64 g, i64 fst) {
+                    if (fst >= endc) return;
+                    S += (double)(ff[g] >= 0 ? ff[g] : fst);
+                    ++b;
+                });
+                const i64 w2 = wJ + W(c);
+                const double merged = (double)w2 * (double)(w2 + b) + (double)b * (double)endc - S;
+                const double orig2 = (double)orig + (double)W(c) * inf[c].nsupr + inf[c].ulen;
+                if (merged - orig2 > zero_frac * merged) break;
+                for_ucols(uidx[c], xsup, [&](i64 g, i64 fst) {
+                    if (fst < endc && ff[g] < 0) { ff[g] = (int32_t)fst; touched.push_back((int32_t)g); }
+                });
+                wJ = (int)w2;
+                orig = (i64)orig2;
+                e = c;
+            }
+            for (int32_t g : touched) ff[g] = -1;
+            s = e + 1;
+        }
+    }
+    ns2 = (int)gstart.size();
+    tick("pass 2 (chains)");
+    if (ns2 == ns1) return false;
+    gstart.push_back(ns);
+    grp.assign(ns, 0);
+    xsup2.assign(ns2 + 1, 0);
+    for (int J = 0; J < ns2; ++J) {
+        for (int s = gstart[J]; s < gstart[J + 1]; ++s) grp[s] = J;
+        xsup2[J] = xsup[gstart[J]];
+        if (gstart[J + 1] - gstart[J] > 1) ++n_merged_groups;
+    }
+    xsup2[ns2] = xsup[ns];
+    supno2.assign(n, 0);
+    for (int J = 0; J < ns2; ++J)
+        for (i64 c = xsup2[J]; c < xsup2[J + 1]; ++c) supno2[c] = J;
+    auto W2 = [&](i64 J) { return (int)(xsup2[J + 1] - xsup2[J]); };
+
+    // original value offsets (contiguous in supernode order) and program offsets
+    std::vector<i64> lsrc(ns + 1, 0), usrc(ns + 1, 0), lmap(ns + 1, 0), fcol(ns + 1, 0), nub(ns + 1, 0);
+    for (int s = 0; s < ns; ++s) {
+        lsrc[s + 1] = lsrc[s] + (lidx[s] ? (i64)lidx[s][1] * W(s) : 0);
+        usrc[s + 1] = usrc[s] + (uidx[s] ? (i64)uidx[s][1] : 0);
+        lmap[s + 1] = lmap[s] + (lidx[s] ? (i64)lidx[s][1] : 0);
+        fcol[s + 1] = fcol[s] + inf[s].ucols;
+        nub[s + 1] = nub[s] + (uidx[s] ? (i64)uidx[s][0] : 0);
+    }
+    lval1 = lsrc[ns];
+    uval1 = usrc[ns];
+
+    // ---- pass 3a: merged structure sizes per J (parallel)
+    // U row J: merged block columns J' with the first rows of every column
+    struct URow {
+        std::vector<int> blk;           // J' ascending
+        std::vector<int32_t> fst;       // all columns of all blocks, first row (end: empty)
+        std::vector<i64> colstart;      // per block: first column entry
+    };
+    std::vector<URow> urow(ns2);
+    std::vector<i64> lidx_len(ns2 + 1, 0), lval_len(ns2 + 1, 0), uidx_len(ns2 + 1, 0),
+        uval_len(ns2 + 1, 0), ucol_len(ns2 + 1, 0);
+    std::vector<int> nblk2(ns2, 0);
+    parallel_for(ns2, [&](int J) {
+        thread_local std::vector<int32_t> ff;
+        if ((i64)ff.size() < n) ff.assign(n, -1);
+        const int s0 = gstart[J], e = gstart[J + 1] - 1, wJ = W2(J);
+        const i64 endJ = xsup2[J + 1];
+        // L: diagonal block + e's blocks below J grouped by merged block row
+        const int_t *ix = lidx[e];
+        i64 nb = 1, rows = wJ;
+        if (ix) {
+            i64 p = SLU_BC_HEADER, last = -1;
+            for (i64 b = 0; b < ix[0]; ++b) {
+                const i64 gb = ix[p], nr = ix[p + 1];
+                if (gb != e) {
+                    const int I = grp[gb];
+                    if (I != last) { ++nb; last = I; }
+                    rows += nr;
+                }
+                p += SLU_LB_DESCRIPTOR + nr;
+            }
+        }
+        nblk2[J] = (int)nb;
+        lidx_len[J + 1] = SLU_BC_HEADER + SLU_LB_DESCRIPTOR * nb + rows;
+        lval_len[J + 1] = rows * wJ;
+        // U: first rows over the members (the first member holding a column)
+        URow &U = urow[J];
+        std::vector<int32_t> cols;
+        for (int a = s0; a <= e; ++a)
+            for_ucols(uidx[a], xsup, [&](i64 g, i64 fst) {
+                if (fst >= xsup[a + 1] || g < endJ) return;
+                if (ff[g] < 0) { ff[g] = (int32_t)fst; cols.push_back((int32_t)g); }
+            });
+        std::sort(cols.begin(), cols.end());
+        i64 len = 0, ncol = 0;
+        for (size_t i = 0; i < cols.size();) {
+            const int Jp = supno2[cols[i]];
+            U.blk.push_back(Jp);
+            U.colstart.push_back(ncol);
+            for (i64 c = xsup2[Jp]; c < xsup2[Jp + 1]; ++c) {
+                const int32_t f = ff[c] >= 0 ? ff[c] : (int32_t)endJ;
+                U.fst.push_back(f);
+                len += endJ - f;
+            }
+            ncol += W2(Jp);
+            while (i < cols.size() && supno2[cols[i]] == Jp) ++i;
+        }
+        for (int32_t g : cols) ff[g] = -1;
+        ucol_len[J + 1] = ncol;
+        uidx_len[J + 1] = U.blk.empty() ? 0 : SLU_BR_HEADER + SLU_UB_DESCRIPTOR * (i64)U.blk.size() + ncol + 1;
+        uval_len[J + 1] = len;
+    }, 1);
+    for (int J = 0; J < ns2; ++J) {
+        lidx_len[J + 1] += lidx_len[J];
+        lval_len[J + 1] += lval_len[J];
+        uidx_len[J + 1] += uidx_len[J];
+        uval_len[J + 1] += uval_len[J];
+        ucol_len[J + 1] += ucol_len[J];
+    }
+    tick("pass 3a (merged sizes)");
+    lval2 = lval_len[ns2];
+    uval2 = uval_len[ns2];
+    Lidx2.resize(lidx_len[ns2]);
+    Uidx2.resize(uidx_len[ns2]);
+    Loff2.assign(ns2, -1);
+    Lvoff2.assign(ns2, -1);
+    Uoff2.assign(ns2, -1);
+    Uvoff2.assign(ns2, -1);
+    // D: U-kind entries (one per merged U column entry), then L-kind (w_J per J)
+    const i64 DL0 = ucol_len[ns2];
+    D.resize(DL0 + n);
+    lcols.resize(ns);
+    lrow.resize(lmap[ns]);
+    ublks.resize(nub[ns]);
+    ufst.resize(fcol[ns]);
+
+    // ---- pass 3b + 4: merged index arrays, D, expand programs (parallel)
+    parallel_for(ns2, [&](int J) {
+        thread_local std::vector<int32_t> rowpos;
+        if ((i64)rowpos.size() < n) rowpos.assign(n, -1);
+        const int s0 = gstart[J], e = gstart[J + 1] - 1, wJ = W2(J);
+        const i64 x2J = xsup2[J], endJ = xsup2[J + 1];
+        const i64 nsupr2 = (lval_len[J + 1] - lval_len[J]) / wJ;
+        // L index
+        Loff2[J] = lidx_len[J];
+        Lvoff2[J] = lval_len[J];
+        int_t *L = &Lidx2[lidx_len[J]];
+        L[0] = nblk2[J];
+        L[1] = nsupr2;
+        i64 q = SLU_BC_HEADER;
+        L[q] = J;
+        L[q + 1] = wJ;
+        for (int c = 0; c < wJ; ++c) L[q + 2 + c] = x2J + c;
+        q += SLU_LB_DESCRIPTOR + wJ;
+        std::vector<int32_t> below;
+        below_rows(lidx[e], e, below);
+        {
+            const int_t *ix = lidx[e];
+            i64 p = SLU_BC_HEADER, desc = -1, last = -1;
+            for (i64 b = 0; ix && b < ix[0]; ++b) {
+                const i64 gb = ix[p], nr = ix[p + 1];
+                if (gb != e) {
+                    const int I = grp[gb];
+                    if (I != last) {
+                        desc = q;
+                        L[q] = I;
+                        L[q + 1] = 0;
+                        q += SLU_LB_DESCRIPTOR;
+                        last = I;
+                    }
+                    for (i64 i = 0; i < nr; ++i) L[q++] = ix[p + 2 + i];
+                    L[desc + 1] += nr;
+                }
+                p += SLU_LB_DESCRIPTOR + nr;
+            }
+        }
+        SLU_REQUIRE(q == lidx_len[J + 1] - lidx_len[J], "amalgamation: L index length of %d", J);
+        for (size_t i = 0; i < below.size(); ++i) rowpos[below[i]] = (int32_t)(wJ + i);
+        // U index + D (U kind)
+        const URow &U = urow[J];
+        if (!U.blk.empty()) {
+            Uoff2[J] = uidx_len[J];
+            Uvoff2[J] = uval_len[J];
+            int_t *X = &Uidx2[uidx_len[J]];
+            const i64 len1 = uidx_len[J + 1] - uidx_len[J] - 1;
+            X[0] = (int_t)U.blk.size();
+            X[1] = uval_len[J + 1] - uval_len[J];
+            X[2] = len1;
+            X[len1] = -1;
+            i64 p = SLU_BR_HEADER, ce = 0, seg = 0;
+            const i64 d0 = ucol_len[J];
+            for (size_t b = 0; b < U.blk.size(); ++b) {
+                const int Jp = U.blk[b];
+                X[p] = Jp;
+                i64 nnz = 0;
+                for (int c = 0; c < W2(Jp); ++c, ++ce) {
+                    const int32_t f = U.fst[ce];
+                    X[p + SLU_UB_DESCRIPTOR + c] = f;
+                    D[d0 + ce] = Uvoff2[J] + seg - f;
+                    seg += endJ - f;
+                    nnz += endJ - f;
+                }
+                X[p + 1] = nnz;
+                p += SLU_UB_DESCRIPTOR + W2(Jp);
+            }
+        }
+        // D (L kind): row fst of column g inside J -> Lvoff2 + (g - x2J) * ld2 + fst - x2J
+        for (int c = 0; c < wJ; ++c) D[DL0 + x2J + c] = Lvoff2[J] + (i64)c * nsupr2 - x2J;
+        // expand programs of the members
+        for (int a = s0; a <= e; ++a) {
+            const int_t *ix = lidx[a];
+            LCol &C = lcols[a];
+            C.src = lsrc[a];
+            C.dst = Lvoff2[J] + (xsup[a] - x2J) * nsupr2;
+            C.map = lmap[a];
+            C.nsupr = ix ? (int32_t)ix[1] : 0;
+            C.w = W(a);
+            C.ld2 = (int32_t)nsupr2;
+            C.pad = 0;
+            if (ix) {
+                i64 p = SLU_BC_HEADER, o = lmap[a];
+                for (i64 b = 0; b < ix[0]; ++b) {
+                    const i64 nr = ix[p + 1];
+                    for (i64 i = 0; i < nr; ++i) {
+                        const i64 r = ix[p + 2 + i];
+                        const int32_t pos = r < endJ ? (int32_t)(r - x2J) : rowpos[r];
+                        SLU_REQUIRE(pos >= 0, "amalgamation: row %lld of L column %d not in group %d",
+                                    (long long)r, a, J);
+                        lrow[o++] = pos;
+                    }
+                    p += SLU_LB_DESCRIPTOR + nr;
+                }
+            }
+            const int_t *ux = uidx[a];
+            if (!ux) continue;
+            i64 p = SLU_BR_HEADER, src = usrc[a], f0 = fcol[a], bi = nub[a];
+            const i64 enda = xsup[a + 1];
+            for (i64 b = 0; b < ux[0]; ++b, ++bi) {
+                const i64 jb = ux[p], w = W(jb);
+                UBlkX &B = ublks[bi];
+                B.src = src;
+                B.f0 = f0;
+                B.end = (int32_t)enda;
+                B.w = (int32_t)w;
+                B.pad = 0;
+                if (grp[jb] == J) {
+                    B.kind = 1;
+                    B.d0 = DL0 + xsup[jb];
+                } else {
+                    B.kind = 0;
+                    const int Jp = grp[jb];
+                    const auto it = std::lower_bound(U.blk.begin(), U.blk.end(), Jp);
+                    SLU_REQUIRE(it != U.blk.end() && *it == Jp,
+                                "amalgamation: U block (%d,%lld) not in merged row %d", a, (long long)jb, J);
+                    B.d0 = ucol_len[J] + U.colstart[it - U.blk.begin()] + (xsup[jb] - xsup2[Jp]);
+                }
+                for (i64 c = 0; c < w; ++c) {
+                    const i64 fst = ux[p + SLU_UB_DESCRIPTOR + c];
+                    ufst[f0 + c] = (int32_t)fst;
+                    src += enda - fst;
+                }
+                f0 += w;
+                p += SLU_UB_DESCRIPTOR + w;
+            }
+        }
+        for (int32_t r : below) rowpos[r] = -1;
+    }, 1);
+    tick("pass 3b/4 (merged arrays, programs)");
+    // explicit zeros introduced
+    zeros = (lval2 + uval2) - (lval1 + uval1);
+    return true;
+}
+
+void Amalg::coarse_glu(std::vector<int_t> &xlsub, std::vector<int_t> &lsub,
+                       std::vector<int_t> &xusub, std::vector<int_t> &usub) const {
+    xlsub.assign(n + 1, 0);
+    lsub.clear();
+    lsub.reserve(Lidx2.size());
+    for (int J = 0; J < ns2; ++J) {
+        const int_t *ix = Lidx2.data() + Loff2[J];
+        xlsub[xsup2[J]] = (int_t)lsub.size();
+        i64 p = SLU_BC_HEADER;
+        for (i64 b = 0; b < ix[0]; ++b) {
+            const i64 nr = ix[p + 1];
+            lsub.insert(lsub.end(), ix + p + 2, ix + p + 2 + nr);
+            p += SLU_LB_DESCRIPTOR + nr;
+        }
+        for (i64 c = xsup2[J] + 1; c <= xsup2[J + 1]; ++c) xlsub[c] = (int_t)lsub.size();
+    }
+    // U: per column, the first row of its segment in every coarse block row
+    xusub.assign(n + 1, 0);
+    auto walk = [&](auto &&f) {
+        for (int I = 0; I < ns2; ++I) {
+            if (Uoff2[I] < 0) continue;
+            const int_t *ux = Uidx2.data() + Uoff2[I];
+            const i64 end = xsup2[I + 1];
+            i64 p = SLU_BR_HEADER;
+            for (i64 b = 0; b < ux[0]; ++b) {
+                const i64 Jp = ux[p], w = xsup2[Jp + 1] - xsup2[Jp];
+                for (i64 c = 0; c < w; ++c) {
+                    const i64 fst = ux[p + SLU_UB_DESCRIPTOR + c];
+                    if (fst < end) f(xsup2[Jp] + c, fst);
+                }
+                p += SLU_UB_DESCRIPTOR + w;
+            }
+        }
+    };
+    walk([&](i64 g, i64) { ++xusub[g + 1]; });
+    for (i64 j = 0; j < n; ++j) xusub[j + 1] += xusub[j];
+    usub.assign(std::max<i64>(xusub[n], 1), 0);
+    std::vector<int_t> fill(xusub.begin(), xusub.end() - 1);
+    walk([&](i64 g, i64 fst) { usub[fill[g]++] = fst; });
+}
+
+template <typename T> void Amalg::apply(T *oL, T *oU, T *mL, T *mU, int dir) const {
+    parallel_for((int)lcols.size(), [&](int s) {
+        const LCol &C = lcols[s];
+        for (int c = 0; c < C.w; ++c)
+            for (int i = 0; i < C.nsupr; ++i) {
+                T *o = oL + C.src + (i64)c * C.nsupr + i;
+                T *m = mL + C.dst + (i64)c * C.ld2 + lrow[C.map + i];
+                if (dir == 0) *m = *o;
+                else *o = *m;
+            }
+    });
+    parallel_for((int)ublks.size(), [&](int b) {
+        const UBlkX &B = ublks[b];
+        i64 src = B.src;
+        T *M = B.kind ? mL : mU;
+        for (int c = 0; c < B.w; ++c) {
+            const i64 f = ufst[B.f0 + c], len = B.end - f;
+            T *m = M + D[B.d0 + c] + f;
+            for (i64 i = 0; i < len; ++i) {
+                if (dir == 0) m[i] = oU[src + i];
+                else oU[src + i] = m[i];
+            }
+            src += len;
+        }
+    });
+}
+
+template void Amalg::apply<double>(double *, double *, double *, double *, int) const;
+template void Amalg::apply<float>(float *, float *, float *, float *, int) const;
+template void Amalg::apply<std::complex<double>>(std::complex<double> *, std::complex<double> *,
+                                                 std::complex<double> *, std::complex<double> *,
+                                                 int) const;
+
+} // namespace slu
+

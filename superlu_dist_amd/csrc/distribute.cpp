@@ -218,10 +218,12 @@ void *distribute_glu_t(i64 n, const int_t *xsup_in, const int_t *supno_in, const
     Llu->Lrowind_bc_cnt = li + 1;
     Llu->Lnzval_bc_cnt = lv + 1;
     Llu->Lrowind_bc_dat = (int_t *)malloc((li + 1) * sizeof(int_t));
-    Llu->Lnzval_bc_dat = (T *)malloc((lv + 1) * sizeof(T));
-    SLU_REQUIRE(Llu->Lrowind_bc_dat && Llu->Lnzval_bc_dat, "distribute: out of host memory (L)");
+    // a == nullptr: index arrays only (no value storage; the coarse symbolic
+    // of frontend.cpp reads the structure of the 1x1 layout)
+    Llu->Lnzval_bc_dat = a ? (T *)malloc((lv + 1) * sizeof(T)) : nullptr;
+    SLU_REQUIRE(Llu->Lrowind_bc_dat && (Llu->Lnzval_bc_dat || !a), "distribute: out of host memory (L)");
     Llu->Lrowind_bc_dat[li] = 0;
-    Llu->Lnzval_bc_dat[lv] = zero_of<T>();
+    if (a) Llu->Lnzval_bc_dat[lv] = zero_of<T>();
     Llu->Ufstnz_br_ptr = (int_t **)calloc(std::max<i64>(nlr, 1), sizeof(int_t *));
     Llu->Unzval_br_ptr = (T **)calloc(std::max<i64>(nlr, 1), sizeof(T *));
     Llu->Ufstnz_br_offset = (long *)malloc(std::max<i64>(nlr, 1) * sizeof(long));
@@ -240,17 +242,17 @@ void *distribute_glu_t(i64 n, const int_t *xsup_in, const int_t *supno_in, const
     Llu->Ufstnz_br_cnt = ui + 1;
     Llu->Unzval_br_cnt = uv + 1;
     Llu->Ufstnz_br_dat = (int_t *)malloc((ui + 1) * sizeof(int_t));
-    Llu->Unzval_br_dat = (T *)malloc((uv + 1) * sizeof(T));
-    SLU_REQUIRE(Llu->Ufstnz_br_dat && Llu->Unzval_br_dat, "distribute: out of host memory (U)");
+    Llu->Unzval_br_dat = a ? (T *)malloc((uv + 1) * sizeof(T)) : nullptr;
+    SLU_REQUIRE(Llu->Ufstnz_br_dat && (Llu->Unzval_br_dat || !a), "distribute: out of host memory (U)");
     Llu->Ufstnz_br_dat[ui] = 0;
-    Llu->Unzval_br_dat[uv] = zero_of<T>();
+    if (a) Llu->Unzval_br_dat[uv] = zero_of<T>();
 
     // ---- U block rows (one thread per row: index, zeroed segments, A's values)
     slu::parallel_for((int)nlr, [&](int lb) {
         if (!u_len[lb]) return;
         const i64 gb = (i64)lb * Pr + myrow, klst = xsup[gb + 1];
         int_t *index = Llu->Ufstnz_br_dat + Llu->Ufstnz_br_offset[lb];
-        T *uval = Llu->Unzval_br_dat + Llu->Unzval_br_offset[lb];
+        T *uval = a ? Llu->Unzval_br_dat + Llu->Unzval_br_offset[lb] : nullptr;
         Llu->Ufstnz_br_ptr[lb] = index;
         Llu->Unzval_br_ptr[lb] = uval;
         const i64 len1 = u_len1[lb];
@@ -273,11 +275,13 @@ void *distribute_glu_t(i64 n, const int_t *xsup_in, const int_t *supno_in, const
             index[desc + SLU_UB_DESCRIPTOR + (j - xsup[jb])] = irow;
             const i64 k = klst - irow;
             index[desc + 1] += k;
-            T *seg = uval + vo;
-            std::fill(seg, seg + k, zero_of<T>());
-            for (i64 p = xa[j]; p < xa[j + 1]; ++p) {
-                const i64 r = asub[p];
-                if (r >= irow && r < klst) seg[r - irow] = a[p];
+            if (a) {
+                T *seg = uval + vo;
+                std::fill(seg, seg + k, zero_of<T>());
+                for (i64 p = xa[j]; p < xa[j + 1]; ++p) {
+                    const i64 r = asub[p];
+                    if (r >= irow && r < klst) seg[r - irow] = a[p];
+                }
             }
             vo += k;
         }
@@ -297,7 +301,7 @@ void *distribute_glu_t(i64 n, const int_t *xsup_in, const int_t *supno_in, const
         const i64 jb = (i64)ljb * Pc + mycol, f = xsup[jb], w = W(jb);
         const i64 len = l_len[ljb], nrbl = l_nrbl[ljb];
         int_t *index = Llu->Lrowind_bc_dat + Llu->Lrowind_bc_offset[ljb];
-        T *lusup = Llu->Lnzval_bc_dat + Llu->Lnzval_bc_offset[ljb];
+        T *lusup = a ? Llu->Lnzval_bc_dat + Llu->Lnzval_bc_offset[ljb] : nullptr;
         Llu->Lrowind_bc_ptr[ljb] = index;
         Llu->Lnzval_bc_ptr[ljb] = lusup;
         // blocks in first-appearance order, rows per block
@@ -342,8 +346,8 @@ void *distribute_glu_t(i64 n, const int_t *xsup_in, const int_t *supno_in, const
             index[start[s]++] = row;
             pos[row] = cnt[s]++;
         }
-        std::fill(lusup, lusup + len * w, zero_of<T>());
-        for (i64 c = 0; c < w; ++c) {
+        if (a) std::fill(lusup, lusup + len * w, zero_of<T>());
+        for (i64 c = 0; a && c < w; ++c) {
             const i64 j = f + c;
             for (i64 p = xa[j]; p < xa[j + 1]; ++p) {
                 const i64 row = asub[p];

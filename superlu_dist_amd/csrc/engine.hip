@@ -36,6 +36,7 @@
 #include <string>
 #include <type_traits>
 #include <condition_variable>
+#include <functional>
 #include <thread>
 #include <vector>
 
@@ -44,6 +45,8 @@
 #include "fill.h"
 #include "solve.h"
 #include "hostio.h"
+#include "amalg.h"
+#include "amalg_dev.h"
 #include "slu_mi355x.h"
 
 using std::vector;
@@ -373,6 +376,10 @@ struct PlanBase {
 // panel TRSMs -> L-panel (row) / U-panel (column) broadcasts -> Schur update.
 template <typename T, typename HT, typename LocalLU, typename LUS>
 struct Plan : PlanBase {
+    using value_type = T;
+    using host_type = HT;
+    using local_type = LocalLU;
+    using lus_type = LUS;
     // ---- problem
     int n = 0, nsupers = 0, Pr = 1, Pc = 1, iam = 0, myrow = 0, mycol = 0;
     slu_comm *comm = nullptr;
@@ -1021,6 +1028,7 @@ struct Plan : PlanBase {
         for (int k = 0; k < nsupers; ++k) bylev[level_of[k]].push_back(k);
         levels.assign(maxlev + 1, LevelRange{});
         stats.nsupers = nsupers;
+        stats.nsupers_in = nsupers;
         stats.nlevels = maxlev + 1;
     }
 
@@ -1892,6 +1900,9 @@ struct Plan : PlanBase {
         i64 off, bytes; // in the slot
     };
     vector<D2HFill> d2h_fills;
+    // called on the D2H stream before fill F's push, after its level's
+    // panels are done (AmalgPlan: compress the level into the caller's layout)
+    std::function<void(int, hipStream_t)> d2h_pre;
     vector<PushSeg> h_push;
     vector<HostSeg> h_unpack;
     DevBuf<PushSeg> d_push;
@@ -2018,6 +2029,7 @@ struct Plan : PlanBase {
                 }
                 const D2HFill &F = d2h_fills[j];
                 HIPCHK(hipStreamWaitEvent(cs, ev_pan[F.level], 0));
+                if (d2h_pre) d2h_pre(F.level, cs); // (amalgamated plan: relayout of the levels)
                 if (use_sdma) {
                     // gather into an HBM slot (HBM-bound, microseconds), then
                     // one DMA-engine copy to the pinned slot: the PCIe-bound
@@ -3045,6 +3057,409 @@ template <typename P> PlanBase *make_plan(void *LU, int n, int pr, int pc, int i
     return new P((decltype(std::declval<P>().LU))LU, n, pr, pc, iam, c, o);
 }
 
+
+// ---------------------------------------------------------------- amalgamation
+// A 1x1 plan over the coarse partition of csrc/amalg.h.  The inner plan is an
+// ordinary Plan built on the coarse LUstruct's index arrays (held here, no
+// host values); the caller's values travel in their own layout (d_oL / d_oU)
+// and are relaid on the device: expand at upload (caller -> coarse), compress
+// at download (coarse -> caller).  The device-resident state between upload
+// and download -- what factor(), snapshot / restore, fill_a, solve and refine
+// work on -- is the coarse layout.
+template <typename T, typename HT, typename LocalLU, typename LUS>
+struct AmalgPlan : PlanBase {
+    using Inner = Plan<T, HT, LocalLU, LUS>;
+    LUS *LU = nullptr;
+    int n = 0, ns = 0;
+    Amalg A;
+    // the coarse LUstruct the inner plan reads (index arrays only)
+    LUS mlu{};
+    LocalLU mllu{};
+    Glu_persist_t mglu{};
+    vector<int_t *> mlidx, muidx;
+    std::unique_ptr<Inner> in;
+    slu_engine_opts opts{};
+    // caller layout on the device, and the relayout programs
+    DevBuf<T> d_oL, d_oU;
+    DevBuf<LColX> d_lx;
+    DevBuf<int32_t> d_lrow, d_ufst;
+    DevBuf<Amalg::UBlkX> d_ub;
+    DevBuf<i64> d_D;
+    vector<i64> usrc; // caller U value offset per block row
+    std::thread up_thread;
+    std::string up_err;
+    double up_ms = 0, h2d_bytes = 0;
+    double t_amalg = 0, t_plan = 0, t_expand = 0, t_compress = 0, t_d2h = 0;
+    bool coarse_current = false; // d_oL / d_oU stale: the coarse storage holds newer values
+
+    static double ms_since(std::chrono::steady_clock::time_point t0) {
+        return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0)
+            .count();
+    }
+
+    // Returns nullptr when nothing merges (the caller then builds a Plan).
+    static AmalgPlan *make(LUS *lu, int n_, const slu_engine_opts *o, double zero_frac, int maxw) {
+        auto t0 = std::chrono::steady_clock::now();
+        std::unique_ptr<AmalgPlan> P(new AmalgPlan);
+        P->LU = lu;
+        P->n = n_;
+        if (o) P->opts = *o;
+        const int_t *xsup = lu->Glu_persist->xsup;
+        P->ns = (int)(lu->Glu_persist->supno[n_ - 1] + 1);
+        LocalLU *L = lu->Llu;
+        const int ns = P->ns;
+        // caller value layout: contiguous per block column / row in supernode order
+        i64 lv = 0, uv = 0;
+        P->usrc.assign(ns + 1, 0);
+        for (int s = 0; s < ns; ++s) {
+            if (L->Lrowind_bc_ptr[s]) lv += (i64)L->Lrowind_bc_ptr[s][1] * (xsup[s + 1] - xsup[s]);
+            if (L->Ufstnz_br_ptr[s]) uv += L->Ufstnz_br_ptr[s][1];
+            P->usrc[s + 1] = uv;
+        }
+        HIPCHK(hipSetDevice(0));
+        P->d_oL.alloc(std::max<i64>(lv, 1));
+        P->d_oU.alloc(std::max<i64>(uv, 1));
+        if (P->opts.overlap_upload) {
+            AmalgPlan *raw = P.get();
+            P->up_thread = std::thread([raw] {
+                try {
+                    HIPCHK(hipSetDevice(0));
+                    raw->h2d();
+                } catch (const std::exception &e) {
+                    raw->up_err = e.what();
+                }
+            });
+        }
+        try {
+            vector<const int_t *> li(L->Lrowind_bc_ptr, L->Lrowind_bc_ptr + ns),
+                ui(L->Ufstnz_br_ptr, L->Ufstnz_br_ptr + ns);
+            const auto ta = std::chrono::steady_clock::now();
+            if (!P->A.build(n_, ns, xsup, li.data(), ui.data(), zero_frac, maxw)) {
+                if (P->up_thread.joinable()) P->up_thread.join();
+                return nullptr;
+            }
+            SLU_REQUIRE(P->A.lval1 == lv && P->A.uval1 == uv, "amalgamation: value counts");
+            P->t_amalg = ms_since(ta);
+            P->build_inner();
+            P->build_programs();
+            if (P->opts.overlap_download) P->build_d2h();
+        } catch (...) {
+            if (P->up_thread.joinable()) P->up_thread.join();
+            throw;
+        }
+        P->t_plan = ms_since(t0);
+        P->sync_stats();
+        return P.release();
+    }
+
+    void build_inner() {
+        const int ns2 = A.ns2;
+        mlidx.assign(ns2, nullptr);
+        muidx.assign(ns2, nullptr);
+        for (int J = 0; J < ns2; ++J) {
+            if (A.Loff2[J] >= 0) mlidx[J] = A.Lidx2.data() + A.Loff2[J];
+            if (A.Uoff2[J] >= 0) muidx[J] = A.Uidx2.data() + A.Uoff2[J];
+        }
+        mglu.xsup = A.xsup2.data();
+        mglu.supno = A.supno2.data();
+        mllu.Lrowind_bc_ptr = mlidx.data();
+        mllu.Ufstnz_br_ptr = muidx.data();
+        mlu.Glu_persist = &mglu;
+        mlu.Llu = &mllu;
+        slu_engine_opts io = opts;
+        io.overlap_upload = io.overlap_download = 0;
+        in.reset(new Inner(&mlu, n, 1, 1, 0, nullptr, &io));
+    }
+
+    // Programs in level order of the coarse plan (so the D2H can compress a
+    // level as soon as its panels are done): lx / ublks items of the groups
+    // of level L at [lx_lev[L], lx_lev[L+1]) / [ub_lev[L], ub_lev[L+1]).
+    vector<int> lx_lev, ub_lev;
+    void build_programs() {
+        const int nl = (int)in->levels.size();
+        auto lev = [&](int s) { return in->level_of[A.grp[s]]; };
+        // L: column ranges of <= 64 K values per workgroup
+        vector<vector<LColX>> bl(nl);
+        for (int s = 0; s < ns; ++s) {
+            const Amalg::LCol &C = A.lcols[s];
+            if (!C.nsupr) continue;
+            const int cpi = std::max(1, (int)(65536 / C.nsupr));
+            for (int c0 = 0; c0 < C.w; c0 += cpi)
+                bl[lev(s)].push_back({C.src, C.dst, C.map, C.nsupr, c0, std::min(C.w, c0 + cpi), C.ld2});
+        }
+        vector<LColX> lx;
+        lx_lev.assign(nl + 1, 0);
+        for (int L = 0; L < nl; ++L) {
+            lx.insert(lx.end(), bl[L].begin(), bl[L].end());
+            lx_lev[L + 1] = (int)lx.size();
+        }
+        // U: the blocks of original block row a are ublks[ub0[a] .. ub0[a+1])
+        vector<Amalg::UBlkX> ub;
+        ub.reserve(A.ublks.size());
+        {
+            vector<i64> ub0(ns + 1, 0);
+            for (int s = 0; s < ns; ++s)
+                ub0[s + 1] = ub0[s] + (LU->Llu->Ufstnz_br_ptr[s] ? LU->Llu->Ufstnz_br_ptr[s][0] : 0);
+            SLU_REQUIRE(ub0[ns] == (i64)A.ublks.size(), "amalgamation: U block count");
+            vector<vector<int>> rows(nl);
+            for (int s = 0; s < ns; ++s) rows[lev(s)].push_back(s);
+            ub_lev.assign(nl + 1, 0);
+            for (int L = 0; L < nl; ++L) {
+                for (int s : rows[L]) ub.insert(ub.end(), A.ublks.begin() + ub0[s], A.ublks.begin() + ub0[s + 1]);
+                ub_lev[L + 1] = (int)ub.size();
+            }
+        }
+        nlx = (int)lx.size();
+        if (lx.empty()) lx.push_back({0, 0, 0, 0, 0, 0, 0});
+        if (ub.empty()) ub.resize(1);
+        d_lx.upload(lx);
+        d_ub.upload(ub);
+        d_lrow.upload(A.lrow.empty() ? vector<int32_t>(1) : A.lrow);
+        d_ufst.upload(A.ufst.empty() ? vector<int32_t>(1) : A.ufst);
+        d_D.upload(A.D.empty() ? vector<i64>(1) : A.D);
+    }
+    int nlx = 0;
+
+    // levels [L0, L1) of the relayout on stream st
+    void relayout_levels(int dir, int L0, int L1, hipStream_t st) {
+        const int a = lx_lev[L0], b = lx_lev[L1];
+        if (b > a)
+            hipLaunchKernelGGL((k_amalg_l<T>), dim3(b - a), dim3(256), 0, st, d_lx.p + a, d_lrow.p,
+                               d_oL.p, in->d_L.p, dir);
+        const i64 u0 = ub_lev[L0], nb = ub_lev[L1] - u0;
+        if (nb > 0)
+            hipLaunchKernelGGL((k_amalg_u<T>), dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, st,
+                               d_ub.p + u0, nb, d_ufst.p, d_D.p, d_oU.p, in->d_L.p, in->d_U.p, dir);
+        HIPCHK(hipGetLastError());
+    }
+
+    // The overlapped D2H of the drop-in path (opts.overlap_download): the
+    // inner plan's pinned-slot pipeline (run_d2h) with fills that carry the
+    // caller's layout: a coarse group's members are consecutive supernodes,
+    // so its values are one range of d_oL and one of d_oU; before a fill is
+    // pushed, d2h_pre compresses every level up to the fill's into d_oL /
+    // d_oU on the D2H stream.
+    int compressed_to = 0;
+    void build_d2h() {
+        Inner &P = *in;
+        LocalLU *Llu = LU->Llu;
+        const int_t *xsup = LU->Glu_persist->xsup;
+        const int nl = (int)P.levels.size();
+        if (const char *e = getenv("SLU_D2H_SLOT_KB")) { // as the plain plan
+            P.D2H_SLOT = std::max<i64>(16, atoll(e)) << 10;
+            P.D2H_MIN = P.D2H_SLOT / 4;
+        }
+        vector<i64> lsrc(ns + 1, 0);
+        for (int s = 0; s < ns; ++s)
+            lsrc[s + 1] = lsrc[s] + (Llu->Lrowind_bc_ptr[s] ? (i64)Llu->Lrowind_bc_ptr[s][1] * (xsup[s + 1] - xsup[s]) : 0);
+        vector<int> g0(A.ns2 + 1, ns); // first original supernode of each group
+        for (int s = ns - 1; s >= 0; --s) g0[A.grp[s]] = s;
+        i64 fb = 0;
+        int seg0 = 0, hs0 = 0;
+        const i64 SLOT = P.D2H_SLOT, PIECE = Inner::D2H_PIECE;
+        auto close = [&](int L) {
+            if (fb == 0) return;
+            P.d2h_fills.push_back({L, seg0, (int)P.h_push.size() - seg0, hs0, (int)P.h_unpack.size() - hs0, fb});
+            seg0 = (int)P.h_push.size();
+            hs0 = (int)P.h_unpack.size();
+            fb = 0;
+        };
+        auto add = [&](const char *dev, char *host, i64 bytes, int L) {
+            i64 done = 0;
+            while (done < bytes) {
+                const i64 take = std::min(bytes - done, SLOT - fb);
+                for (i64 o = 0; o < take; o += PIECE)
+                    P.h_push.push_back({dev + done + o, fb + o, (int)std::min(PIECE, take - o)});
+                for (i64 o = 0; o < take; o += 4 * PIECE)
+                    P.h_unpack.push_back({host + done + o, fb + o, std::min(4 * PIECE, take - o)});
+                fb += (take + 15) & ~(i64)15;
+                done += take;
+                if (fb >= SLOT) close(L);
+            }
+        };
+        for (int L = 0; L < nl; ++L) {
+            for (int J : P.bylev[L])
+                for (int s = g0[J]; s < g0[J + 1]; ++s) {
+                    if (Llu->Lrowind_bc_ptr[s])
+                        add((const char *)(d_oL.p + lsrc[s]), (char *)Llu->Lnzval_bc_ptr[s],
+                            (lsrc[s + 1] - lsrc[s]) * (i64)sizeof(T), L);
+                    if (Llu->Ufstnz_br_ptr[s])
+                        add((const char *)(d_oU.p + usrc[s]), (char *)Llu->Unzval_br_ptr[s],
+                            (usrc[s + 1] - usrc[s]) * (i64)sizeof(T), L);
+                }
+            if (fb >= P.D2H_MIN || L + 1 == nl) close(L);
+        }
+        P.d_push.upload(P.h_push.empty() ? vector<PushSeg>(1) : P.h_push);
+        P.d2h_pre = [this](int L, hipStream_t st) {
+            if (L + 1 > compressed_to) {
+                relayout_levels(1, compressed_to, L + 1, st);
+                compressed_to = L + 1;
+            }
+        };
+        P.opts.overlap_download = 1;
+    }
+
+    // caller layout: host arrays <-> d_oL / d_oU
+    vector<Xfer> xfers() {
+        LocalLU *L = LU->Llu;
+        vector<Xfer> xs;
+        const int_t *xsup = LU->Glu_persist->xsup;
+        i64 lo = 0;
+        for (int s = 0; s < ns; ++s) {
+            if (!L->Lrowind_bc_ptr[s]) continue;
+            const i64 cnt = (i64)L->Lrowind_bc_ptr[s][1] * (xsup[s + 1] - xsup[s]);
+            xs.push_back({(char *)(d_oL.p + lo), (char *)L->Lnzval_bc_ptr[s], (size_t)cnt * sizeof(T)});
+            lo += cnt;
+        }
+        for (int s = 0; s < ns; ++s)
+            if (L->Ufstnz_br_ptr[s])
+                xs.push_back({(char *)(d_oU.p + usrc[s]), (char *)L->Unzval_br_ptr[s],
+                              (size_t)(usrc[s + 1] - usrc[s]) * sizeof(T)});
+        return merge_xfers(std::move(xs));
+    }
+    void h2d() {
+        const auto t0 = std::chrono::steady_clock::now();
+        vector<Xfer> xs = xfers();
+        staged_h2d(xs, 0);
+        h2d_bytes = 0;
+        for (auto &x : xs) h2d_bytes += (double)x.bytes;
+        up_ms = ms_since(t0);
+    }
+
+    void relayout(int dir) {
+        hipStream_t st = in->stream;
+        if (dir == 0) {
+            HIPCHK(hipMemsetAsync(in->d_L.p, 0, in->d_L.bytes(), st));
+            HIPCHK(hipMemsetAsync(in->d_U.p, 0, in->d_U.bytes(), st));
+        }
+        relayout_levels(dir, 0, (int)in->levels.size(), st);
+        HIPCHK(hipStreamSynchronize(st));
+    }
+
+    void sync_stats() {
+        stats = in->stats;
+        // the caller's partition's algorithmic work (what the reference's
+        // pdgstrf does on this LUstruct); the coarse partition's own counts
+        // (explicit zeros included) stay in the kernel-level fields
+        // (schur_big_flops, schur_flops_padded)
+        const bool cp = sizeof(T) == 16;
+        stats.schur_flops = A.fl_schur * (cp ? 4.0 : 1.0);
+        stats.panel_flops = (cp ? 6 * A.fl_s1 + 10 * A.fl_w + 8 * A.fl_s2 : A.fl_s1 + 2 * A.fl_s2) +
+                            (cp ? 4.0 : 1.0) * A.fl_trsm + A.fl_trsv;
+        stats.nsupers_in = ns;
+        stats.amalg_groups = A.n_merged_groups;
+        stats.amalg_zeros = (double)A.zeros;
+        stats.t_amalg_ms = t_amalg;
+        stats.t_plan_ms = t_plan;
+        stats.t_upload_ms = up_ms;
+        stats.h2d_bytes = h2d_bytes;
+        stats.t_expand_ms = t_expand;
+        stats.t_compress_ms = t_compress;
+        stats.t_d2h_ms = t_d2h;
+        stats.d2h_bytes = (double)(d_oL.bytes() + d_oU.bytes());
+    }
+
+    void upload() override {
+        const auto t0 = std::chrono::steady_clock::now();
+        if (up_thread.joinable()) {
+            up_thread.join();
+            if (!up_err.empty()) {
+                std::string e;
+                e.swap(up_err);
+                throw Error(e);
+            }
+        } else {
+            h2d();
+        }
+        const auto t1 = std::chrono::steady_clock::now();
+        relayout(0);
+        t_expand = ms_since(t1);
+        in->vstate = 1;
+        in->d_acur = nullptr;
+        in->host_current = false;
+        coarse_current = false;
+        host_done = false;
+        sync_stats();
+        stats.t_upload_wait_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+    }
+    void factor(double anorm, int *info, int *tiny) override {
+        compressed_to = 0;
+        in->factor(anorm, info, tiny);
+        // overlap_download: the caller's arrays already hold the factors
+        coarse_current = !in->host_current;
+        host_done = in->host_current;
+        sync_stats();
+        if (host_done) {
+            stats.t_d2h_ms = in->stats.t_d2h_ms;
+            stats.t_d2h_tail_ms = in->stats.t_d2h_tail_ms;
+            stats.d2h_bytes = in->stats.d2h_bytes;
+            stats.n_d2h_copies = in->stats.n_d2h_copies;
+        }
+    }
+    bool host_done = false;
+    void download() override {
+        in->sync();
+        if (host_done) return;
+        if (coarse_current) {
+            const auto t0 = std::chrono::steady_clock::now();
+            relayout(1);
+            t_compress = ms_since(t0);
+            coarse_current = false;
+        }
+        const auto t0 = std::chrono::steady_clock::now();
+        for (const Xfer &x : xfers()) HIPCHK(hipMemcpy(x.host, x.dev, x.bytes, hipMemcpyDeviceToHost));
+        t_d2h = ms_since(t0);
+        sync_stats();
+    }
+    void snapshot() override { in->snapshot(); }
+    void restore() override {
+        in->restore();
+        coarse_current = true;
+        host_done = false;
+    }
+    void sync() override { in->sync(); }
+    void set_timing(int timing, int serial) override { in->set_timing(timing, serial); }
+    void solve(void *b, int64_t ldb, int nrhs) override {
+        in->solve(b, ldb, nrhs);
+        sync_stats();
+    }
+    void set_a_pattern(int64_t ncol, const int64_t *xa, const int64_t *asub) override {
+        in->set_a_pattern(ncol, xa, asub);
+        sync_stats();
+    }
+    void fill_a(const void *a, int on_device) override {
+        in->fill_a(a, on_device);
+        coarse_current = true;
+        host_done = false;
+        sync_stats();
+    }
+    void refine(const void *b, void *x, int64_t ld, int nrhs, double *berr, int *steps) override {
+        in->refine(b, x, ld, nrhs, berr, steps);
+        sync_stats();
+    }
+    void check_exchange(int64_t *nsec, int64_t *nbytes) override { in->check_exchange(nsec, nbytes); }
+    ~AmalgPlan() override {
+        if (up_thread.joinable()) up_thread.join();
+    }
+};
+
+// The plan for a caller's LUstruct: the amalgamated one on 1x1 grids when
+// chains merge (SLU_AMALG=0 turns it off; SLU_AMALG_ZERO sets the explicit
+// zero fraction, default 0.10), else the plain plan.
+template <typename P> PlanBase *make_plan_any(void *LU, int n, int pr, int pc, int iam, slu_comm *c,
+                                              const slu_engine_opts *o) {
+    using A = AmalgPlan<typename P::value_type, typename P::host_type, typename P::local_type,
+                        typename P::lus_type>;
+    const char *e = getenv("SLU_AMALG");
+    const bool on = !(e && !strcmp(e, "0"));
+    if (on && pr * pc == 1 && !(o && o->schedule_only)) {
+        const char *z = getenv("SLU_AMALG_ZERO");
+        if (PlanBase *p = A::make((typename P::lus_type *)LU, n, o, z ? atof(z) : 0.10, FAST_MAXW))
+            return p;
+    }
+    return make_plan<P>(LU, n, pr, pc, iam, c, o);
+}
+
 } // namespace slu
 
 struct slu_plan {
@@ -3195,13 +3610,13 @@ slu_plan *slu_plan_create(int dtype, void *LU, int n, int nprow, int npcol, int 
         p->dtype = dtype;
         switch (dtype) {
         case SLU_D:
-            p->impl.reset(make_plan<Plan<double, double, dLocalLU_t, dLUstruct_t>>(LU, n, nprow, npcol, iam, comm, opts));
+            p->impl.reset(make_plan_any<Plan<double, double, dLocalLU_t, dLUstruct_t>>(LU, n, nprow, npcol, iam, comm, opts));
             break;
         case SLU_S:
-            p->impl.reset(make_plan<Plan<float, float, sLocalLU_t, sLUstruct_t>>(LU, n, nprow, npcol, iam, comm, opts));
+            p->impl.reset(make_plan_any<Plan<float, float, sLocalLU_t, sLUstruct_t>>(LU, n, nprow, npcol, iam, comm, opts));
             break;
         case SLU_Z:
-            p->impl.reset(make_plan<Plan<zc, doublecomplex, zLocalLU_t, zLUstruct_t>>(LU, n, nprow, npcol, iam, comm, opts));
+            p->impl.reset(make_plan_any<Plan<zc, doublecomplex, zLocalLU_t, zLUstruct_t>>(LU, n, nprow, npcol, iam, comm, opts));
             break;
         default:
             throw Error(fmt("bad dtype %d", dtype));

@@ -16,6 +16,8 @@
 //     nzval = concatenated column segments [fstnz, xsup[gb+1])
 //   ToRecv / ToSendD / ToSendR / bufmax as SRC/pddistribute.c:752-801,2370.
 #include "slu_mi355x.h"
+#include "amalg.h"
+#include "common.h"
 
 #include <algorithm>
 #include <complex>
@@ -174,6 +176,11 @@ struct slu_symb {
     // distributed by the reference's pddistribute (csrc/distribute.cpp)
     bool ref = false;
     vector<int64_t> xlsub, lsub, xusub, usub;
+    // SLU_SYMB_COARSE: the partition and Glu above are the engine's coarse
+    // partition of the reference's (csrc/amalg.h); the reference's own
+    // partition size and algorithmic work (real-flop sums) are kept here
+    int64_t nsupers_fine = 0;
+    double fl[6] = {0, 0, 0, 0, 0, 0}; // schur, trsm, trsv, s1, s2, w
 };
 
 extern "C" {
@@ -267,8 +274,10 @@ int slu_order_nd_grid(int nx, int ny, int nz, int64_t *perm_c) {
 // A Pc''s rows relabelled by perm_c, symbfact with relax / maxsup.  The
 // supernode partition and L / U structure are then exactly what the
 // reference's pdgssvx would hand pddistribute and pdgstrf for this perm_c.
+static void coarsen(slu_symb *S);
+
 static slu_symb *symbolic_reference(const slu_csc *A, vector<int64_t> perm, int relax,
-                                    int maxsup) {
+                                    int maxsup, bool coarse) {
     const int64_t n = A->n;
     vector<int64_t> etree(n), cb(n), ce(n);
     if (slu_colorder(n, n, A->colptr, A->rowind, 0, 1, perm.data(), etree.data(), cb.data(),
@@ -305,7 +314,43 @@ static slu_symb *symbolic_reference(const slu_csc *A, vector<int64_t> perm, int 
     }
     S->nnzL = (double)sz[3];
     S->nnzU = (double)sz[4];
+    S->nsupers_fine = S->nsupers;
+    if (coarse) coarsen(S);
     return S;
+}
+
+// Replace the reference's partition by the engine's coarse one (csrc/amalg.h):
+// the 1x1 index arrays of the reference's pddistribute (no values), their
+// amalgamation, and the coarse Glu, so that slu_distribute lays the coarse
+// partition out on any grid with the reference's own rules.
+static void coarsen(slu_symb *S) {
+    void *LU = slu_distribute_glu(SLU_D, S->n, S->xsup.data(), S->supno.data(), S->xlsub.data(),
+                                  S->lsub.data(), S->xusub.data(), S->usub.data(), nullptr, nullptr,
+                                  nullptr, 1, 1, 0, 0);
+    if (!LU) throw slu::Error(slu_last_error());
+    slu_lu_view v;
+    slu_lu_get_view(LU, SLU_D, &v);
+    const int ns = (int)S->nsupers;
+    vector<const int_t *> li(ns, nullptr), ui(ns, nullptr);
+    for (int s = 0; s < ns; ++s) {
+        if (v.Lidx_off[s] >= 0) li[s] = v.Lidx + v.Lidx_off[s];
+        if (v.Uidx_off[s] >= 0) ui[s] = v.Uidx + v.Uidx_off[s];
+    }
+    slu::Amalg A;
+    const bool merged = A.build(S->n, ns, S->xsup.data(), li.data(), ui.data(), 0.10, 256);
+    slu_lustruct_free(LU, SLU_D);
+    S->fl[0] = A.fl_schur; S->fl[1] = A.fl_trsm; S->fl[2] = A.fl_trsv;
+    S->fl[3] = A.fl_s1; S->fl[4] = A.fl_s2; S->fl[5] = A.fl_w;
+    if (!merged) return;
+    A.coarse_glu(S->xlsub, S->lsub, S->xusub, S->usub);
+    S->nsupers = A.ns2;
+    S->xsup.assign(A.xsup2.begin(), A.xsup2.end());
+    S->supno.assign(A.supno2.begin(), A.supno2.end());
+    S->sptr.assign(S->nsupers + 1, 0);
+    for (int64_t k = 0; k < S->nsupers; ++k) {
+        const int64_t f = S->xsup[k];
+        S->sptr[k + 1] = S->sptr[k] + (S->xlsub[f + 1] - S->xlsub[f]);
+    }
 }
 
 slu_symb *slu_symbolic(const slu_csc *A, const int64_t *perm_c_in, int relax,
@@ -316,7 +361,14 @@ slu_symb *slu_symbolic(const slu_csc *A, const int64_t *perm_c_in, int relax,
     vector<int64_t> perm(n);
     if (perm_c_in) std::copy(perm_c_in, perm_c_in + n, perm.begin());
     else std::iota(perm.begin(), perm.end(), 0);
-    if (flags & SLU_SYMB_REFERENCE) return symbolic_reference(A, std::move(perm), relax, maxsup);
+    if (flags & SLU_SYMB_REFERENCE) {
+        try {
+            return symbolic_reference(A, std::move(perm), relax, maxsup, (flags & SLU_SYMB_COARSE) != 0);
+        } catch (const std::exception &e) {
+            slu::set_last_error(e.what());
+            return nullptr;
+        }
+    }
 
     // etree of P(A+A^T)P^T, then compose perm with its postorder
     Graph g = sym_pattern(A, perm);
@@ -449,6 +501,12 @@ void slu_symb_arrays(const slu_symb *s, int64_t *xsup, int64_t *supno,
 void slu_symb_struct_sizes(const slu_symb *s, int64_t *sizes) {
     // (for SLU_SYMB_REFERENCE: |struct(L_s)| from symbfact's lsub)
     for (int64_t k = 0; k < s->nsupers; ++k) sizes[k] = s->sptr[k + 1] - s->sptr[k];
+}
+// SLU_SYMB_REFERENCE: [nsupers of the reference's partition, then its
+// algorithmic-work sums schur, trsm, trsv, s1, s2, w] (csrc/amalg.h)
+void slu_symb_ref_info(const slu_symb *s, double *out) {
+    out[0] = (double)s->nsupers_fine;
+    for (int i = 0; i < 6; ++i) out[1 + i] = s->fl[i];
 }
 void slu_symb_counts(const slu_symb *s, double *nnzL, double *nnzU) {
     if (nnzL) *nnzL = s->nnzL;

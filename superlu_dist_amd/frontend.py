@@ -73,11 +73,12 @@ def nd_order(nx, ny, nz=1):
     return perm
 
 
-SLU_SYMB_MULTICHILD, SLU_SYMB_REFERENCE = 1, 2
+SLU_SYMB_MULTICHILD, SLU_SYMB_REFERENCE, SLU_SYMB_COARSE = 1, 2, 4
 
 
 class Symbolic:
-    def __init__(self, A, perm_c=None, relax=60, maxsup=256, multichild=False, reference=False):
+    def __init__(self, A, perm_c=None, relax=60, maxsup=256, multichild=False, reference=False,
+                 coarse=False):
         """multichild: chain supernodes continue through columns with several
         etree children (csrc/frontend.cpp; shortens the supernodal tree of
         level-set nested dissections such as the library's METIS_NodeND).
@@ -85,7 +86,11 @@ class Symbolic:
         symbfact, SRC/pdgssvx.c:1046-1076, bit-exact restatements in
         csrc/symbolic.cpp), distributed by the reference's pddistribute
         (csrc/distribute.cpp): the supernodes and L/U structure the reference
-        hands pdgstrf for this perm_c."""
+        hands pdgstrf for this perm_c.
+        coarse (with reference): the engine's coarse partition of that
+        structure (csrc/amalg.h, what a 1x1 plan factors internally), laid out
+        by the same pddistribute rules on any grid; ref_flops() is still the
+        reference partition's work."""
         self.A = A
         pc = None
         if perm_c is not None:
@@ -94,7 +99,8 @@ class Symbolic:
         self.reference = reference
         self.ptr = lib().slu_symbolic(A.ptr, pc, relax, maxsup,
                                       (SLU_SYMB_MULTICHILD if multichild else 0) |
-                                      (SLU_SYMB_REFERENCE if reference else 0))
+                                      (SLU_SYMB_REFERENCE if reference else 0) |
+                                      (SLU_SYMB_COARSE if coarse else 0))
         if not self.ptr:
             raise RuntimeError("slu_symbolic: " + lib().slu_last_error().decode())
         self.n = A.n
@@ -123,6 +129,19 @@ class Symbolic:
         schur = 2.0 * b * b * w
         return {"schur": schur.sum(), "panel": (diag + trsm + trsv).sum(),
                 "total": (schur + diag + trsm + trsv).sum()}
+
+    def ref_flops(self):
+        """reference symbolic: algorithmic flops of the reference's partition
+        (SURVEY 8d accounting, as the plan reports them; for coarse=True the
+        partition before the engine's amalgamation) and its supernode count"""
+        out = (C.c_double * 7)()
+        lib().slu_symb_ref_info(self.ptr, out)
+        cp = self.A.dtype == SLU_Z
+        schur, trsm, trsv, s1, s2, w = out[1:]
+        m = 4.0 if cp else 1.0
+        panel = (6 * s1 + 10 * w + 8 * s2 if cp else s1 + 2 * s2) + m * trsm + trsv
+        return {"schur": m * schur, "panel": panel, "total": m * schur + panel,
+                "nsupers": int(out[0])}
 
     def distribute(self, nprow=1, npcol=1, myrow=0, mycol=0):
         return LUStruct(self, nprow, npcol, myrow, mycol)
@@ -234,3 +253,58 @@ class LUStruct:
         if getattr(self, "ptr", None):
             lib().slu_lustruct_free(self.ptr, self.dtype)
             self.ptr = None
+
+
+class Amalgamation:
+    """The engine's supernode amalgamation of a 1x1 LUStruct (csrc/amalg.h):
+    the coarse partition the plan factors, as an LUStruct of its own
+    (``merged``, values zero until ``expand``), and the host versions of the
+    device expand / compress programs.  For tests: the plan applies the same
+    programs on the device."""
+
+    def __init__(self, lu, zero_frac=0.10, maxw=256):
+        self.lu = lu
+        self.h = lib().slu_amalg_create(lu.dtype, lu.ptr, lu.n, zero_frac, maxw)
+        if not self.h:
+            raise RuntimeError(lib().slu_last_error().decode())
+        sz = np.zeros(8, np.int64)
+        lib().slu_amalg_sizes(self.h, as_i64p(sz))
+        self.ns1, self.ns2, nli, nui, self.lval2, self.uval2, self.groups, self.zeros = map(int, sz)
+        n = lu.n
+        xs, sn = np.zeros(self.ns2 + 1, np.int64), np.zeros(n, np.int64)
+        Li, Ui = np.zeros(max(nli, 1), np.int64), np.zeros(max(nui, 1), np.int64)
+        Lo, Lv, Uo, Uv = (np.zeros(self.ns2, np.int64) for _ in range(4))
+        lib().slu_amalg_arrays(self.h, as_i64p(xs), as_i64p(sn), as_i64p(Li), as_i64p(Lo),
+                               as_i64p(Lv), as_i64p(Ui), as_i64p(Uo), as_i64p(Uv))
+        npt = DTYPES[lu.dtype]
+        self.merged = LUStruct.from_arrays(lu.dtype, n, xs, sn, 1, 1, 0, 0, Li[:nli], Lo,
+                                           np.zeros(self.lval2 + 1, npt), Lv, Ui[:nui], Uo,
+                                           np.zeros(self.uval2 + 1, npt), Uv)
+
+    def flops(self):
+        """the ORIGINAL partition's algorithmic flops, as the plan reports them"""
+        out = (C.c_double * 2)()
+        lib().slu_amalg_flops(self.h, self.lu.dtype, out)
+        return out[0] + out[1]
+
+    def apply(self, oL, oU, mL, mU, direction):
+        arrs = [np.ascontiguousarray(a) for a in (oL, oU, mL, mU)]
+        rc = lib().slu_amalg_apply(self.h, self.lu.dtype, *[a.ctypes.data_as(C.c_void_p)
+                                                            for a in arrs], direction)
+        if rc:
+            raise RuntimeError("slu_amalg_apply")
+
+    def expand(self):
+        """merged := the original LUStruct's values (structural zeros elsewhere)"""
+        self.merged.Lval[:] = 0
+        self.merged.Uval[:] = 0
+        self.apply(self.lu.Lval, self.lu.Uval, self.merged.Lval, self.merged.Uval, 0)
+
+    def compress(self, oL, oU):
+        """oL / oU (the original layout) := the merged values at their positions"""
+        self.apply(oL, oU, self.merged.Lval, self.merged.Uval, 1)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().slu_amalg_free(self.h)
+            self.h = None

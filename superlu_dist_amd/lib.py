@@ -78,7 +78,10 @@ class PlanStats(C.Structure):
                 ("t_upload_ms", C.c_double), ("t_upload_wait_ms", C.c_double),
                 ("t_d2h_ms", C.c_double), ("t_d2h_tail_ms", C.c_double),
                 ("h2d_bytes", C.c_double), ("d2h_bytes", C.c_double),
-                ("n_d2h_copies", C.c_int64), ("comm_buf_bytes", C.c_double)]
+                ("n_d2h_copies", C.c_int64), ("comm_buf_bytes", C.c_double),
+                ("nsupers_in", C.c_int64), ("amalg_groups", C.c_int64),
+                ("amalg_zeros", C.c_double), ("t_amalg_ms", C.c_double),
+                ("t_expand_ms", C.c_double), ("t_compress_ms", C.c_double)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -119,6 +122,13 @@ def lib():
         "slu_symb_struct_sizes": (None, [P, c_i64p]),
         "slu_distribute": (P, [P, C.POINTER(SluCsc), C.c_int, C.c_int, C.c_int, C.c_int]),
         "slu_lustruct_free": (None, [P, C.c_int]),
+        "slu_amalg_create": (P, [C.c_int, P, C.c_int64, C.c_double, C.c_int]),
+        "slu_amalg_sizes": (None, [P, c_i64p]),
+        "slu_amalg_arrays": (None, [P] + [c_i64p] * 8),
+        "slu_amalg_apply": (C.c_int, [P, C.c_int, P, P, P, P, C.c_int]),
+        "slu_amalg_free": (None, [P]),
+        "slu_symb_ref_info": (None, [P, C.POINTER(C.c_double)]),
+        "slu_amalg_flops": (None, [P, C.c_int, C.POINTER(C.c_double)]),
         "slu_distribute_glu": (P, [C.c_int, C.c_int64, c_i64p, c_i64p, c_i64p, c_i64p, c_i64p,
                                    c_i64p, c_i64p, c_i64p, P, C.c_int, C.c_int, C.c_int, C.c_int]),
         "slu_lustruct_build": (P, [C.c_int, C.c_int64, C.c_int64, c_i64p, c_i64p, C.c_int,

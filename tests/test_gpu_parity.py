@@ -149,7 +149,8 @@ def test_gpu_overlapped_upload_download(slot_kb, dtype, monkeypatch):
     assert p.factor(an) == (0, 0)
     p.download()                           # a no-op: already written back
     st = p.stats()
-    assert st["d2h_bytes"] == st["lu_bytes"] and st["h2d_bytes"] == st["lu_bytes"]
+    vb = (gpu.Lval.size - 1 + gpu.Uval.size - 1) * gpu.Lval.itemsize  # the caller's values
+    assert st["d2h_bytes"] == vb and st["h2d_bytes"] == vb
     pyoracle.oracle_factor([ref], 1, 1, A.n, False, an)
     err = cases.factor_error([gpu], [(ref.Lval[:-1], ref.Uval[:-1])])
     assert err < TOL[dtype], err
@@ -195,17 +196,22 @@ def test_gpu_graph_ordering_multichild_matches_oracle(kind, dims, dtype):
         assert np.abs(x - xt).max() / np.abs(xt).max() < 1e-10
 
 
-@pytest.mark.parametrize("kind,dims,dtype", [
-    (STENCIL_3D7, (20, 20, 20), 0),
-    (STENCIL_3D7, (24, 24, 24), 0),
-    (STENCIL_3D27, (14, 14, 14), 1),
-    (STENCIL_3D7, (12, 12, 12), 2),
-    (STENCIL_2D5, (60, 60, 1), 0),
+@pytest.mark.parametrize("kind,dims,dtype,amalg", [
+    (STENCIL_3D7, (20, 20, 20), 0, True),
+    (STENCIL_3D7, (20, 20, 20), 0, False),
+    (STENCIL_3D7, (24, 24, 24), 0, True),
+    (STENCIL_3D27, (14, 14, 14), 1, True),
+    (STENCIL_3D27, (14, 14, 14), 1, False),
+    (STENCIL_3D7, (12, 12, 12), 2, True),
+    (STENCIL_2D5, (60, 60, 1), 0, True),
 ])
-def test_gpu_reference_structure_matches_oracle(kind, dims, dtype):
+def test_gpu_reference_structure_matches_oracle(kind, dims, dtype, amalg, monkeypatch):
     """The LUstruct the reference's pdgssvx builds for a given perm_c (its
     own sp_colorder + symbfact + pddistribute, bench.py's headline
-    structure): many width-1 supernodes from the separators' borders."""
+    structure): many width-1 supernodes from the separators' borders.  The
+    plan factors the engine's coarse partition (csrc/amalg.h) and relays the
+    values into the caller's layout; SLU_AMALG=0 factors the fine one."""
+    monkeypatch.setenv("SLU_AMALG", "1" if amalg else "0")
     kw = dict(diag=6 - 0.25, diag_im=-0.0025) if dtype == 2 else {}
     A = Csc.stencil(kind, *dims, dtype=dtype, **kw)
     S = Symbolic(A, nd_order(*dims), 60, 256, reference=True)
@@ -217,6 +223,8 @@ def test_gpu_reference_structure_matches_oracle(kind, dims, dtype):
     err = cases.factor_error([gpu], [(ref.Lval, ref.Uval)])
     assert err < TOL[dtype], err
     assert abs(st["schur_flops"] + st["panel_flops"] - o["flops"]) <= 1e-9 * o["flops"] + 10
+    assert st["nsupers_in"] == S.nsupers
+    assert (st["nsupers"] < S.nsupers) == amalg
 
 
 @pytest.mark.skipif(not pyoracle.have_reference_harness(), reason="oracle/_ref not built")
