@@ -336,7 +336,19 @@ bool Amalg::build(int64_t n_, int ns, const int_t *xsup, const int_t *const *lid
             }
         }
         SLU_REQUIRE(q == lidx_len[J + 1] - lidx_len[J], "amalgamation: L index length of %d", J);
-        for (size_t i = 0; i < below.size(); ++i) rowpos[below[i]] = (int32_t)(wJ + i);
+        // rows ascending within each block below the diagonal (the layout is
+        // the engine's own: ascending rows keep the Schur scatter's
+        // destination addresses in runs)
+        {
+            i64 p = SLU_BC_HEADER + SLU_LB_DESCRIPTOR + wJ;
+            int32_t r = wJ;
+            for (i64 b = 1; b < L[0]; ++b) {
+                const i64 nr = L[p + 1];
+                std::sort(L + p + 2, L + p + 2 + nr);
+                for (i64 i = 0; i < nr; ++i) rowpos[L[p + 2 + i]] = r++;
+                p += SLU_LB_DESCRIPTOR + nr;
+            }
+        }
         // U index + D (U kind)
         const URow &U = urow[J];
         if (!U.blk.empty()) {

@@ -3277,16 +3277,33 @@ struct AmalgPlan : PlanBase {
                 if (fb >= SLOT) close(L);
             }
         };
+        // one piece per group and factor where the caller's arrays are
+        // contiguous over the group's members (pddistribute's *_dat layout),
+        // else one per member
         for (int L = 0; L < nl; ++L) {
-            for (int J : P.bylev[L])
-                for (int s = g0[J]; s < g0[J + 1]; ++s) {
-                    if (Llu->Lrowind_bc_ptr[s])
-                        add((const char *)(d_oL.p + lsrc[s]), (char *)Llu->Lnzval_bc_ptr[s],
-                            (lsrc[s + 1] - lsrc[s]) * (i64)sizeof(T), L);
-                    if (Llu->Ufstnz_br_ptr[s])
-                        add((const char *)(d_oU.p + usrc[s]), (char *)Llu->Unzval_br_ptr[s],
-                            (usrc[s + 1] - usrc[s]) * (i64)sizeof(T), L);
+            for (int J : P.bylev[L]) {
+                for (int pass = 0; pass < 2; ++pass) {
+                    const vector<i64> &off = pass ? usrc : lsrc;
+                    const T *dbase = pass ? d_oU.p : d_oL.p;
+                    auto hptr = [&](int s) -> char * {
+                        if (pass) return Llu->Ufstnz_br_ptr[s] ? (char *)Llu->Unzval_br_ptr[s] : nullptr;
+                        return Llu->Lrowind_bc_ptr[s] ? (char *)Llu->Lnzval_bc_ptr[s] : nullptr;
+                    };
+                    int a = g0[J];
+                    while (a < g0[J + 1]) {
+                        int b = a;
+                        while (b < g0[J + 1] && (off[b + 1] == off[b] || !hptr(b))) ++b; // empty
+                        if (b == g0[J + 1]) break;
+                        char *h0 = hptr(b);
+                        int e = b + 1;
+                        while (e < g0[J + 1] && (off[e + 1] == off[e] ||
+                                                 hptr(e) == h0 + (off[e] - off[b]) * (i64)sizeof(T)))
+                            ++e;
+                        add((const char *)(dbase + off[b]), h0, (off[e] - off[b]) * (i64)sizeof(T), L);
+                        a = e;
+                    }
                 }
+            }
             if (fb >= P.D2H_MIN || L + 1 == nl) close(L);
         }
         P.d_push.upload(P.h_push.empty() ? vector<PushSeg>(1) : P.h_push);

@@ -275,6 +275,7 @@ int slu_order_nd_grid(int nx, int ny, int nz, int64_t *perm_c) {
 // supernode partition and L / U structure are then exactly what the
 // reference's pdgssvx would hand pddistribute and pdgstrf for this perm_c.
 static void coarsen(slu_symb *S);
+static void glu_work(slu_symb *S);
 
 static slu_symb *symbolic_reference(const slu_csc *A, vector<int64_t> perm, int relax,
                                     int maxsup, bool coarse) {
@@ -315,8 +316,37 @@ static slu_symb *symbolic_reference(const slu_csc *A, vector<int64_t> perm, int 
     S->nnzL = (double)sz[3];
     S->nnzU = (double)sz[4];
     S->nsupers_fine = S->nsupers;
+    glu_work(S);
     if (coarse) coarsen(S);
     return S;
+}
+
+// The reference partition's algorithmic work from the Glu arrays (the
+// accounting of the plan and of csrc/amalg.h): per supernode the
+// diagonal LU, the L-panel TRSM over its rows below the diagonal block, and
+// per U segment (a usub entry is the first row of a column's segment in its
+// block row) the TRSV and the Schur update.
+static void glu_work(slu_symb *S) {
+    const int64_t ns = S->nsupers, n = S->n;
+    vector<int64_t> b(ns, 0);
+    double fl[6] = {0, 0, 0, 0, 0, 0};
+    for (int64_t s = 0; s < ns; ++s) {
+        const double w = (double)(S->xsup[s + 1] - S->xsup[s]);
+        const int64_t f = S->xsup[s];
+        b[s] = (S->xlsub[f + 1] - S->xlsub[f]) - (int64_t)w;
+        fl[5] += w;
+        fl[3] += w * (w - 1) / 2;
+        fl[4] += (w - 1) * w * (2 * w - 1) / 6;
+        fl[1] += w * (w + 1) * (double)b[s];
+    }
+    for (int64_t j = 0; j < n; ++j)
+        for (int64_t i = S->xusub[j]; i < S->xusub[j + 1]; ++i) {
+            const int64_t irow = S->usub[i], s = S->supno[irow];
+            const double seg = (double)(S->xsup[s + 1] - irow);
+            fl[2] += seg * (seg + 1);
+            fl[0] += 2.0 * (double)b[s] * seg;
+        }
+    for (int i = 0; i < 6; ++i) S->fl[i] = fl[i];
 }
 
 // Replace the reference's partition by the engine's coarse one (csrc/amalg.h):

@@ -139,3 +139,17 @@ def test_coarse_grid_distribution_matches_1x1():
     c = pyoracle.compare_blocksums(pyoracle.blocksums(one),
                                    np.concatenate([pyoracle.blocksums(lu) for lu in lus]))
     assert c["match"] and c["rel_err"] <= 1e-13, c
+
+
+@pytest.mark.parametrize("kind,dims,dtype", CASES)
+def test_reference_symbolic_work_is_the_oracle_accounting(kind, dims, dtype):
+    """Symbolic(reference=True).ref_flops(): the reference partition's work
+    (bench.py's rate) equals the oracle's count on that LUstruct."""
+    kw = dict(diag=6 - 0.25, diag_im=-0.0025) if dtype == 2 else {}
+    A = Csc.stencil(kind, *dims, dtype=dtype, **kw)
+    S = Symbolic(A, nd_order(*dims), 60, 256, reference=True)
+    lu = S.distribute(1, 1, 0, 0)
+    o = pyoracle.oracle_factor([lu], 1, 1, A.n, False, 1.0)
+    f = S.ref_flops()
+    assert f["nsupers"] == S.nsupers
+    assert abs(f["total"] - o["flops"]) <= 1e-9 * o["flops"] + 10
