@@ -289,11 +289,13 @@ bool Amalg::build(int64_t n_, int ns, const int_t *xsup, const int_t *const *lid
     Uvoff2.assign(ns2, -1);
     // D: U-kind entries (one per merged U column entry), then L-kind (w_J per J)
     const i64 DL0 = ucol_len[ns2];
-    D.resize(DL0 + n);
-    lcols.resize(ns);
-    lrow.resize(lmap[ns]);
-    ublks.resize(nub[ns]);
-    ufst.resize(fcol[ns]);
+    if (programs) {
+        D.resize(DL0 + n);
+        lcols.resize(ns);
+        lrow.resize(lmap[ns]);
+        ublks.resize(nub[ns]);
+        ufst.resize(fcol[ns]);
+    }
 
     // ---- pass 3b + 4: merged index arrays, D, expand programs (parallel)
     parallel_for(ns2, [&](int J) {
@@ -369,7 +371,7 @@ bool Amalg::build(int64_t n_, int ns, const int_t *xsup, const int_t *const *lid
                 for (int c = 0; c < W2(Jp); ++c, ++ce) {
                     const int32_t f = U.fst[ce];
                     X[p + SLU_UB_DESCRIPTOR + c] = f;
-                    D[d0 + ce] = Uvoff2[J] + seg - f;
+                    if (programs) D[d0 + ce] = Uvoff2[J] + seg - f;
                     seg += endJ - f;
                     nnz += endJ - f;
                 }
@@ -378,9 +380,9 @@ bool Amalg::build(int64_t n_, int ns, const int_t *xsup, const int_t *const *lid
             }
         }
         // D (L kind): row fst of column g inside J -> Lvoff2 + (g - x2J) * ld2 + fst - x2J
-        for (int c = 0; c < wJ; ++c) D[DL0 + x2J + c] = Lvoff2[J] + (i64)c * nsupr2 - x2J;
+        for (int c = 0; programs && c < wJ; ++c) D[DL0 + x2J + c] = Lvoff2[J] + (i64)c * nsupr2 - x2J;
         // expand programs of the members
-        for (int a = s0; a <= e; ++a) {
+        for (int a = s0; programs && a <= e; ++a) {
             const int_t *ix = lidx[a];
             LCol &C = lcols[a];
             C.src = lsrc[a];

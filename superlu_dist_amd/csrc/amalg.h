@@ -78,6 +78,7 @@ struct Amalg {
     std::vector<int32_t> ufst;  // first row of every original U column segment
     std::vector<int64_t> D;     // merged destination base per (merged row, column)
     int64_t n_merged_groups = 0, zeros = 0;
+    bool programs = true; // false: the coarse structure only (no expand / compress programs)
     // algorithmic work of the ORIGINAL partition (the reference's accounting,
     // SURVEY 8d; the plan's own counts are the coarse partition's): real-flop
     // sums, weighted by value type in the plan

@@ -326,6 +326,7 @@ struct LevelRange {
     int big_off = 0, big_n = 0; // 128x128 Schur tiles (first bigc_n: critical)
     int bigc_n = 0, tilec_n = 0; // critical tiles (destinations in the next level's panels)
     int df_off = 0, df_n = 0;   // fast diag items
+    int df_maxw = 0;            // widest of them
     int lf_off = 0, lf_n = 0;   // fast L-panel TRSM items
     int uf_off = 0, uf_n = 0;   // fast U-panel TRSM items
     int dc_off = 0, dc_n = 0;   // diag-package copy items (2D grids)
@@ -1428,6 +1429,7 @@ struct Plan : PlanBase {
                 }
             R.big_n = (int)tiles_big.size() - R.big_off;
             R.df_n = (int)df_items.size() - R.df_off;
+            for (int i = R.df_off; i < R.df_off + R.df_n; ++i) R.df_maxw = std::max(R.df_maxw, df_items[i].w);
             R.lf_n = (int)lf_items.size() - R.lf_off;
             R.uf_n = (int)uf_items.size() - R.uf_off;
             R.diag_n = (int)diag_items.size() - R.diag_off;
@@ -2241,6 +2243,10 @@ struct Plan : PlanBase {
                         hipLaunchKernelGGL(k_diag_lu_c<T>, dim3(R.df_n), dim3(DC_THREADS), 0, P,
                                            d_df.p + R.df_off, thresh, opts.replace_tiny_pivot,
                                            d_counters.p, d_zpiv.p);
+                    else if (R.df_maxw <= DF_SMALLW)
+                        hipLaunchKernelGGL((k_diag_lu_f<T, DF_SMALLW, DF_SMALL_THREADS>), dim3(R.df_n),
+                                           dim3(DF_SMALL_THREADS), 0, P, d_df.p + R.df_off, thresh,
+                                           opts.replace_tiny_pivot, d_counters.p, d_zpiv.p);
                     else
                         hipLaunchKernelGGL(k_diag_lu_f<T>, dim3(R.df_n), dim3(DF_THREADS), 0, P,
                                            d_df.p + R.df_off, thresh, opts.replace_tiny_pivot,

@@ -367,6 +367,7 @@ static void coarsen(slu_symb *S) {
         if (v.Uidx_off[s] >= 0) ui[s] = v.Uidx + v.Uidx_off[s];
     }
     slu::Amalg A;
+    A.programs = false; // the structure is all the coarse symbolic needs
     const bool merged = A.build(S->n, ns, S->xsup.data(), li.data(), ui.data(), 0.10, 256);
     slu_lustruct_free(LU, SLU_D);
     S->fl[0] = A.fl_schur; S->fl[1] = A.fl_trsm; S->fl[2] = A.fl_trsv;

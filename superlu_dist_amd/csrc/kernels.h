@@ -620,12 +620,20 @@ __device__ inline zc rlane(zc v, int l) { return {rlane(v.r, l), rlane(v.i, l)};
 //   3. the panel and U12 go back to global memory and A22 -= L21 U12 runs on
 //      MFMA with both operands in LDS, the next batch's loads in flight.
 constexpr int DF_THREADS = 512;
-template <typename T>
-__global__ void __launch_bounds__(DF_THREADS)
+// MAXW / NTHR: the widest block a launch holds and its workgroup size.  The
+// levels near the leaves hold thousands of narrow (relaxed) supernodes: a
+// <= 64-wide variant on 256 threads takes 50 KB of LDS instead of 150 KB,
+// so three workgroups share a CU instead of one.
+constexpr int DF_SMALLW = 64, DF_SMALL_THREADS = 256;
+template <typename T, int MAXW = FAST_MAXW, int NTHR = DF_THREADS>
+__global__ void __launch_bounds__(NTHR, NTHR == DF_SMALL_THREADS ? 2 : 1)
 k_diag_lu_f(const DiagItemF<T> *items, double thresh, int replace_tiny, int *tiny_count,
             int *zpiv) {
+    constexpr int DF_THREADS = NTHR; // (shadows the default for the loops below)
+    constexpr int FAST_MAXW = MAXW;
     constexpr int PW = PWOf<T>::v;
     constexpr int NW = DF_THREADS / 64;
+    static_assert(NW >= 2 && MAXW >= PW, "waves 0 and 1 form the inverses");
     using Sx = S<T>;
     using M = Mma<T>;
     const DiagItemF<T> it = items[blockIdx.x];

@@ -243,3 +243,35 @@ def test_gpu_reference_structure_fingerprints_match_reference_pdgstrf():
                                    want_blocksums=True, timeout=300)
     c = pyoracle.compare_blocksums(pyoracle.blocksums(lu), st["blocksums"])
     assert c["match"] and c["rel_err"] <= 1e-12, c
+
+
+def test_dropin_plan_cache_refactors_new_values(monkeypatch):
+    """The drop-in keeps its last 1x1 plan (pdgssvx's SamePattern_SameRowPerm
+    refactorization, abi.cpp): a second pdgstrf on the same LUstruct with new
+    values must factor the NEW values; a second LUstruct of the same pattern
+    (its own arrays) must not be served by the first one's plan."""
+    from superlu_dist_amd import capi
+    A = Csc.stencil(STENCIL_3D7, 16, 16, 16)
+    S = Symbolic(A, nd_order(16, 16, 16), 60, 256, reference=True)
+    lu, ref = S.distribute(), S.distribute()
+    L0, U0 = lu.Lval.copy(), lu.Uval.copy()
+    for scale in (1.0, 2.0, 0.5):             # same structure, new values each call
+        lu.Lval[:] = L0 * scale
+        lu.Uval[:] = U0 * scale
+        ref.Lval[:] = L0 * scale
+        ref.Uval[:] = U0 * scale
+        rv, info, _ = capi.pxgstrf(lu, 12.0 * scale)
+        assert rv == 0 and info == 0
+        pyoracle.oracle_factor([ref], 1, 1, A.n, False, 12.0 * scale)
+        err = cases.factor_error([lu], [(ref.Lval, ref.Uval)])
+        assert err < TOL[0], (scale, err)
+    other = S.distribute()                     # same pattern, other arrays
+    rv, info, _ = capi.pxgstrf(other, 12.0)
+    lu.Lval[:] = L0
+    lu.Uval[:] = U0
+    ref.Lval[:] = L0
+    ref.Uval[:] = U0
+    pyoracle.oracle_factor([ref], 1, 1, A.n, False, 12.0)
+    assert rv == 0 and info == 0
+    err = cases.factor_error([other], [(ref.Lval, ref.Uval)])
+    assert err < TOL[0], err
