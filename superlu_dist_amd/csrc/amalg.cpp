@@ -288,13 +288,14 @@ bool Amalg::build(int64_t n_, int ns, const int_t *xsup, const int_t *const *lid
     Uoff2.assign(ns2, -1);
     Uvoff2.assign(ns2, -1);
     // D: U-kind entries (one per merged U column entry), then L-kind (w_J per J)
-    const i64 DL0 = ucol_len[ns2];
+    DL0 = ucol_len[ns2];
+    SLU_REQUIRE(DL0 + n < (1ll << 31), "amalgamation: destination table exceeds int32");
     if (programs) {
         D.resize(DL0 + n);
         lcols.resize(ns);
         lrow.resize(lmap[ns]);
-        ublks.resize(nub[ns]);
-        ufst.resize(fcol[ns]);
+        urows.resize(ns);
+        ucol.resize(2 * fcol[ns]);
     }
 
     // ---- pass 3b + 4: merged index arrays, D, expand programs (parallel)
@@ -407,34 +408,31 @@ bool Amalg::build(int64_t n_, int ns, const int_t *xsup, const int_t *const *lid
                 }
             }
             const int_t *ux = uidx[a];
+            URowX &R = urows[a];
+            R.src = usrc[a];
+            R.c0 = fcol[a];
+            R.nc = (int32_t)(fcol[a + 1] - fcol[a]);
+            R.end = (int32_t)xsup[a + 1];
+            R.w = W(a);
+            R.pad = 0;
             if (!ux) continue;
-            i64 p = SLU_BR_HEADER, src = usrc[a], f0 = fcol[a], bi = nub[a];
-            const i64 enda = xsup[a + 1];
-            for (i64 b = 0; b < ux[0]; ++b, ++bi) {
+            i64 p = SLU_BR_HEADER, f0 = fcol[a];
+            for (i64 b = 0; b < ux[0]; ++b) {
                 const i64 jb = ux[p], w = W(jb);
-                UBlkX &B = ublks[bi];
-                B.src = src;
-                B.f0 = f0;
-                B.end = (int32_t)enda;
-                B.w = (int32_t)w;
-                B.pad = 0;
+                i64 d0;
                 if (grp[jb] == J) {
-                    B.kind = 1;
-                    B.d0 = DL0 + xsup[jb];
+                    d0 = DL0 + xsup[jb];
                 } else {
-                    B.kind = 0;
                     const int Jp = grp[jb];
                     const auto it = std::lower_bound(U.blk.begin(), U.blk.end(), Jp);
                     SLU_REQUIRE(it != U.blk.end() && *it == Jp,
                                 "amalgamation: U block (%d,%lld) not in merged row %d", a, (long long)jb, J);
-                    B.d0 = ucol_len[J] + U.colstart[it - U.blk.begin()] + (xsup[jb] - xsup2[Jp]);
+                    d0 = ucol_len[J] + U.colstart[it - U.blk.begin()] + (xsup[jb] - xsup2[Jp]);
                 }
-                for (i64 c = 0; c < w; ++c) {
-                    const i64 fst = ux[p + SLU_UB_DESCRIPTOR + c];
-                    ufst[f0 + c] = (int32_t)fst;
-                    src += enda - fst;
+                for (i64 c = 0; c < w; ++c, ++f0) {
+                    ucol[2 * f0] = (int32_t)(d0 + c);
+                    ucol[2 * f0 + 1] = (int32_t)ux[p + SLU_UB_DESCRIPTOR + c];
                 }
-                f0 += w;
                 p += SLU_UB_DESCRIPTOR + w;
             }
         }
@@ -498,13 +496,12 @@ template <typename T> void Amalg::apply(T *oL, T *oU, T *mL, T *mU, int dir) con
                 else *o = *m;
             }
     });
-    parallel_for((int)ublks.size(), [&](int b) {
-        const UBlkX &B = ublks[b];
-        i64 src = B.src;
-        T *M = B.kind ? mL : mU;
-        for (int c = 0; c < B.w; ++c) {
-            const i64 f = ufst[B.f0 + c], len = B.end - f;
-            T *m = M + D[B.d0 + c] + f;
+    parallel_for((int)urows.size(), [&](int a) {
+        const URowX &R = urows[a];
+        i64 src = R.src;
+        for (int c = 0; c < R.nc; ++c) {
+            const i64 d = ucol[2 * (R.c0 + c)], f = ucol[2 * (R.c0 + c) + 1], len = R.end - f;
+            T *m = (d >= DL0 ? mL : mU) + D[d] + f;
             for (i64 i = 0; i < len; ++i) {
                 if (dir == 0) m[i] = oU[src + i];
                 else oU[src + i] = m[i];

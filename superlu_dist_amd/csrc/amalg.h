@@ -63,19 +63,22 @@ struct Amalg {
         int32_t ld2;     // merged leading dimension
         int32_t pad;
     };
-    struct UBlkX {       // one original U block (a, jb)
-        int64_t src;     // value offset in the original U values
-        int64_t d0;      // D index of its first column
-        int64_t f0;      // ufst index of its first column
+    struct URowX {       // one original U block row a
+        int64_t src;     // value offset of its first segment in the original U values
+        int64_t c0;      // first of its column entries in ucol
+        int32_t nc;      // column entries (all columns of all its blocks)
         int32_t end;     // xsup[a + 1]
-        int32_t w;       // columns (width of jb)
-        int32_t kind;    // 0: into the merged U, 1: into the merged L diagonal block (jb in J)
+        int32_t w;       // width of a (segments are at most this long)
         int32_t pad;
     };
     std::vector<LCol> lcols;
     std::vector<int32_t> lrow;  // merged row position of every stored original L row
-    std::vector<UBlkX> ublks;
-    std::vector<int32_t> ufst;  // first row of every original U column segment
+    std::vector<URowX> urows;
+    // per original U column entry (block order, column order): the D index
+    // of its coarse destination (>= DL0: inside the coarse diagonal block, in
+    // the coarse L) and the first row of its segment
+    std::vector<int32_t> ucol;  // interleaved (didx, fst)
+    int64_t DL0 = 0;
     std::vector<int64_t> D;     // merged destination base per (merged row, column)
     int64_t n_merged_groups = 0, zeros = 0;
     bool programs = true; // false: the coarse structure only (no expand / compress programs)

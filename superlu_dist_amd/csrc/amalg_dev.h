@@ -32,25 +32,52 @@ __global__ void __launch_bounds__(256) k_amalg_l(const LColX *items, const int32
     }
 }
 
-// one thread per original U block (a, jb): its column segments, in order
+// one wave per original U block row: a wide row (w >= 16) column by column
+// with the lanes over the segment; a narrow one (every segment shorter than
+// 16) with the lanes over its columns, each lane's source offset from a wave
+// prefix sum of the segment lengths
 template <typename T>
-__global__ void __launch_bounds__(256) k_amalg_u(const Amalg::UBlkX *blks, int64_t nb,
-                                                 const int32_t *ufst, const int64_t *D, T *oU,
-                                                 T *mL, T *mU, int dir) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= nb) return;
-    const Amalg::UBlkX B = blks[i];
-    T *M = B.kind ? mL : mU;
-    int64_t src = B.src;
-    for (int c = 0; c < B.w; ++c) {
-        const int32_t f = ufst[B.f0 + c];
-        const int len = B.end - f;
-        T *m = M + D[B.d0 + c] + f;
-        for (int k = 0; k < len; ++k) {
-            if (dir == 0) m[k] = oU[src + k];
-            else oU[src + k] = m[k];
+__global__ void __launch_bounds__(256) k_amalg_u(const Amalg::URowX *rows, int nrows,
+                                                 const int32_t *ucol, const int64_t *D, int64_t DL0,
+                                                 T *oU, T *mL, T *mU, int dir) {
+    const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (r >= nrows) return;
+    const Amalg::URowX R = rows[r];
+    int64_t src = R.src;
+    const int2 *uc = (const int2 *)ucol + R.c0;
+    if (R.w >= 16) {
+        for (int c = 0; c < R.nc; ++c) {
+            const int2 e = uc[c];
+            const int len = R.end - e.y;
+            T *m = (e.x >= DL0 ? mL : mU) + D[e.x] + e.y;
+            for (int i = lane; i < len; i += 64) {
+                if (dir == 0) m[i] = oU[src + i];
+                else oU[src + i] = m[i];
+            }
+            src += len;
         }
-        src += len;
+        return;
+    }
+    for (int b = 0; b < R.nc; b += 64) {
+        const int c = b + lane;
+        int2 e = make_int2(0, R.end);
+        if (c < R.nc) e = uc[c];
+        const int len = R.end - e.y;
+        int incl = len; // inclusive prefix sum over the wave
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int v = __shfl_up(incl, d);
+            if (lane >= d) incl += v;
+        }
+        const int64_t o = src + incl - len;
+        if (len > 0) {
+            T *m = (e.x >= DL0 ? mL : mU) + D[e.x] + e.y;
+            for (int i = 0; i < len; ++i) {
+                if (dir == 0) m[i] = oU[o + i];
+                else oU[o + i] = m[i];
+            }
+        }
+        src += __shfl(incl, 63);
     }
 }
 

@@ -3088,8 +3088,8 @@ struct AmalgPlan : PlanBase {
     // caller layout on the device, and the relayout programs
     DevBuf<T> d_oL, d_oU;
     DevBuf<LColX> d_lx;
-    DevBuf<int32_t> d_lrow, d_ufst;
-    DevBuf<Amalg::UBlkX> d_ub;
+    DevBuf<int32_t> d_lrow, d_ucol;
+    DevBuf<Amalg::URowX> d_ur;
     DevBuf<i64> d_D;
     vector<i64> usrc; // caller U value offset per block row
     std::thread up_thread;
@@ -3199,29 +3199,26 @@ struct AmalgPlan : PlanBase {
             lx.insert(lx.end(), bl[L].begin(), bl[L].end());
             lx_lev[L + 1] = (int)lx.size();
         }
-        // U: the blocks of original block row a are ublks[ub0[a] .. ub0[a+1])
-        vector<Amalg::UBlkX> ub;
-        ub.reserve(A.ublks.size());
+        // U: the original block rows in level order
+        vector<Amalg::URowX> ur;
+        ur.reserve(ns);
         {
-            vector<i64> ub0(ns + 1, 0);
-            for (int s = 0; s < ns; ++s)
-                ub0[s + 1] = ub0[s] + (LU->Llu->Ufstnz_br_ptr[s] ? LU->Llu->Ufstnz_br_ptr[s][0] : 0);
-            SLU_REQUIRE(ub0[ns] == (i64)A.ublks.size(), "amalgamation: U block count");
             vector<vector<int>> rows(nl);
-            for (int s = 0; s < ns; ++s) rows[lev(s)].push_back(s);
+            for (int s = 0; s < ns; ++s)
+                if (A.urows[s].nc) rows[lev(s)].push_back(s);
             ub_lev.assign(nl + 1, 0);
             for (int L = 0; L < nl; ++L) {
-                for (int s : rows[L]) ub.insert(ub.end(), A.ublks.begin() + ub0[s], A.ublks.begin() + ub0[s + 1]);
-                ub_lev[L + 1] = (int)ub.size();
+                for (int s : rows[L]) ur.push_back(A.urows[s]);
+                ub_lev[L + 1] = (int)ur.size();
             }
         }
         nlx = (int)lx.size();
         if (lx.empty()) lx.push_back({0, 0, 0, 0, 0, 0, 0});
-        if (ub.empty()) ub.resize(1);
+        if (ur.empty()) ur.resize(1);
         d_lx.upload(lx);
-        d_ub.upload(ub);
+        d_ur.upload(ur);
         d_lrow.upload(A.lrow.empty() ? vector<int32_t>(1) : A.lrow);
-        d_ufst.upload(A.ufst.empty() ? vector<int32_t>(1) : A.ufst);
+        d_ucol.upload(A.ucol.empty() ? vector<int32_t>(2) : A.ucol);
         d_D.upload(A.D.empty() ? vector<i64>(1) : A.D);
     }
     int nlx = 0;
@@ -3232,10 +3229,11 @@ struct AmalgPlan : PlanBase {
         if (b > a)
             hipLaunchKernelGGL((k_amalg_l<T>), dim3(b - a), dim3(256), 0, st, d_lx.p + a, d_lrow.p,
                                d_oL.p, in->d_L.p, dir);
-        const i64 u0 = ub_lev[L0], nb = ub_lev[L1] - u0;
-        if (nb > 0)
-            hipLaunchKernelGGL((k_amalg_u<T>), dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, st,
-                               d_ub.p + u0, nb, d_ufst.p, d_D.p, d_oU.p, in->d_L.p, in->d_U.p, dir);
+        const int u0 = ub_lev[L0], nr = ub_lev[L1] - u0;
+        if (nr > 0)
+            hipLaunchKernelGGL((k_amalg_u<T>), dim3((unsigned)((nr + 3) / 4)), dim3(256), 0, st,
+                               d_ur.p + u0, nr, d_ucol.p, d_D.p, (i64)A.DL0, d_oU.p, in->d_L.p,
+                               in->d_U.p, dir);
         HIPCHK(hipGetLastError());
     }
 
