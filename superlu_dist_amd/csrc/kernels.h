@@ -89,6 +89,17 @@ template <> struct S<zc> {
     }
 };
 
+// v if c else 0 without control flow.  In k_schur_big a short-circuit
+// (c1 && c2) ? v : 0 at the LDS store let the compiler sink the global load
+// feeding v into a branch behind the stage's MFMAs, exposing its latency.
+__device__ __forceinline__ double keep_if(bool c, double v) {
+    return __longlong_as_double(__double_as_longlong(v) & -(long long)c);
+}
+__device__ __forceinline__ float keep_if(bool c, float v) {
+    return __int_as_float(__float_as_int(v) & -(int)c);
+}
+__device__ __forceinline__ zc keep_if(bool c, zc v) { return {keep_if(c, v.r), keep_if(c, v.i)}; }
+
 __device__ inline double one_of(double) { return 1.0; }
 __device__ inline float one_of(float) { return 1.0f; }
 __device__ inline zc one_of(zc) { return {1.0, 0.0}; }
@@ -843,8 +854,10 @@ k_diag_lu_f(const DiagItemF<T> *items, double thresh, int replace_tiny, int *tin
 #pragma unroll
                     for (int i = 0; i < 4; ++i) {
                         const int r = fr * 16 + M::row(lane, i), c = fc * 16 + (lane & 15);
-                        dst[q][i] = (f < nff && r < nbl && c < nbl) ? A22[r + (int64_t)c * ld]
-                                                                    : Sx::zero();
+                        // unconditional load from a clamped address + branch-free
+                        // mask: the next batch's loads stay ahead of the MFMAs
+                        const bool ok = (f < nff) & (r < nbl) & (c < nbl);
+                        dst[q][i] = keep_if(ok, A22[min(r, nbl - 1) + (int64_t)min(c, nbl - 1) * ld]);
                     }
                 }
             };
@@ -1395,12 +1408,12 @@ k_schur_big(const TileItem *tiles, const KInfo<T> *kinfo, T *Lval, T *Uval,
         for (int s = 0; s < AE; ++s) {
             const int kk = k0 + ak + (SB_THREADS / SB_BM) * s;
             sA[(ak + (SB_THREADS / SB_BM) * s) * LDS_A + ar] =
-                (avalid && kk < ki.kw) ? ra[s] : Sx::zero();
+                keep_if(avalid & (kk < ki.kw), ra[s]);
         }
 #pragma unroll
         for (int s = 0; s < BE; ++s) {
             const int t = ki.kmin + k0 + bk + s;
-            sB[(bk + s) * LDS_B + bc] = (bvalid && t <= tlast && t >= bt0) ? rb[s] : Sx::zero();
+            sB[(bk + s) * LDS_B + bc] = keep_if(bvalid & (t <= tlast) & (t >= bt0), rb[s]);
         }
     };
 

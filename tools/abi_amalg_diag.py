@@ -17,7 +17,8 @@ S = Symbolic(A, nd_order(nx, nx, nx), 60, 256, reference=True)
 lu = S.distribute(1, 1, 0, 0)
 L0, U0 = lu.Lval.copy(), lu.Uval.copy()
 out = {}
-for overlap in (False, True, True):
+modes = (False, True, True) if len(sys.argv) < 3 else tuple(m == "1" for m in sys.argv[2].split(","))
+for overlap in modes:
     lu.Lval[:] = L0
     lu.Uval[:] = U0
     t0 = time.perf_counter()
