@@ -32,44 +32,50 @@ __global__ void __launch_bounds__(256) k_amalg_l(const LColX *items, const int32
     }
 }
 
-// One wave per original U block row, 64 columns at a time: the lanes fetch
-// the columns' descriptors and coarse destinations in parallel and prefix-sum
-// the segment lengths (into LDS), then sweep the chunk's values -- contiguous
-// in the caller's layout -- one element per lane, each finding its column by
-// a binary search over the 64 prefix sums.  No dependent global load per
-// column (a column-at-a-time loop was 41 ms at 100^3, three load round trips
-// per column of the wide rows).
+// One wave per chunk of <= 64 columns of an original U block row (the
+// engine splits the rows; the top separators' rows hold thousands of columns
+// of segments up to 256 long).  The lanes fetch the chunk's column
+// descriptors and coarse destinations at once and prefix-sum the segment
+// lengths.  A chunk of short segments (<= 256 values) is then swept one value
+// per lane, each lane finding its column by binary search over the prefix
+// sums in LDS; a chunk of long segments goes column by column with the lanes
+// over the segment (coalesced on both sides).
+struct UChunk {
+    int64_t src; // value offset of the chunk's first segment (caller's layout)
+    int64_t c0;  // first column entry in ucol
+    int32_t nc;  // <= 64
+    int32_t end; // xsup[a + 1] of the row
+};
+
 template <typename T>
-__global__ void __launch_bounds__(256) k_amalg_u(const Amalg::URowX *rows, int nrows,
+__global__ void __launch_bounds__(256) k_amalg_u(const UChunk *chunks, int nchunks,
                                                  const int32_t *ucol, const int64_t *D, int64_t DL0,
                                                  T *oU, T *mL, T *mU, int dir) {
     __shared__ int s_incl[4][64];
     __shared__ int64_t s_dst[4][64]; // coarse offset of the column's first value, kind in bit 62
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int r = blockIdx.x * 4 + w;
-    if (r >= nrows) return; // (whole waves: no barrier below)
-    const Amalg::URowX R = rows[r];
-    int64_t src = R.src;
-    const int2 *uc = (const int2 *)ucol + R.c0;
-    for (int b = 0; b < R.nc; b += 64) {
-        const int c = b + lane;
-        int len = 0;
-        int64_t dst = 0;
-        if (c < R.nc) {
-            const int2 e = uc[c];
-            len = R.end - e.y;
-            dst = D[e.x] + e.y;
-            if (e.x >= DL0) dst |= (int64_t)1 << 62;
-        }
-        int incl = len;
+    if (r >= nchunks) return; // (whole waves: no barrier below)
+    const UChunk C = chunks[r];
+    constexpr int64_t KIND = (int64_t)1 << 62;
+    int len = 0;
+    int64_t dst = 0;
+    if (lane < C.nc) {
+        const int2 e = ((const int2 *)ucol)[C.c0 + lane];
+        len = C.end - e.y;
+        dst = D[e.x] + e.y;
+        if (e.x >= DL0) dst |= KIND;
+    }
+    int incl = len;
 #pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const int v = __shfl_up(incl, d);
-            if (lane >= d) incl += v;
-        }
+    for (int d = 1; d < 64; d <<= 1) {
+        const int v = __shfl_up(incl, d);
+        if (lane >= d) incl += v;
+    }
+    const int total = __shfl(incl, 63);
+    if (total <= 256) {
         s_incl[w][lane] = incl;
         s_dst[w][lane] = dst;
-        const int total = __shfl(incl, 63);
         __builtin_amdgcn_wave_barrier();
         for (int t = lane; t < total; t += 64) {
             int lo = 0, hi = 63; // first column j with incl[j] > t
@@ -80,12 +86,22 @@ __global__ void __launch_bounds__(256) k_amalg_u(const Amalg::URowX *rows, int n
             }
             const int start = lo ? s_incl[w][lo - 1] : 0;
             const int64_t d = s_dst[w][lo];
-            T *m = ((d >> 62) & 1 ? mL : mU) + (d & (((int64_t)1 << 62) - 1)) + (t - start);
-            if (dir == 0) *m = oU[src + t];
-            else oU[src + t] = *m;
+            T *m = (d & KIND ? mL : mU) + (d & (KIND - 1)) + (t - start);
+            if (dir == 0) *m = oU[C.src + t];
+            else oU[C.src + t] = *m;
         }
-        src += total;
-        __builtin_amdgcn_wave_barrier();
+        return;
+    }
+    const int excl = incl - len;
+    for (int j = 0; j < C.nc; ++j) {
+        const int lj = __shfl(len, j);
+        if (lj == 0) continue;
+        const int64_t off = C.src + __shfl(excl, j), d = __shfl(dst, j);
+        T *m = (d & KIND ? mL : mU) + (d & (KIND - 1));
+        for (int i = lane; i < lj; i += 64) {
+            if (dir == 0) m[i] = oU[off + i];
+            else oU[off + i] = m[i];
+        }
     }
 }
 

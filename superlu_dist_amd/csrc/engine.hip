@@ -3089,7 +3089,7 @@ struct AmalgPlan : PlanBase {
     DevBuf<T> d_oL, d_oU;
     DevBuf<LColX> d_lx;
     DevBuf<int32_t> d_lrow, d_ucol;
-    DevBuf<Amalg::URowX> d_ur;
+    DevBuf<UChunk> d_ur;
     DevBuf<i64> d_D;
     vector<i64> usrc; // caller U value offset per block row
     std::thread up_thread;
@@ -3180,7 +3180,7 @@ struct AmalgPlan : PlanBase {
     // Programs in level order of the coarse plan (so the D2H can compress a
     // level as soon as its panels are done): lx / ublks items of the groups
     // of level L at [lx_lev[L], lx_lev[L+1]) / [ub_lev[L], ub_lev[L+1]).
-    vector<int> lx_lev, ub_lev;
+    vector<int> lx_lev, ub_lev; // (ub_lev: U chunks)
     void build_programs() {
         const int nl = (int)in->levels.size();
         auto lev = [&](int s) { return in->level_of[A.grp[s]]; };
@@ -3199,16 +3199,23 @@ struct AmalgPlan : PlanBase {
             lx.insert(lx.end(), bl[L].begin(), bl[L].end());
             lx_lev[L + 1] = (int)lx.size();
         }
-        // U: the original block rows in level order
-        vector<Amalg::URowX> ur;
-        ur.reserve(ns);
+        // U: the original block rows in level order, in chunks of <= 64 columns
+        vector<UChunk> ur;
         {
             vector<vector<int>> rows(nl);
             for (int s = 0; s < ns; ++s)
                 if (A.urows[s].nc) rows[lev(s)].push_back(s);
             ub_lev.assign(nl + 1, 0);
             for (int L = 0; L < nl; ++L) {
-                for (int s : rows[L]) ur.push_back(A.urows[s]);
+                for (int s : rows[L]) {
+                    const Amalg::URowX &R = A.urows[s];
+                    i64 src = R.src;
+                    for (int c0 = 0; c0 < R.nc; c0 += 64) {
+                        const int nc = std::min(64, R.nc - c0);
+                        ur.push_back({src, R.c0 + c0, nc, R.end});
+                        for (int c = c0; c < c0 + nc; ++c) src += R.end - A.ucol[2 * (R.c0 + c) + 1];
+                    }
+                }
                 ub_lev[L + 1] = (int)ur.size();
             }
         }
