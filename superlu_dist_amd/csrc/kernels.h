@@ -100,6 +100,24 @@ __device__ __forceinline__ float keep_if(bool c, float v) {
 }
 __device__ __forceinline__ zc keep_if(bool c, zc v) { return {keep_if(c, v.r), keep_if(c, v.i)}; }
 
+// Staging loop "for (e = tid; e < n; e += NT) st(e, ld(e))" with the loads of
+// U consecutive iterations issued before their stores: ld(e, ok) must read a
+// valid address for every e < n + NT*U (callers clamp it) and return the
+// value masked by ok (keep_if).  A plain loop compiles to load -> wait ->
+// LDS store per iteration, a full global-memory round trip each (the
+// diagonal LU and TRSM kernels spent most of their time in such loops).
+template <int NT, int U, typename T, typename LD, typename ST>
+__device__ __forceinline__ void stage_loop(int tid, int n, LD ld, ST st) {
+    for (int e0 = tid; e0 < n; e0 += NT * U) {
+        T v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = ld(e0 + u * NT, e0 + u * NT < n);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (e0 + u * NT < n) st(e0 + u * NT, v[u]);
+    }
+}
+
 __device__ inline double one_of(double) { return 1.0; }
 __device__ inline float one_of(float) { return 1.0f; }
 __device__ inline zc one_of(zc) { return {1.0, 0.0}; }
@@ -668,14 +686,22 @@ k_diag_lu_f(const DiagItemF<T> *items, double thresh, int replace_tiny, int *tin
         // 1b multiply by zero: stale LDS there could be NaN, and 0 * NaN
         // would reach the stored U11^{-1})
         const int nrs = max(nrow, PW);
-        for (int e = tid; e < nrs * PW; e += DF_THREADS) {
-            const int r = e % nrs, c = e / nrs;
-            sP[r][c] = (c < pw && r < nrow) ? A11[r + (int64_t)c * ld] : Sx::zero();
-        }
-        for (int e = tid; e < nbl * PW; e += DF_THREADS) {
-            const int i = e % PW, c = e / PW;
-            sU[i][c] = i < pw ? A11[i + (int64_t)(pw + c) * ld] : Sx::zero();
-        }
+        stage_loop<DF_THREADS, 4, T>(
+            tid, nrs * PW,
+            [&](int e, bool ok) {
+                const int r = e % nrs, c = min(e / nrs, PW - 1);
+                return keep_if(ok & (c < pw) & (r < nrow),
+                               gld(A11 + min(r, nrow - 1) + (int64_t)min(c, pw - 1) * ld));
+            },
+            [&](int e, T v) { sP[e % nrs][e / nrs] = v; });
+        if (nbl > 0)
+            stage_loop<DF_THREADS, 4, T>(
+                tid, nbl * PW,
+                [&](int e, bool ok) {
+                    const int i = e % PW, c = min(e / PW, nbl - 1);
+                    return keep_if(ok & (i < pw), gld(A11 + min(i, pw - 1) + (int64_t)(pw + c) * ld));
+                },
+                [&](int e, T v) { sU[e % PW][e / PW] = v; });
         __syncthreads();
         // ---- 1. A11 = L11 U11 in registers (wave 0); meanwhile, on the first
         // panel, the other waves pull the trailing block into L2 (every
@@ -1724,20 +1750,25 @@ k_trsm_reg(const TrsmItemF<T> *items) {
     for (int b = 0; b < NBMAX; ++b) {
         if (b >= nb) break;
         __syncthreads();
-        for (int e = tid; e < PW * PW; e += 64 * TR_WAVES) sD[e / PW][e % PW] = it.dinv[(int64_t)b * PW * PW + e];
+        stage_loop<64 * TR_WAVES, 4, T>(
+            tid, PW * PW,
+            [&](int e, bool ok) { return keep_if(ok, gld(it.dinv + (int64_t)b * PW * PW + min(e, PW * PW - 1))); },
+            [&](int e, T v) { sD[e / PW][e % PW] = v; });
         const int kr = b * PW;
-        for (int e = tid; e < kr * PW; e += 64 * TR_WAVES) {
-            int i, j;
-            T v;
-            if (MODE == 0) {
-                i = e % kr; j = e / kr;
-                v = (b * PW + j < w) ? it.t[i + (int64_t)(b * PW + j) * it.ldt] : Sx::zero();
-            } else {
-                j = e % PW; i = e / PW;
-                v = (b * PW + j < w) ? it.t[(b * PW + j) + (int64_t)i * it.ldt] : Sx::zero();
-            }
-            sT[i][j] = v;
-        }
+        if (kr > 0)
+            stage_loop<64 * TR_WAVES, 8, T>(
+                tid, kr * PW,
+                [&](int e, bool ok) {
+                    const int ee = min(e, kr * PW - 1);
+                    const int i = MODE == 0 ? ee % kr : ee / PW, j = MODE == 0 ? ee / kr : ee % PW;
+                    const int col = min(b * PW + j, w - 1);
+                    const T *src = MODE == 0 ? it.t + i + (int64_t)col * it.ldt : it.t + col + (int64_t)i * it.ldt;
+                    return keep_if(ok & (b * PW + j < w), gld(src));
+                },
+                [&](int e, T v) {
+                    if (MODE == 0) sT[e % kr][e / kr] = v;
+                    else sT[e / PW][e % PW] = v;
+                });
         __syncthreads();
         typename M::acc_t a0 = M::zero(), a1 = M::zero();
 #pragma unroll
