@@ -143,8 +143,20 @@ typedef struct {
 typedef int (*slu_host_p2p_fn)(void *ctx, int nops, const slu_host_p2p_op *ops);
 slu_comm *slu_comm_create_host_p2p(slu_host_p2p_fn fn, void *ctx, int nprow,
                                    int npcol, int iam, int device);
-/* Ranks in group 0 / 1 / 2 of c (for RCCL: ncclCommCount of the world / row /
- * column communicator), -1 on error. */
+/* 3D grids (the reference's gridinfo3d_t, SRC/superlu_grid3d.c; pdgstrf3d,
+ * SRC/pdgstrf3d.c:121): npdep (a power of two) layers of an nprow x npcol
+ * grid, rank iam3d = layer * nprow * npcol + row * npcol + column.  Group 3
+ * of the communicator joins the ranks at my (row, column) of every layer
+ * (the reference's grid3d->zscp); the plan of a 3D communicator factors the
+ * layer's forests of the supernodal etree and reduces the ancestors between
+ * layers (see slu_plan_gather3d).  The _host_p2p3d variant is the
+ * point-to-point test transport with group 3 added (peer = layer). */
+slu_comm *slu_comm_create3d(const void *uid128, int nprow, int npcol, int npdep,
+                            int iam3d, int device);
+slu_comm *slu_comm_create_host_p2p3d(slu_host_p2p_fn fn, void *ctx, int nprow,
+                                     int npcol, int npdep, int iam3d, int device);
+/* Ranks in group 0 / 1 / 2 / 3 of c (for RCCL: ncclCommCount of the layer's
+ * world / row / column communicator or of the layer group), -1 on error. */
 int slu_comm_size(const slu_comm *c, int group);
 void slu_comm_destroy(slu_comm *c);
 
@@ -233,6 +245,12 @@ int slu_plan_refine(slu_plan *p, const void *b, void *x, int64_t ld, int nrhs, d
  * section is checked byte for byte against what its root wrote.  Collective;
  * returns 0 and the number / bytes of sections this rank received. */
 int slu_plan_check_exchange(slu_plan *p, int64_t *nsections, int64_t *nbytes);
+/* 3D plans, after slu_plan_factor (collective over the layers): the factored
+ * forests travel to layer 0, whose ranks then hold every supernode's final
+ * L / U values (pdgssvx3d's dgatherAllFactoredLU, SRC/pd3dcomm.c:816);
+ * the other layers' storage is left partial.  slu_plan_download then gives
+ * the factors on layer 0. */
+int slu_plan_gather3d(slu_plan *p);
 void slu_plan_destroy(slu_plan *p);
 
 /* Plan statistics (algorithmic work of one factorization on this rank). */
@@ -275,6 +293,12 @@ typedef struct {
     double t_amalg_ms;         /* host analysis + programs (part of t_plan_ms) */
     double t_expand_ms;        /* device relayout caller -> coarse (last upload) */
     double t_compress_ms;      /* device relayout coarse -> caller (last download) */
+    /* 3D grids (timing on): device time of each of this layer's phases
+     * (phase p = the forest at level p, 0 = leaves) and of its ancestor
+     * reductions, last slu_plan_factor */
+    double t_phase_ms[8];
+    double t_zreduce_ms;
+    int64_t npdep, zlayer, phase_last; /* 3D: layers, mine, my last phase */
 } slu_plan_stats;
 int slu_plan_get_stats(const slu_plan *p, slu_plan_stats *st);
 

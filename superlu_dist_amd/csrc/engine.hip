@@ -108,6 +108,11 @@ template <typename T> struct DevBuf {
 struct slu_comm {
     int nprow = 1, npcol = 1, iam = 0, myrow = 0, mycol = 0, device = 0;
     ncclComm_t world = nullptr, row = nullptr, col = nullptr;
+    // 3D grids (SRC/superlu_grid3d.c: Pz layers of a Pr x Pc grid, the
+    // reference's grid3d->zscp): world / row / col above are the layer's,
+    // zcomm joins the ranks at my (row, column) position of every layer
+    int npdep = 1, zlayer = 0;
+    ncclComm_t all = nullptr, zcomm = nullptr;
     slu_host_bcast_fn host_fn = nullptr;
     slu_host_p2p_fn host_p2p = nullptr; // point-to-point test transport
     void *host_ctx = nullptr;
@@ -117,7 +122,7 @@ namespace slu {
 
 using i64 = int64_t;
 
-enum { G_WORLD = 0, G_ROW = 1, G_COL = 2 };
+enum { G_WORLD = 0, G_ROW = 1, G_COL = 2, G_Z = 3 };
 
 // Grouped broadcasts of device buffers within the world / a process row /
 // a process column.  Ops are queued and issued together by flush() (one
@@ -136,10 +141,14 @@ struct Xport {
     vector<char> hbuf;
     double sent = 0, recvd = 0; // bytes this rank moved (RCCL sections)
     int gsize(int g) const {
-        return g == G_WORLD ? c->nprow * c->npcol : g == G_ROW ? c->npcol : c->nprow;
+        return g == G_WORLD ? c->nprow * c->npcol : g == G_ROW ? c->npcol : g == G_COL ? c->nprow : c->npdep;
     }
-    int grank(int g) const { return g == G_WORLD ? c->iam : g == G_ROW ? c->mycol : c->myrow; }
-    ncclComm_t comm_of(int g) const { return g == G_WORLD ? c->world : g == G_ROW ? c->row : c->col; }
+    int grank(int g) const {
+        return g == G_WORLD ? c->iam : g == G_ROW ? c->mycol : g == G_COL ? c->myrow : c->zlayer;
+    }
+    ncclComm_t comm_of(int g) const {
+        return g == G_WORLD ? c->world : g == G_ROW ? c->row : g == G_COL ? c->col : c->zcomm;
+    }
     void bcast(int g, int root, void *buf, size_t bytes) {
         if (bytes && gsize(g) > 1) ops.push_back({g, root, buf, bytes, ~0u});
     }
@@ -345,6 +354,33 @@ struct Sec {
     uint32_t mask;      // group ranks that receive the section
 };
 
+// 3D grids: one chunk (<= ZR_CHUNK values) of a contiguous range of this
+// rank's L (arr 0) or U (arr 1) values -- a block column L(:,k) or block row
+// U(k,:) of an ancestor supernode -- zeroed, packed into the exchange
+// buffer, added from it (ancestor reduction, SRC/pd3dcomm.c:704-730: alpha =
+// beta = 1) or copied from it (gather of the factored forests,
+// SRC/pd3dcomm.c:733-760: alpha = 0).  HBM-bound copies, lanes over values.
+struct ZRange {
+    int64_t off, boff;
+    int32_t len, arr;
+};
+enum { ZR_ZERO = 0, ZR_PACK = 1, ZR_ADD = 2, ZR_COPY = 3 };
+constexpr int ZR_CHUNK = 1 << 16;
+
+template <typename T>
+__global__ void __launch_bounds__(256) k_zranges(const ZRange *r, T *L, T *U, T *buf, int op) {
+    const ZRange z = r[blockIdx.x];
+    T *v = (z.arr ? U : L) + z.off;
+    T *b = buf + z.boff;
+    using Sx = S<T>;
+    for (int i = threadIdx.x; i < z.len; i += 256) {
+        if (op == ZR_ZERO) v[i] = Sx::zero();
+        else if (op == ZR_PACK) b[i] = v[i];
+        else if (op == ZR_ADD) v[i] = Sx::sub(v[i], Sx::neg(b[i]));
+        else v[i] = b[i];
+    }
+}
+
 struct PlanBase {
     virtual ~PlanBase() = default;
     virtual void upload() = 0;
@@ -359,6 +395,7 @@ struct PlanBase {
     virtual void fill_a(const void *a, int on_device) = 0;
     virtual void refine(const void *b, void *x, int64_t ld, int nrhs, double *berr, int *steps) = 0;
     virtual void check_exchange(int64_t *nsec, int64_t *nbytes) = 0;
+    virtual void gather_layers() { throw Error("gather_layers: not a 3D plan"); }
     slu_plan_stats stats{};
 };
 
@@ -423,6 +460,27 @@ struct Plan : PlanBase {
     vector<int> level_of;
     vector<vector<int>> bylev;
     vector<LevelRange> levels;
+
+    // ---- 3D grids (pdgstrf3d, SRC/pdgstrf3d.c:121-348).  Pz = 2^(maxlvl-1)
+    // layers, each a Pr x Pc grid holding the whole LUstruct; the supernodal
+    // etree is cut into 2^maxlvl - 1 forests (heap order: 0 = the top
+    // ancestors, 2t+1 / 2t+2 the two halves below forest t).  Layer z factors
+    // its leaf forest, then (phase p >= 1, layers with z % 2^p == 0) the
+    // forest above, after adding the partner layer's partial updates of every
+    // ancestor block (reduction at the end of phase p-1 between z and
+    // z + 2^(p-1)); only the layer that factors an ancestor forest starts it
+    // from A's values, the others from zero (SRC/pd3dcomm.c:754-771).
+    bool zmode = false;
+    int npdep = 1, zl = 0, maxlvl = 1, my_last = 0;
+    vector<int> forest_of, phase_of; // per supernode; phase -1: not factored here
+    vector<int> phase_lv;            // my phase p = levels [phase_lv[p], phase_lv[p+1])
+    vector<int> zr_off;              // zero ranges [zr_off[0], zr_off[1]); reduction p: [zr_off[p+1], zr_off[p+2])
+    vector<i64> zr_cnt;              // values exchanged by reduction p
+    vector<ZRange> zr;
+    DevBuf<ZRange> d_zr;
+    DevBuf<T> d_zbuf;
+    vector<i64> uval_len;
+    double zbytes = 0; // reduction bytes sent + received per factorization
     vector<DiagItem<T>> diag_items;
     vector<TrsmLItem<T>> tl_items;
     vector<TrsmUItem<T>> tu_items;
@@ -480,6 +538,15 @@ struct Plan : PlanBase {
         xmode = Pr * Pc > 1;
         SLU_REQUIRE(!xmode || (comm && (comm->world || comm->host_fn || comm->host_p2p)),
                     "a %dx%d grid needs a communicator (slu_comm_create)", Pr, Pc);
+        zmode = comm && comm->npdep > 1;
+        if (zmode) {
+            npdep = comm->npdep;
+            zl = comm->zlayer;
+            while ((1 << (maxlvl - 1)) < npdep) ++maxlvl;
+            SLU_REQUIRE(comm->zcomm || comm->host_p2p,
+                        "a 3D grid needs RCCL (slu_comm_create3d) or the point-to-point host transport");
+            SLU_REQUIRE(!(o && o->overlap_download), "3D grids: no overlapped download (factors are spread over the layers)");
+        }
         if (xmode)
             SLU_REQUIRE(comm->nprow == Pr && comm->npcol == Pc && comm->iam == iam,
                         "communicator is for a %dx%d grid rank %d, plan for %dx%d rank %d",
@@ -505,6 +572,7 @@ struct Plan : PlanBase {
             exchange_needs();
             compute_levels();
             layout_values();
+            if (zmode) build_zranges(false);
             return;
         }
         if (comm) HIPCHK(hipSetDevice(comm->device));
@@ -571,6 +639,7 @@ struct Plan : PlanBase {
             tick("compute_levels");
             layout_values();
             tick("layout_values");
+            if (zmode) build_zranges(true);
             build_schedule();
             if (prof)
                 fprintf(stderr, "[slu plan %d]   (add_supernode %.1f ms, merge + atomics %.1f ms)\n",
@@ -614,7 +683,10 @@ struct Plan : PlanBase {
             return sc.g == G_ROW ? myrow * Pc + sc.root : sc.root * Pc + mycol;
         };
         i64 ns = 0, nb = 0;
-        for (size_t L = 0; L < levels.size(); ++L) {
+        const int nzp = zmode ? my_last + 1 : 1;
+        for (int zp = 0; zp < nzp; ++zp) {
+        const size_t L0 = zmode ? phase_lv[zp] : 0, L1 = zmode ? phase_lv[zp + 1] : levels.size();
+        for (size_t L = L0; L < L1; ++L) {
             const LevelRange &R = levels[L];
             for (int ph = 0; ph < 2; ++ph) {
                 const vector<Sec> &secs = ph ? psecs : dsecs;
@@ -661,10 +733,33 @@ struct Plan : PlanBase {
                 }
             }
         }
+        if (zmode && zp < maxlvl - 1) { // the ancestor reduction after my phase zp
+            const bool recv = zl % (2 << zp) == 0;
+            const int peer = recv ? zl + (1 << zp) : zl - (1 << zp), root = recv ? peer : zl;
+            const size_t bytes = (size_t)zr_cnt[zp] * sizeof(T);
+            vector<unsigned char> zb(std::max<size_t>(bytes, 1), 0);
+            if (!recv)
+                for (size_t b = 0; b < bytes; ++b) zb[b] = pat(1000000 + zp, 0, root, iam, b);
+            X.section(G_Z, root, 1u << (recv ? zl : peer), zb.data(), bytes);
+            X.flush();
+            if (recv && bytes) {
+                for (size_t b = 0; b < bytes; ++b)
+                    SLU_REQUIRE(zb[b] == pat(1000000 + zp, 0, root, iam, b),
+                                "3D reduction %d: byte %zu from layer %d differs", zp, b, root);
+                ++ns;
+                nb += (i64)bytes;
+            }
+        }
+        }
         // the final info reduction of factor()
         vector<i64> mine(1, iam);
         auto all = X.allgatherv(G_WORLD, mine);
         for (int r = 0; r < Pr * Pc; ++r) SLU_REQUIRE(all[r].size() == 1 && all[r][0] == r, "info all-gather");
+        if (zmode) {
+            mine[0] = zl;
+            auto az = X.allgatherv(G_Z, mine);
+            for (int z = 0; z < npdep; ++z) SLU_REQUIRE(az[z].size() == 1 && az[z][0] == z, "3D info all-gather");
+        }
         *nsec = ns;
         *nbytes = nb;
     }
@@ -716,12 +811,14 @@ struct Plan : PlanBase {
         }
         lval_total = off;
         uval_off.assign(nlr, -1);
+        uval_len.assign(nlr, 0);
         off = 0;
         u_contig = Llu->Unzval_br_dat != nullptr;
         for (int lb = 0; lb < nlr; ++lb) {
             const int_t *index = Llu->Ufstnz_br_ptr[lb];
             if (!index) continue;
             uval_off[lb] = off;
+            uval_len[lb] = index[1];
             if (Llu->Unzval_br_dat && (HT *)Llu->Unzval_br_ptr[lb] != (HT *)Llu->Unzval_br_dat + off)
                 u_contig = false;
             off += index[1];
@@ -1018,6 +1115,7 @@ struct Plan : PlanBase {
                             (long long)v[e], (long long)v[e + 1]);
                 tgt[fill[v[e]]++] = (int)v[e + 1];
             }
+        if (zmode) return compute_levels_3d(cnt, tgt);
         level_of.assign(nsupers, 0);
         int maxlev = 0;
         for (int k = 0; k < nsupers; ++k) {
@@ -1031,6 +1129,290 @@ struct Plan : PlanBase {
         stats.nsupers = nsupers;
         stats.nsupers_in = nsupers;
         stats.nlevels = maxlev + 1;
+    }
+
+    // ------------------------------------------------------- 3D forests
+    // The forest partition of SRC/supernodalForest.c (getGreedyLoadBalForests
+    // :794, iterativeFrPartitioning :618, getLoadImbalance :463): starting
+    // from the etree's roots, while the two-way greedy split of the current
+    // tree set is more than 20 % imbalanced (and fewer than 1024 trees), the
+    // heaviest tree's single-child chain from its root down to the first
+    // branching goes to the ancestor forest and the branch's children replace
+    // it; the set is then split greedily (heaviest first, into the lighter
+    // half) and each half is partitioned the same way one level down; the
+    // halves at the bottom are the layers' leaf forests.  The tree is the
+    // elimination tree of the block dependency DAG (Liu's algorithm with path
+    // compression over the DAG's edges), so every supernode a block column
+    // or row of k updates is an ancestor of k -- the property the phases rely
+    // on.  Weights estimate each supernode's Schur work, w * m^2 with m the
+    // summed widths of its successors (the reference's scuWeight, from the
+    // same block structure).
+    void compute_forests(const vector<i64> &cnt, const vector<int> &tgt) {
+        const int ns = nsupers;
+        vector<int> parent(ns, -1), anc(ns, -1);
+        {   // edges by target
+            vector<i64> rc(ns + 1, 0);
+            for (int k = 0; k < ns; ++k)
+                for (i64 e = cnt[k]; e < cnt[k + 1]; ++e) rc[tgt[e] + 1]++;
+            for (int k = 0; k < ns; ++k) rc[k + 1] += rc[k];
+            vector<int> src(rc[ns]);
+            vector<i64> f(rc.begin(), rc.end() - 1);
+            for (int k = 0; k < ns; ++k)
+                for (i64 e = cnt[k]; e < cnt[k + 1]; ++e) src[f[tgt[e]]++] = k;
+            for (int t = 0; t < ns; ++t)
+                for (i64 e = rc[t]; e < rc[t + 1]; ++e) {
+                    int r = src[e];
+                    while (anc[r] != -1 && anc[r] != t) { // root of r's current subtree
+                        const int nx = anc[r];
+                        anc[r] = t;                       // path compression
+                        r = nx;
+                    }
+                    if (anc[r] == -1 && r != t) {
+                        parent[r] = t;
+                        anc[r] = t;
+                    }
+                }
+        }
+        vector<double> wt(ns, 0), sub(ns, 0);
+        for (int k = 0; k < ns; ++k) {
+            double m = 0;
+            for (i64 e = cnt[k]; e < cnt[k + 1]; ++e) m += W(tgt[e]);
+            wt[k] = (double)W(k) * (m * m + (double)W(k) * W(k) / 3.0) + 1.0;
+        }
+        vector<vector<int>> kids(ns);
+        vector<int> roots;
+        for (int k = 0; k < ns; ++k) {
+            sub[k] += wt[k];
+            if (parent[k] >= 0) {
+                sub[parent[k]] += sub[k];
+                kids[parent[k]].push_back(k);
+            } else {
+                roots.push_back(k);
+            }
+        }
+        const int nf = (1 << maxlvl) - 1;
+        forest_of.assign(ns, -1);
+        vector<vector<int>> heads((size_t)nf);
+        heads[0] = roots;
+        auto split2 = [&](vector<int> set, vector<int> *out) {
+            std::stable_sort(set.begin(), set.end(), [&](int a, int b) { return sub[a] > sub[b]; });
+            double w[2] = {0, 0};
+            for (int t : set) {
+                const int h = w[0] > w[1] ? 1 : 0;
+                w[h] += sub[t];
+                if (out) out[h].push_back(t);
+            }
+            return w[0] + w[1] > 0 ? std::fabs(w[0] - w[1]) / (w[0] + w[1]) : 0.0;
+        };
+        auto mark_subtrees = [&](const vector<int> &hs, int f) {
+            vector<int> st(hs.begin(), hs.end());
+            while (!st.empty()) {
+                const int v = st.back();
+                st.pop_back();
+                forest_of[v] = f;
+                for (int c : kids[v]) st.push_back(c);
+            }
+        };
+        if (maxlvl == 1) mark_subtrees(heads[0], 0);
+        for (int lvl = 0; lvl < maxlvl - 1; ++lvl)
+            for (int tr = (1 << lvl) - 1; tr < (1 << (lvl + 1)) - 1; ++tr) {
+                vector<int> set = heads[tr];
+                while (split2(set, nullptr) > 0.2 && set.size() < 1024) {
+                    size_t idx = 0;
+                    for (size_t i = 1; i < set.size(); ++i)
+                        if (sub[set[i]] > sub[set[idx]]) idx = i;
+                    int v = set[idx];
+                    while (kids[v].size() == 1) v = kids[v][0];
+                    if (kids[v].empty()) break;
+                    for (int u = set[idx];; u = kids[u][0]) { // the chain joins the ancestors
+                        forest_of[u] = tr;
+                        if (u == v) break;
+                    }
+                    set.erase(set.begin() + idx);
+                    set.insert(set.end(), kids[v].begin(), kids[v].end());
+                }
+                vector<int> half[2];
+                split2(set, half);
+                if (lvl == maxlvl - 2) {
+                    mark_subtrees(half[0], 2 * tr + 1);
+                    mark_subtrees(half[1], 2 * tr + 2);
+                } else {
+                    heads[2 * tr + 1] = half[0];
+                    heads[2 * tr + 2] = half[1];
+                }
+            }
+        for (int k = 0; k < ns; ++k) SLU_REQUIRE(forest_of[k] >= 0, "supernode %d in no forest", k);
+    }
+
+    // heap index of layer z's forest at level ilvl (0 = leaves), as
+    // SRC/supernodal_etree.c:802-812 (getGridTrees)
+    int tree_of(int z, int ilvl) const {
+        int t = npdep - 1 + z;
+        for (int i = 0; i < ilvl; ++i) t = (t - 1) / 2;
+        return t;
+    }
+    int ilvl_of_forest(int f) const { // 0 = leaves
+        int d = 0;
+        while ((2 << d) - 1 <= f) ++d;
+        return maxlvl - 1 - d;
+    }
+
+    void compute_levels_3d(const vector<i64> &cnt, const vector<int> &tgt) {
+        compute_forests(cnt, tgt);
+        my_last = 0;
+        while (my_last < maxlvl - 1 && zl % (2 << my_last) == 0) ++my_last;
+        phase_of.assign(nsupers, -1);
+        for (int k = 0; k < nsupers; ++k) {
+            const int il = ilvl_of_forest(forest_of[k]);
+            if (forest_of[k] == tree_of(zl, il) && il <= my_last) phase_of[k] = il;
+        }
+        // every block a factored supernode updates lies on this layer's path
+        // of forests at its phase or above (the partition's invariant)
+        for (int k = 0; k < nsupers; ++k) {
+            if (phase_of[k] < 0) continue;
+            for (i64 e = cnt[k]; e < cnt[k + 1]; ++e) {
+                const int t = tgt[e], il = ilvl_of_forest(forest_of[t]);
+                SLU_REQUIRE(il >= phase_of[k] && forest_of[t] == tree_of(zl, il),
+                            "3D forests: supernode %d (phase %d) updates %d outside its path", k,
+                            phase_of[k], t);
+            }
+        }
+        vector<int> lin(nsupers, 0);
+        vector<int> depth(maxlvl, 0);
+        for (int k = 0; k < nsupers; ++k) {
+            if (phase_of[k] < 0) continue;
+            depth[phase_of[k]] = std::max(depth[phase_of[k]], lin[k] + 1);
+            for (i64 e = cnt[k]; e < cnt[k + 1]; ++e)
+                if (phase_of[tgt[e]] == phase_of[k]) lin[tgt[e]] = std::max(lin[tgt[e]], lin[k] + 1);
+        }
+        phase_lv.assign(my_last + 2, 0);
+        for (int p = 0; p <= my_last; ++p) phase_lv[p + 1] = phase_lv[p] + depth[p];
+        const int nl = phase_lv[my_last + 1];
+        level_of.assign(nsupers, -1);
+        bylev.assign(nl, {});
+        for (int k = 0; k < nsupers; ++k)
+            if (phase_of[k] >= 0) {
+                level_of[k] = phase_lv[phase_of[k]] + lin[k];
+                bylev[level_of[k]].push_back(k);
+            }
+        levels.assign(nl, LevelRange{});
+        int nf = 0;
+        for (int k = 0; k < nsupers; ++k) nf += phase_of[k] >= 0;
+        stats.npdep = npdep;
+        stats.zlayer = zl;
+        stats.phase_last = my_last;
+        stats.nsupers = nf;
+        stats.nsupers_in = nsupers;
+        stats.nlevels = nl;
+    }
+
+    // local value ranges of supernode k's L block column / U block row,
+    // appended to zr in chunks (buffer positions from *bo on)
+    void add_zranges(int k, i64 *bo) {
+        auto add = [&](i64 off, i64 len, int arr) {
+            for (i64 c = 0; c < len; c += ZR_CHUNK) {
+                const int l = (int)std::min<i64>(ZR_CHUNK, len - c);
+                zr.push_back(ZRange{off + c, *bo, l, arr});
+                *bo += l;
+            }
+        };
+        if (k % Pc == mycol && lval_off[k / Pc] >= 0)
+            add(lval_off[k / Pc], (i64)lval_ld[k / Pc] * W(k), 0);
+        if (k % Pr == myrow && uval_off[k / Pr] >= 0) add(uval_off[k / Pr], uval_len[k / Pr], 1);
+    }
+
+    void build_zranges(bool device) {
+        zr.clear();
+        zr_off.assign(1, 0);
+        zr_cnt.clear();
+        i64 bo = 0;
+        // ancestor forests this layer does not factor start from zero
+        for (int k = 0; k < nsupers; ++k) {
+            const int il = ilvl_of_forest(forest_of[k]);
+            if (il >= 1 && forest_of[k] == tree_of(zl, il) && il > my_last) add_zranges(k, &bo);
+        }
+        zr_off.push_back((int)zr.size());
+        // reduction after phase p: every ancestor forest above it on my path
+        i64 mx = 0;
+        for (int p = 0; p < maxlvl - 1; ++p) {
+            bo = 0;
+            if (p <= my_last)
+                for (int k = 0; k < nsupers; ++k) {
+                    const int il = ilvl_of_forest(forest_of[k]);
+                    if (il > p && forest_of[k] == tree_of(zl, il)) add_zranges(k, &bo);
+                }
+            zr_off.push_back((int)zr.size());
+            zr_cnt.push_back(bo);
+            mx = std::max(mx, bo);
+        }
+        if (!device) return;
+        d_zr.upload(zr);
+        d_zbuf.alloc(std::max<i64>(mx, 1));
+    }
+
+    void launch_zranges(int a, int b, int op, hipStream_t st) {
+        if (b > a)
+            hipLaunchKernelGGL(k_zranges<T>, dim3(b - a), dim3(256), 0, st, d_zr.p + a, d_L.p, d_U.p,
+                               d_zbuf.p, op);
+    }
+
+    // ancestor reduction at the end of phase p (SRC/pd3dcomm.c:786-813):
+    // layer z + 2^p sends its partial sums, layer z adds them
+    void zreduce(int p, hipStream_t st) {
+        const bool recv = zl % (2 << p) == 0;
+        const int peer = recv ? zl + (1 << p) : zl - (1 << p);
+        const int a = zr_off[p + 1], b = zr_off[p + 2];
+        const i64 cnt = zr_cnt[p];
+        if (!recv) launch_zranges(a, b, ZR_PACK, st);
+        X.s = st;
+        X.section(G_Z, recv ? peer : zl, 1u << (recv ? zl : peer), d_zbuf.p, (size_t)cnt * sizeof(T));
+        X.flush();
+        zbytes += (double)cnt * sizeof(T);
+        if (recv) launch_zranges(a, b, ZR_ADD, st);
+    }
+
+    // After factor(): the factored forests travel to layer 0 (every layer's
+    // part of it), as pdgssvx3d's dgatherAllFactoredLU (SRC/pd3dcomm.c:816-858).
+    void gather_layers() override {
+        SLU_REQUIRE(zmode, "gather_layers: not a 3D plan");
+        SLU_REQUIRE(vstate == 2, "gather_layers: factor first");
+        sync();
+        hipStream_t st = stream;
+        for (int il = 0; il < maxlvl - 1; ++il) {
+            if (zl % (1 << il)) break;
+            const bool recv = zl % (2 << il) == 0;
+            const int sender = recv ? zl + (1 << il) : zl, peer = recv ? sender : zl - (1 << il);
+            // forests the sender's half of the layers factored: at level a
+            // <= il, trees (2^(maxlvl-1-a) - 1) + (sender >> a) + [0, 2^(il-a))
+            vector<char> want((size_t)(1 << maxlvl), 0);
+            for (int a = 0; a <= il; ++a) {
+                const int t0 = (1 << (maxlvl - 1 - a)) - 1 + (sender >> a);
+                for (int t = t0; t < t0 + (1 << (il - a)); ++t) want[t] = 1;
+            }
+            vector<ZRange> keep;
+            keep.swap(zr);
+            i64 bo = 0;
+            for (int k = 0; k < nsupers; ++k)
+                if (want[forest_of[k]]) add_zranges(k, &bo);
+            DevBuf<ZRange> dr;
+            dr.upload(zr);
+            DevBuf<T> buf;
+            buf.alloc(std::max<i64>(bo, 1));
+            const int nr = (int)zr.size();
+            zr.swap(keep);
+            if (!recv && nr)
+                hipLaunchKernelGGL(k_zranges<T>, dim3(nr), dim3(256), 0, st, dr.p, d_L.p, d_U.p, buf.p,
+                                   (int)ZR_PACK);
+            X.s = st;
+            X.section(G_Z, sender, 1u << (recv ? zl : peer), buf.p, (size_t)bo * sizeof(T));
+            X.flush();
+            if (recv && nr)
+                hipLaunchKernelGGL(k_zranges<T>, dim3(nr), dim3(256), 0, st, dr.p, d_L.p, d_U.p, buf.p,
+                                   (int)ZR_COPY);
+            HIPCHK(hipStreamSynchronize(st));
+            if (!recv) break;
+        }
+        host_current = false;
     }
 
     // ------------------------------------------------------- value layout
@@ -1797,8 +2179,11 @@ struct Plan : PlanBase {
                                      d_cg.bytes() + d_cb.bytes() + d_pair.bytes() + d_prec.bytes() +
                                      d_ct0.bytes() + d_cvoff.bytes() + d_dcopy.bytes() +
                                      d_pcopy.bytes());
-        stats.comm_bytes = (double)comm_volume * sizeof(T);
-        stats.comm_buf_bytes = (double)(dpk_total + pan_total) * sizeof(T);
+        double zvol = 0; // 3D: the ancestor reductions this layer takes part in
+        if (zmode)
+            for (int p = 0; p <= std::min(my_last, maxlvl - 2); ++p) zvol += (double)zr_cnt[p] * sizeof(T);
+        stats.comm_bytes = (double)comm_volume * sizeof(T) + zvol;
+        stats.comm_buf_bytes = (double)(dpk_total + pan_total) * sizeof(T) + (double)d_zbuf.bytes();
         // the tables went up by pageable hipMemcpy on the null stream; the
         // plan's streams are non-blocking, so make sure every copy has landed
         HIPCHK(hipDeviceSynchronize());
@@ -2214,6 +2599,10 @@ struct Plan : PlanBase {
             fn();
             if (timing) spans.push_back({a, mark_on(st), kind, cur_level});
         };
+        if (zmode) { // ancestor forests another layer factors start from zero
+            launch_zranges(zr_off[0], zr_off[1], ZR_ZERO, stream);
+            zbytes = 0;
+        }
         int e_start = timing ? mark() : -1;
         vector<int> lvl_end;
         HIPCHK(hipEventRecord(ev_start, stream));
@@ -2227,9 +2616,18 @@ struct Plan : PlanBase {
         // Critical tiles update exactly the destinations in the panels of
         // level L+1, so panel(L+1) (diag LU, TRSM, exchanges) runs beside the
         // bulk of level L's Schur update (SRC/pdgstrf.c:1115-1356 look-ahead).
-        for (size_t L = 0; L < levels.size(); ++L) {
+        // 3D grids: my phases one after the other, each followed by its
+        // ancestor reduction (SRC/pdgstrf3d.c:300-345)
+        const int nph = zmode ? my_last + 1 : 1;
+        int last_L = -1;
+        vector<std::array<int, 3>> zmarks; // (phase start, phase end, reduction end) events
+        int zstart = e_start;
+        for (int ph = 0; ph < nph; ++ph) {
+        const size_t L0 = zmode ? phase_lv[ph] : 0, L1 = zmode ? phase_lv[ph + 1] : levels.size();
+        for (size_t L = L0; L < L1; ++L) {
             const LevelRange &R = levels[L];
             cur_level = (int)L;
+            last_L = (int)L;
             hipStream_t P = opts.serial ? stream : pstream;
             if (R.diag_n)
                 span(0, P, [&] {
@@ -2315,6 +2713,22 @@ struct Plan : PlanBase {
             HIPCHK(hipEventRecord(ev_rest[L], stream));
             if (opts.timing >= 2) lvl_end.push_back(mark_on(stream)); // level wall time
         }
+        if (zmode) {
+            hipStream_t P = opts.serial ? stream : pstream;
+            if (last_L >= 0) HIPCHK(hipStreamWaitEvent(P, ev_rest[last_L], 0));
+            const int e_ph = timing ? mark_on(P) : -1;
+            if (ph < maxlvl - 1) {
+                span(4, P, [&] { zreduce(ph, P); });
+                HIPCHK(hipEventRecord(ev_pend, P));
+                HIPCHK(hipStreamWaitEvent(stream, ev_pend, 0));
+            }
+            if (timing) {
+                const int e_red = mark_on(P);
+                zmarks.push_back({zstart, e_ph, e_red});
+                zstart = e_red;
+            }
+        }
+        }
         HIPCHK(hipEventRecord(ev_pend, pstream));
         HIPCHK(hipStreamWaitEvent(stream, ev_pend, 0));
         HIPCHK(hipGetLastError());
@@ -2366,11 +2780,16 @@ struct Plan : PlanBase {
         int my_info = 0;
         for (int k = 0; k < nsupers; ++k)
             if (zp[k]) my_info = zp[k];
-        if (xmode) {
+        if (xmode || zmode) { // MIN over the grid (3D: all layers, SRC/pdgstrf3d.c:351-355)
             vector<i64> mine(1, my_info ? my_info : n + 1);
-            auto all = X.allgatherv(G_WORLD, mine);
             i64 g = n + 1;
-            for (auto &v : all) g = std::min(g, v[0]);
+            if (xmode)
+                for (auto &v : X.allgatherv(G_WORLD, mine)) g = std::min(g, v[0]);
+            if (zmode) {
+                mine[0] = g;
+                X.s = stream;
+                for (auto &v : X.allgatherv(G_Z, mine)) g = std::min(g, v[0]);
+            }
             my_info = g == n + 1 ? 0 : (int)g;
         }
         *info = my_info;
@@ -2393,6 +2812,14 @@ struct Plan : PlanBase {
                 }
             }
             for (auto &R : levels) stats.schur_big_flops += R.big_flops;
+            for (int i = 0; i < 8; ++i) stats.t_phase_ms[i] = 0;
+            stats.t_zreduce_ms = 0;
+            for (size_t i = 0; i < zmarks.size() && i < 8; ++i) {
+                HIPCHK(hipEventElapsedTime(&ms, ev[zmarks[i][0]], ev[zmarks[i][1]]));
+                stats.t_phase_ms[i] = ms;
+                HIPCHK(hipEventElapsedTime(&ms, ev[zmarks[i][1]], ev[zmarks[i][2]]));
+                stats.t_zreduce_ms += ms;
+            }
             if (opts.timing >= 2) { // per-level breakdown (stderr)
                 vector<std::array<double, 5>> t(levels.size(), {0, 0, 0, 0, 0});
                 for (auto &s : spans) {
@@ -2736,6 +3163,7 @@ struct Plan : PlanBase {
     // right-hand sides in batches of SvNr<T>: every factor element is read once
     // per batch and sweep
     void solve(void *b, int64_t ldb, int nrhs) override {
+        SLU_REQUIRE(!zmode, "solve: 3D plans hold the factors spread over the layers (gather them to a 2D plan)");
         SLU_REQUIRE(vstate == 2, "solve: the device storage holds no factors (factor first)");
         if (!sv_ready) build_solve();
         if (xmode) {
@@ -2867,6 +3295,7 @@ struct Plan : PlanBase {
     }
 
     void refine(const void *b, void *x, int64_t ld, int nrhs, double *berr, int *steps) override {
+        SLU_REQUIRE(!zmode, "refine: not on 3D plans");
         SLU_REQUIRE(vstate == 2, "refine: the device storage holds no factors (factor first)");
         SLU_REQUIRE(a_fact != nullptr,
                     "refine needs the values of A the factors came from (slu_plan_fill_a "
@@ -3480,7 +3909,7 @@ template <typename P> PlanBase *make_plan_any(void *LU, int n, int pr, int pc, i
                         typename P::lus_type>;
     const char *e = getenv("SLU_AMALG");
     const bool on = !(e && !strcmp(e, "0"));
-    if (on && pr * pc == 1 && !(o && o->schedule_only)) {
+    if (on && pr * pc == 1 && !(o && o->schedule_only) && !(c && c->npdep > 1)) {
         const char *z = getenv("SLU_AMALG_ZERO");
         if (PlanBase *p = A::make((typename P::lus_type *)LU, n, o, z ? atof(z) : 0.10, FAST_MAXW))
             return p;
@@ -3570,6 +3999,55 @@ slu_comm *slu_comm_create(const void *uid, int nprow, int npcol, int iam, int de
     }
 }
 
+slu_comm *slu_comm_create3d(const void *uid, int nprow, int npcol, int npdep, int iam3d, int device) {
+    try {
+        const int P = nprow * npcol;
+        SLU_REQUIRE(nprow > 0 && npcol > 0 && npdep > 0 && (npdep & (npdep - 1)) == 0,
+                    "3D grid %dx%dx%d: Pz must be a power of two", nprow, npcol, npdep);
+        SLU_REQUIRE(iam3d >= 0 && iam3d < P * npdep, "rank %d outside a %dx%dx%d grid", iam3d, nprow,
+                    npcol, npdep);
+        auto *c = new slu_comm;
+        c->nprow = nprow;
+        c->npcol = npcol;
+        c->npdep = npdep;
+        c->zlayer = iam3d / P;
+        c->iam = iam3d % P;
+        c->myrow = c->iam / npcol;
+        c->mycol = c->iam % npcol;
+        c->device = device;
+        HIPCHK(hipSetDevice(device));
+        if (P * npdep > 1) {
+            SLU_REQUIRE(uid != nullptr, "uid required for a %dx%dx%d grid", nprow, npcol, npdep);
+            ncclUniqueId id;
+            memcpy(&id, uid, sizeof id);
+            NCCLCHK(ncclCommInitRank(&c->all, P * npdep, id, iam3d));
+            NCCLCHK(ncclCommSplit(c->all, c->zlayer, c->iam, &c->world, nullptr));
+            NCCLCHK(ncclCommSplit(c->all, c->iam, c->zlayer, &c->zcomm, nullptr));
+            NCCLCHK(ncclCommSplit(c->world, c->myrow, c->mycol, &c->row, nullptr));
+            NCCLCHK(ncclCommSplit(c->world, c->mycol, c->myrow, &c->col, nullptr));
+        }
+        return c;
+    } catch (const std::exception &e) {
+        set_last_error(e.what());
+        return nullptr;
+    }
+}
+
+slu_comm *slu_comm_create_host_p2p3d(slu_host_p2p_fn fn, void *ctx, int nprow, int npcol, int npdep,
+                                     int iam3d, int device) {
+    try {
+        SLU_REQUIRE(npdep > 0 && (npdep & (npdep - 1)) == 0, "Pz = %d is not a power of two", npdep);
+        slu_comm *c = slu_comm_create_host_p2p(fn, ctx, nprow, npcol, iam3d % (nprow * npcol), device);
+        if (!c) return nullptr;
+        c->npdep = npdep;
+        c->zlayer = iam3d / (nprow * npcol);
+        return c;
+    } catch (const std::exception &e) {
+        set_last_error(e.what());
+        return nullptr;
+    }
+}
+
 slu_comm *slu_comm_create_host(slu_host_bcast_fn fn, void *ctx, int nprow, int npcol, int iam,
                                int device) {
     try {
@@ -3614,13 +4092,14 @@ slu_comm *slu_comm_create_host_p2p(slu_host_p2p_fn fn, void *ctx, int nprow, int
 
 int slu_comm_size(const slu_comm *c, int group) {
     if (!c) return -1;
-    if (c->world) { // what RCCL itself reports for the communicator
+    if (c->world || c->zcomm) { // what RCCL itself reports for the communicator
         int n = -1;
-        ncclComm_t cm = group == 0 ? c->world : group == 1 ? c->row : c->col;
+        ncclComm_t cm = group == 0 ? c->world : group == 1 ? c->row : group == 2 ? c->col : c->zcomm;
+        if (!cm) return 1;
         if (ncclCommCount(cm, &n) != ncclSuccess) return -1;
         return n;
     }
-    return group == 0 ? c->nprow * c->npcol : group == 1 ? c->npcol : c->nprow;
+    return group == 0 ? c->nprow * c->npcol : group == 1 ? c->npcol : group == 2 ? c->nprow : c->npdep;
 }
 
 void slu_comm_destroy(slu_comm *c) {
@@ -3628,6 +4107,8 @@ void slu_comm_destroy(slu_comm *c) {
     if (c->row) ncclCommDestroy(c->row);
     if (c->col) ncclCommDestroy(c->col);
     if (c->world) ncclCommDestroy(c->world);
+    if (c->zcomm) ncclCommDestroy(c->zcomm);
+    if (c->all) ncclCommDestroy(c->all);
     delete c;
 }
 
@@ -3654,6 +4135,16 @@ slu_plan *slu_plan_create(int dtype, void *LU, int n, int nprow, int npcol, int 
         set_last_error(e.what());
         if (err && errlen > 0) snprintf(err, errlen, "%s", e.what());
         return nullptr;
+    }
+}
+
+int slu_plan_gather3d(slu_plan *p) {
+    try {
+        p->impl->gather_layers();
+        return 0;
+    } catch (const std::exception &e) {
+        set_last_error(e.what());
+        return -1;
     }
 }
 

@@ -56,7 +56,7 @@ class Comm:
         return self
 
     @classmethod
-    def host_p2p(cls, nprow, npcol, iam, device, p2p):
+    def host_p2p(cls, nprow, npcol, iam, device, p2p, _npdep=1, _iam3d=None):
         """Point-to-point test transport: ``p2p(ops)`` receives the list of
         (group, peer, is_send, uint8 numpy buffer) of one exchange phase --
         exactly the ncclSend / ncclRecv pairs the RCCL transport issues, in
@@ -79,14 +79,44 @@ class Comm:
                 return 1
 
         self._cb = HOST_P2P_FN(_cb)
-        self.ptr = lib().slu_comm_create_host_p2p(self._cb, None, nprow, npcol, iam, device)
+        if _npdep > 1:
+            self.ptr = lib().slu_comm_create_host_p2p3d(self._cb, None, nprow, npcol, _npdep,
+                                                        _iam3d, device)
+        else:
+            self.ptr = lib().slu_comm_create_host_p2p(self._cb, None, nprow, npcol, iam, device)
         if not self.ptr:
             raise RuntimeError(lib().slu_last_error().decode())
         return self
 
+    @classmethod
+    def grid3d(cls, nprow, npcol, npdep, iam3d, device=0, uid=None):
+        """RCCL communicators of a 3D grid (npdep layers of nprow x npcol;
+        iam3d = layer * nprow * npcol + row * npcol + column)."""
+        self = cls.__new__(cls)
+        self.nprow, self.npcol, self.npdep = nprow, npcol, npdep
+        self.iam = iam3d % (nprow * npcol)
+        buf = None
+        if nprow * npcol * npdep > 1:
+            if uid is None:
+                raise ValueError("multi-rank grids need the RCCL unique id")
+            buf = C.create_string_buffer(bytes(uid), 128)
+        self.ptr = lib().slu_comm_create3d(buf, nprow, npcol, npdep, iam3d, device)
+        if not self.ptr:
+            raise RuntimeError(lib().slu_last_error().decode())
+        return self
+
+    @classmethod
+    def host_p2p3d(cls, nprow, npcol, npdep, iam3d, device, p2p):
+        """host_p2p for a 3D grid: group 3 = the ranks at my (row, column)
+        of every layer, peer = layer."""
+        self = cls.host_p2p(nprow, npcol, iam3d % (nprow * npcol), device, p2p, _npdep=npdep,
+                            _iam3d=iam3d)
+        self.npdep = npdep
+        return self
+
     def size(self, group=0):
-        """Ranks in the grid (0), my process row (1) or column (2); for RCCL
-        what ncclCommCount reports."""
+        """Ranks in the grid (0), my process row (1) or column (2), the
+        layers of a 3D grid (3); for RCCL what ncclCommCount reports."""
         return lib().slu_comm_size(self.ptr, group)
 
     @staticmethod
@@ -209,6 +239,11 @@ class Plan:
         ns, nb = C.c_int64(), C.c_int64()
         self._chk(lib().slu_plan_check_exchange(self.ptr, C.byref(ns), C.byref(nb)))
         return ns.value, nb.value
+
+    def gather3d(self):
+        """3D plans (collective over the layers): bring the factored forests
+        to layer 0, whose ranks then hold the final factors (download())."""
+        self._chk(lib().slu_plan_gather3d(self.ptr))
 
     def stats(self):
         st = PlanStats()

@@ -81,10 +81,14 @@ class PlanStats(C.Structure):
                 ("n_d2h_copies", C.c_int64), ("comm_buf_bytes", C.c_double),
                 ("nsupers_in", C.c_int64), ("amalg_groups", C.c_int64),
                 ("amalg_zeros", C.c_double), ("t_amalg_ms", C.c_double),
-                ("t_expand_ms", C.c_double), ("t_compress_ms", C.c_double)]
+                ("t_expand_ms", C.c_double), ("t_compress_ms", C.c_double),
+                ("t_phase_ms", C.c_double * 8), ("t_zreduce_ms", C.c_double),
+                ("npdep", C.c_int64), ("zlayer", C.c_int64), ("phase_last", C.c_int64)]
 
     def as_dict(self):
-        return {k: getattr(self, k) for k, _ in self._fields_}
+        d = {k: getattr(self, k) for k, _ in self._fields_}
+        d["t_phase_ms"] = list(d["t_phase_ms"])
+        return d
 
 
 _lib = None
@@ -141,6 +145,9 @@ def lib():
         "slu_comm_create": (P, [P, C.c_int, C.c_int, C.c_int, C.c_int]),
         "slu_comm_create_host": (P, [HOST_BCAST_FN, P, C.c_int, C.c_int, C.c_int, C.c_int]),
         "slu_comm_create_host_p2p": (P, [HOST_P2P_FN, P, C.c_int, C.c_int, C.c_int, C.c_int]),
+        "slu_comm_create3d": (P, [P, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]),
+        "slu_comm_create_host_p2p3d": (P, [HOST_P2P_FN, P, C.c_int, C.c_int, C.c_int, C.c_int,
+                                           C.c_int]),
         "slu_comm_size": (C.c_int, [P, C.c_int]),
         "slu_comm_destroy": (None, [P]),
         "slu_plan_create": (P, [C.c_int, P, C.c_int, C.c_int, C.c_int, C.c_int, P,
@@ -157,6 +164,7 @@ def lib():
         "slu_plan_sync": (C.c_int, [P]),
         "slu_plan_set_timing": (C.c_int, [P, C.c_int, C.c_int]),
         "slu_plan_check_exchange": (C.c_int, [P, c_i64p, c_i64p]),
+        "slu_plan_gather3d": (C.c_int, [P]),
         "slu_plan_destroy": (None, [P]),
         "slu_plan_get_stats": (C.c_int, [P, C.POINTER(PlanStats)]),
         "slu_last_error": (C.c_char_p, []),

@@ -24,23 +24,32 @@ def free_port():
 
 
 class GlooGrid:
-    """torch.distributed gloo groups of a Pr x Pc grid (world / rows / columns)."""
+    """torch.distributed gloo groups of a Pr x Pc grid (world / rows /
+    columns), or of pz such layers (3D: global rank = layer * Pr * Pc + rank in
+    the layer; group 3 = my (row, column) position in every layer)."""
 
-    def __init__(self, rank, pr, pc):
+    def __init__(self, rank, pr, pc, pz=1):
         import torch.distributed as dist
         self.dist = dist
-        self.rank, self.pr, self.pc = rank, pr, pc
-        self.myrow, self.mycol = rank // pc, rank % pc
-        rows = [dist.new_group([r * pc + c for c in range(pc)]) for r in range(pr)]
-        cols = [dist.new_group([r * pc + c for r in range(pr)]) for c in range(pc)]
-        self.row, self.col = rows[self.myrow], cols[self.mycol]
+        P = pr * pc
+        self.rank, self.pr, self.pc, self.pz = rank, pr, pc, pz
+        self.layer, r2 = rank // P, rank % P
+        self.base = self.layer * P
+        self.myrow, self.mycol = r2 // pc, r2 % pc
+        self.row = self.col = None
+        if pz == 1:  # (the 3D runs use the point-to-point transport only)
+            rows = [dist.new_group([r * pc + c for c in range(pc)]) for r in range(pr)]
+            cols = [dist.new_group([r * pc + c for r in range(pr)]) for c in range(pc)]
+            self.row, self.col = rows[self.myrow], cols[self.mycol]
 
     def global_root(self, group, root):
         if group == 0:
-            return root
+            return self.base + root
         if group == 1:
-            return self.myrow * self.pc + root
-        return root * self.pc + self.mycol
+            return self.base + self.myrow * self.pc + root
+        if group == 2:
+            return self.base + root * self.pc + self.mycol
+        return root * self.pr * self.pc + self.myrow * self.pc + self.mycol
 
     def bcast(self, group, root, arr):
         import torch
@@ -65,7 +74,7 @@ class GlooGrid:
 
 
 def _worker(rank, world, port, recipe, out_dir, device, fill=False, solve=False,
-            transport="bcast"):
+            transport="bcast", pz=1):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     try:
         import torch.distributed as dist
@@ -77,17 +86,35 @@ def _worker(rank, world, port, recipe, out_dir, device, fill=False, solve=False,
             from refdump import Fixture
             fx = Fixture(recipe.split(":", 1)[1])
             pr, pc, tiny, anorm = fx.pr, fx.pc, fx.replace_tiny, fx.anorm
-            gg = GlooGrid(rank, pr, pc)
-            lu = fx.lu(rank)
+            gg = GlooGrid(rank, pr, pc, pz)
+            lu = fx.lu(rank % (pr * pc))
             A = S = None
         else:
             A, perm, dtype, (pr, pc), relax, maxsup, tiny = recipe()
             anorm = cases.anorm(A)
-            gg = GlooGrid(rank, pr, pc)
+            gg = GlooGrid(rank, pr, pc, pz)
             S = Symbolic(A, perm, relax, maxsup)
-            lu = S.distribute(pr, pc, rank // pc, rank % pc)
+            lu = S.distribute(pr, pc, gg.myrow, gg.mycol)
         res = {}
-        if transport == "schedule":  # no GPU: the exchange schedule over the p2p transport
+        if pz > 1:  # 3D grid: every layer holds the LUstruct; p2p transport
+            comm = Comm.host_p2p3d(pr, pc, pz, rank, -1 if device is None else device, gg.p2p)
+            assert comm.size(3) == pz and comm.size(0) == pr * pc
+            if transport == "schedule":
+                p = Plan(lu, comm=comm, schedule_only=True)
+                res["nsec"], res["nbytes"] = p.check_exchange()
+                res["nlevels"] = p.stats()["nlevels"]
+                res["nsupers"] = p.stats()["nsupers"]
+            else:
+                p = Plan(lu, comm=comm, replace_tiny=tiny)
+                p.upload()
+                info, ntiny = p.factor(anorm)
+                st = p.stats()
+                res.update(info=info, tiny=ntiny, flops=st["schur_flops"] + st["panel_flops"],
+                           comm_bytes=st["comm_bytes"], nsupers=st["nsupers"])
+                p.gather3d()
+                p.download()
+            del p
+        elif transport == "schedule":  # no GPU: the exchange schedule over the p2p transport
             comm = Comm.host_p2p(pr, pc, rank, -1, gg.p2p)
             p = Plan(lu, comm=comm, schedule_only=True)
             res["nsec"], res["nbytes"] = p.check_exchange()
@@ -146,7 +173,7 @@ def _worker(rank, world, port, recipe, out_dir, device, fill=False, solve=False,
 
 
 def run_grid(recipe, pr, pc, out_dir, device=0, timeout=240, fill=False, solve=False,
-             transport="bcast"):
+             transport="bcast", pz=1):
     """Run ``recipe`` (picklable callable returning cases.build()-style
     tuples, or "refdump:<case>" for the per-rank LUstructs of a reference
     dump fixture) on a pr x pc grid; returns the per-rank result dicts.
@@ -159,10 +186,10 @@ def run_grid(recipe, pr, pc, out_dir, device=0, timeout=240, fill=False, solve=F
     with two HIP runtimes.  Each worker imports torch.distributed first."""
     import multiprocessing as mp
     ctx = mp.get_context("spawn")
-    world = pr * pc
+    world = pr * pc * pz
     port = free_port()
     procs = [ctx.Process(target=_worker, args=(r, world, port, recipe, str(out_dir), device, fill,
-                                                solve, transport))
+                                                solve, transport, pz))
              for r in range(world)]
     for p in procs:
         p.start()
