@@ -81,7 +81,8 @@ def grid_shape(n):
     return {1: (1, 1), 2: (1, 2), 4: (2, 2), 8: (2, 4), 16: (4, 4)}.get(n, (1, n))
 
 
-def build_lu(workload, nx, pr, pc, myrow, mycol, ordering="grid", symbolic="reference"):
+def build_lu(workload, nx, pr, pc, myrow, mycol, ordering="grid", symbolic="reference",
+             coarse=None):
     from superlu_dist_amd.frontend import STENCIL_2D5, STENCIL_3D7, STENCIL_3D27, Csc, Symbolic, nd_order
     kind, dims, dtype, diag, diag_im = WORKLOADS[workload][:5]
     kind = {"2d5": STENCIL_2D5, "3d7": STENCIL_3D7, "3d27": STENCIL_3D27}[kind]
@@ -103,7 +104,8 @@ def build_lu(workload, nx, pr, pc, myrow, mycol, ordering="grid", symbolic="refe
         # csrc/amalg.h).  Grids: the grid plan has no device relayout, so the
         # same coarse partition is laid out by pddistribute's rules instead
         # (SLU_SYMB_COARSE); the rate counts the reference partition's work.
-        S = Symbolic(A, perm, 60, 256, reference=True, coarse=pr * pc > 1)
+        S = Symbolic(A, perm, 60, 256, reference=True,
+                     coarse=pr * pc > 1 if coarse is None else coarse)
     else:
         # the library front-end's amalgamated partition (chains with <= 10 %
         # explicit zeros; graph ordering: chains through multi-child columns,
@@ -306,6 +308,10 @@ def main():
                     help="per-level phase breakdown of the last step on stderr")
     ap.add_argument("--roofline-only", action="store_true",
                     help="only the serialized (single-stream) profiling step: for rocprofv3 runs")
+    ap.add_argument("--grid3d", default=None, metavar="PRxPCxPZ",
+                    help="3D process grid (pdgstrf3d): PZ layers of a PR x PC grid, PR*PC*PZ = "
+                         "--gpus; the layers factor the etree's forests and reduce the "
+                         "ancestors between them (default: the 2D grid of --gpus ranks)")
     ap.add_argument("--host-transport", action="store_true",
                     help="REHEARSAL ONLY: several ranks on one GPU through the host-staged "
                          "point-to-point test transport (the RCCL send / receive pairs over "
@@ -327,8 +333,16 @@ def main():
     if world != args.gpus:
         log(f"WORLD_SIZE={world} but --gpus {args.gpus}: refusing to measure a different grid")
         sys.exit(2)
-    pr, pc = grid_shape(world)
-    myrow, mycol = rank // pc, rank % pc
+    pz = 1
+    if args.grid3d:
+        pr, pc, pz = (int(x) for x in args.grid3d.lower().split("x"))
+        if pr * pc * pz != world or pz & (pz - 1):
+            log(f"--grid3d {args.grid3d} does not make {world} ranks with a power-of-two depth")
+            sys.exit(2)
+    else:
+        pr, pc = grid_shape(world)
+    layer, r2 = rank // (pr * pc), rank % (pr * pc)
+    myrow, mycol = r2 // pc, r2 % pc
 
     from superlu_dist_amd.engine import Comm, Plan
     dist = None
@@ -345,7 +359,7 @@ def main():
             sys.path.insert(0, os.path.join(ROOT, "tests"))
             from gridrun import GlooGrid
             with _StdoutToStderr():
-                grid = GlooGrid(rank, pr, pc)
+                grid = GlooGrid(rank, pr, pc, pz)
             local = 0
         else:
             ndev = torch.cuda.device_count()
@@ -364,25 +378,29 @@ def main():
             dist.barrier()
 
     t0 = time.time()
-    log(f"front-end {args.workload} nx={args.nx} grid {pr}x{pc}")
+    gname = f"{pr}x{pc}" + (f"x{pz}" if pz > 1 else "")
+    log(f"front-end {args.workload} nx={args.nx} grid {gname}")
     A, S, lu, perm = build_lu(args.workload, args.nx, pr, pc, myrow, mycol, args.ordering,
-                              args.symbolic)
+                              args.symbolic, coarse=world > 1)
     t_front = time.time() - t0
     log(f"front-end {t_front:.1f} s, {S.nsupers} supernodes")
     if world == 1:
         comm = None
     elif grid is not None:
         # the RCCL transport's send / receive pairs, host-staged over gloo
-        comm = Comm.host_p2p(pr, pc, rank, 0, grid.p2p)
+        comm = (Comm.host_p2p3d(pr, pc, pz, rank, 0, grid.p2p) if pz > 1 else
+                Comm.host_p2p(pr, pc, rank, 0, grid.p2p))
     else:
-        comm = Comm(pr, pc, rank, device=local, uid=uid)
+        comm = (Comm.grid3d(pr, pc, pz, rank, device=local, uid=uid) if pz > 1 else
+                Comm(pr, pc, rank, device=local, uid=uid))
     if comm is not None:
-        sizes = (comm.size(0), comm.size(1), comm.size(2))
-        if sizes != (world, pc, pr):
-            log(f"the communicators see {sizes} ranks (grid, row, column), expected "
-                f"{(world, pc, pr)}")
+        sizes = (comm.size(0), comm.size(1), comm.size(2), comm.size(3) if pz > 1 else 1)
+        if sizes != (pr * pc, pc, pr, pz):
+            log(f"the communicators see {sizes} ranks (layer, row, column, layers), expected "
+                f"{(pr * pc, pc, pr, pz)}")
             sys.exit(3)
-        log(f"communicators: grid {sizes[0]}, row {sizes[1]}, column {sizes[2]} ranks")
+        log(f"communicators: layer {sizes[0]}, row {sizes[1]}, column {sizes[2]}, "
+            f"{sizes[3]} layers")
     t0 = time.time()
     plan = Plan(lu, comm=comm, timing=2 if args.level_log else 1)
     t_plan = time.time() - t0
@@ -458,6 +476,17 @@ def main():
         ff = torch.tensor([my_flops], dtype=torch.float64)
         dist.all_reduce(ff, op=dist.ReduceOp.SUM)
         flops_all = float(ff.item())
+    layers3d = None
+    if pz > 1:
+        # per-layer phase times of the last timed step (rank 0 of each layer)
+        import torch.distributed as tdist
+        mine = {"layer": layer, "factored": int(st["nsupers"]), "phase_last": int(st["phase_last"]),
+                "phase_ms": [round(x, 3) for x in st["t_phase_ms"][:int(st["phase_last"]) + 1]],
+                "zreduce_ms": round(st["t_zreduce_ms"], 3),
+                "flops": my_flops, "comm_gb": round(st["comm_bytes"] / 1e9, 3)}
+        allm = [None] * world
+        tdist.all_gather_object(allm, mine)
+        layers3d = [m for i, m in enumerate(allm) if i % (pr * pc) == 0]
     if ref_work is not None:
         # the reference partition's algorithmic work (what pdgstrf does on the
         # LUstruct pdgssvx builds; the coarse partition adds explicit zeros)
@@ -514,14 +543,18 @@ def main():
                                    f"(n={A.n}), {'graph nested dissection (METIS_NodeND)' if args.ordering == 'graph' else 'nested dissection'}, relax 60, maxsup 256, {W[6]}",
                        "symbolic": ("reference sp_colorder + symbfact + pddistribute (ColPerm = MY_PERMC)"
                                     if args.symbolic == "reference" else "library front-end (amalgamated)"),
-                       "grid": f"{pr}x{pc}",
+                       "grid": gname,
                        "nsupers": ref_work["nsupers"] if ref_work else int(S.nsupers),
                        "nsupers_factored": int(st0["nsupers"]),
                        "flops_per_factorization": flops_all,
-                       "nnz_L": S.nnzL, "parallelism": f"2D block-cyclic {pr}x{pc}",
+                       "nnz_L": S.nnzL,
+                       "parallelism": (f"3D: {pz} layers (etree forests, ancestor reductions "
+                                       f"between layers) of 2D block-cyclic {pr}x{pc}" if pz > 1
+                                       else f"2D block-cyclic {pr}x{pc}"),
                        "transport": ("host-staged gloo point-to-point (REHEARSAL, not a measurement)"
                                      if grid is not None else
-                                     (f"rccl ({world} ranks, row/column communicators)"
+                                     (f"rccl ({world} ranks, row/column"
+                                      f"{'/layer' if pz > 1 else ''} communicators)"
                                       if world > 1 else "none")),
                        "hbm_gb_rank0": round((st0["lu_bytes"] + st0["index_bytes"] +
                                               st0["comm_buf_bytes"]) / 1e9, 2),
@@ -533,6 +566,7 @@ def main():
             "next_rows": nxt,
             "abi_pdgstrf": abi,
             "phases_ms_per_step_rank0": {k[2:-3]: round(v / K, 3) for k, v in acc.items()},
+            "layers3d": layers3d,
             "setup_s": {"frontend": round(t_front, 2), "plan": round(t_plan, 2),
                         "h2d_upload_pcie": round(t_upload, 2)},
             "info": info,

@@ -298,6 +298,7 @@ typedef struct {
      * reductions, last slu_plan_factor */
     double t_phase_ms[8];
     double t_zreduce_ms;
+    double zred_bytes[8];      /* 3D: bytes of the reduction after each phase */
     int64_t npdep, zlayer, phase_last; /* 3D: layers, mine, my last phase */
 } slu_plan_stats;
 int slu_plan_get_stats(const slu_plan *p, slu_plan_stats *st);

@@ -481,6 +481,10 @@ struct Plan : PlanBase {
     DevBuf<T> d_zbuf;
     vector<i64> uval_len;
     double zbytes = 0; // reduction bytes sent + received per factorization
+    // SLU_3D_SOLO=1 (measurement hook, tools/model3d.py): one layer alone on
+    // a GPU -- the reductions pack / add but exchange nothing, so each
+    // layer's phase times can be taken without the others running beside it
+    bool zsolo = getenv("SLU_3D_SOLO") && atoi(getenv("SLU_3D_SOLO")) == 1;
     vector<DiagItem<T>> diag_items;
     vector<TrsmLItem<T>> tl_items;
     vector<TrsmUItem<T>> tu_items;
@@ -1343,6 +1347,7 @@ struct Plan : PlanBase {
                 }
             zr_off.push_back((int)zr.size());
             zr_cnt.push_back(bo);
+            if (p < 8) stats.zred_bytes[p] = (double)bo * sizeof(T);
             mx = std::max(mx, bo);
         }
         if (!device) return;
@@ -1365,8 +1370,10 @@ struct Plan : PlanBase {
         const i64 cnt = zr_cnt[p];
         if (!recv) launch_zranges(a, b, ZR_PACK, st);
         X.s = st;
-        X.section(G_Z, recv ? peer : zl, 1u << (recv ? zl : peer), d_zbuf.p, (size_t)cnt * sizeof(T));
-        X.flush();
+        if (!zsolo) {
+            X.section(G_Z, recv ? peer : zl, 1u << (recv ? zl : peer), d_zbuf.p, (size_t)cnt * sizeof(T));
+            X.flush();
+        }
         zbytes += (double)cnt * sizeof(T);
         if (recv) launch_zranges(a, b, ZR_ADD, st);
     }
@@ -2785,7 +2792,7 @@ struct Plan : PlanBase {
             i64 g = n + 1;
             if (xmode)
                 for (auto &v : X.allgatherv(G_WORLD, mine)) g = std::min(g, v[0]);
-            if (zmode) {
+            if (zmode && !zsolo) {
                 mine[0] = g;
                 X.s = stream;
                 for (auto &v : X.allgatherv(G_Z, mine)) g = std::min(g, v[0]);

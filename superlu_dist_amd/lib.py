@@ -83,11 +83,13 @@ class PlanStats(C.Structure):
                 ("amalg_zeros", C.c_double), ("t_amalg_ms", C.c_double),
                 ("t_expand_ms", C.c_double), ("t_compress_ms", C.c_double),
                 ("t_phase_ms", C.c_double * 8), ("t_zreduce_ms", C.c_double),
+                ("zred_bytes", C.c_double * 8),
                 ("npdep", C.c_int64), ("zlayer", C.c_int64), ("phase_last", C.c_int64)]
 
     def as_dict(self):
         d = {k: getattr(self, k) for k, _ in self._fields_}
         d["t_phase_ms"] = list(d["t_phase_ms"])
+        d["zred_bytes"] = list(d["zred_bytes"])
         return d
 
 
