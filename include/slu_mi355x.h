@@ -178,7 +178,10 @@ typedef struct {
                                index exchange, levels and exchange sections,
                                for slu_plan_check_exchange; a grid needs the
                                point-to-point host transport */
-    int reserved[2];
+    const int64_t *forest_map; /* 3D grids: per supernode its forest in heap
+                               order (0 = top ancestors), e.g. the reference's
+                               dtrf3Dpartition_t.supernode2treeMap; NULL: the
+                               engine's own partition (SRC/supernodalForest.c) */
 } slu_engine_opts;
 
 /* A plan = device-resident factors + every index table the kernels use.

@@ -42,6 +42,9 @@ struct Mpi {
                          void *) = nullptr;
     int (*set_attr)(MPI_Comm, int, void *) = nullptr;
     int (*get_attr)(MPI_Comm, int, void *, int *) = nullptr;
+    int (*isend)(const void *, int, MPI_Datatype, int, int, MPI_Comm, MPI_Request *) = nullptr;
+    int (*irecv)(void *, int, MPI_Datatype, int, int, MPI_Comm, MPI_Request *) = nullptr;
+    int (*waitall)(int, MPI_Request *, MPI_Status *) = nullptr;
 };
 
 template <typename F> void mpi_sym(F &f, const char *name) {
@@ -58,6 +61,9 @@ const Mpi &mpi() {
         mpi_sym(x.create_keyval, "MPI_Comm_create_keyval");
         mpi_sym(x.set_attr, "MPI_Comm_set_attr");
         mpi_sym(x.get_attr, "MPI_Comm_get_attr");
+        mpi_sym(x.isend, "MPI_Isend");
+        mpi_sym(x.irecv, "MPI_Irecv");
+        mpi_sym(x.waitall, "MPI_Waitall");
         return x;
     }();
     return m;
@@ -329,6 +335,157 @@ int_t pxgstrf(int dtype, const char *name, superlu_dist_options_t *options, int 
     }
 }
 
+// ------------------------------------------------------------------ 3D
+// pdgstrf3d (SRC/pdgstrf3d.c:121-392): the engine's 3D plan on
+// each rank's LUstruct of its layer, with the caller's forest partition
+// (trf3Dpartition->supernode2treeMap, built by dinitTrf3Dpartition, which
+// also zeroed the ancestor blocks this layer does not own).  Communicators
+// cached on grid3d->comm: RCCL when every rank drives its own GPU, else the
+// point-to-point host transport over MPI_Isend / MPI_Irecv on the layer's
+// grid2d.comm / rscp / cscp and on zscp (the same send / receive pairs the
+// RCCL transport issues, host-staged).
+struct Grid3Comm {
+    slu_comm *c = nullptr;
+    int nprow = 0, npcol = 0, npdep = 0, iam = -1;
+    MPI_Comm comms[4]; // layer, process row, process column, z
+};
+
+int mpi_host_p2p(void *ctx, int nops, const slu_host_p2p_op *ops) {
+    Grid3Comm *g = (Grid3Comm *)ctx;
+    std::vector<MPI_Request> rq;
+    for (int i = 0; i < nops; ++i) {
+        char *p = (char *)ops[i].buf;
+        int64_t left = ops[i].bytes;
+        while (left > 0) { // pieces of <= 1 GiB, matched in order
+            const int cnt = (int)std::min<int64_t>(left, 1 << 30);
+            MPI_Request r;
+            const MPI_Comm cm = g->comms[ops[i].group];
+            const int rc = ops[i].send ? mpi().isend(p, cnt, MPI_BYTE, ops[i].peer, 7301, cm, &r)
+                                       : mpi().irecv(p, cnt, MPI_BYTE, ops[i].peer, 7301, cm, &r);
+            if (rc != MPI_SUCCESS) return 1;
+            rq.push_back(r);
+            p += cnt;
+            left -= cnt;
+        }
+    }
+    if (!rq.empty() && mpi().waitall((int)rq.size(), rq.data(), MPI_STATUSES_IGNORE) != MPI_SUCCESS)
+        return 1;
+    return 0;
+}
+
+int grid3_attr_delete(MPI_Comm, int, void *val, void *) {
+    Grid3Comm *g = (Grid3Comm *)val;
+    slu_comm_destroy(g->c);
+    delete g;
+    return MPI_SUCCESS;
+}
+int g_keyval3 = MPI_KEYVAL_INVALID;
+
+slu_comm *comm_for_grid3d(gridinfo3d_t *g3) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    const Mpi &M = mpi();
+    if (g_keyval3 == MPI_KEYVAL_INVALID)
+        M.create_keyval(MPI_COMM_NULL_COPY_FN, grid3_attr_delete, &g_keyval3, nullptr);
+    const int nprow = (int)g3->nprow, npcol = (int)g3->npcol, npdep = (int)g3->npdep;
+    void *val = nullptr;
+    int flag = 0;
+    M.get_attr(g3->comm, g_keyval3, &val, &flag);
+    if (flag) {
+        Grid3Comm *g = (Grid3Comm *)val;
+        if (g->nprow == nprow && g->npcol == npcol && g->npdep == npdep && g->iam == g3->iam)
+            return g->c;
+    }
+    SLU_REQUIRE(g3->rankorder == 0, "pdgstrf3d: only the default Z-major rank order");
+    const int P = nprow * npcol * npdep;
+    const int dev = pick_device(g3->iam);
+    std::vector<int> devs(P, -1);
+    M.allgather(&dev, 1, MPI_INT, devs.data(), 1, MPI_INT, g3->comm);
+    std::vector<int> sorted(devs);
+    std::sort(sorted.begin(), sorted.end());
+    bool host = std::adjacent_find(sorted.begin(), sorted.end()) != sorted.end();
+    if (const char *t = getenv("SUPERLU_MI355X_TRANSPORT")) host = !strcmp(t, "mpi");
+    auto *g = new Grid3Comm;
+    g->nprow = nprow;
+    g->npcol = npcol;
+    g->npdep = npdep;
+    g->iam = g3->iam;
+    g->comms[0] = g3->grid2d.comm;
+    g->comms[1] = g3->grid2d.rscp.comm;
+    g->comms[2] = g3->grid2d.cscp.comm;
+    g->comms[3] = g3->zscp.comm;
+    // the engine's 3D rank is layer * Pr * Pc + the rank in the layer's grid
+    const int iam3 = g3->zscp.Iam * nprow * npcol + g3->grid2d.iam;
+    if (host) {
+        g->c = slu_comm_create_host_p2p3d(mpi_host_p2p, g, nprow, npcol, npdep, iam3, dev);
+    } else {
+        unsigned char uid[128] = {0};
+        if (g3->iam == 0 && slu_comm_unique_id(uid) != 0) throw slu::Error(slu_last_error());
+        M.bcast(uid, 128, MPI_BYTE, 0, g3->comm);
+        g->c = slu_comm_create3d(uid, nprow, npcol, npdep, iam3, dev);
+    }
+    if (!g->c) {
+        delete g;
+        throw slu::Error(slu_last_error());
+    }
+    M.set_attr(g3->comm, g_keyval3, g);
+    return g->c;
+}
+
+template <typename LUS>
+int_t pxgstrf3d(int dtype, const char *name, superlu_dist_options_t *options, int m, int n,
+                double anorm, dtrf3Dpartition_t *trf, LUS *LUstruct, gridinfo3d_t *g3,
+                SuperLUStat_t *stat, int *info) {
+    gridinfo_t *grid = &g3->grid2d;
+    *info = 0;
+    if (m < 0) *info = -2;
+    else if (n < 0) *info = -3;
+    if (*info) {
+        printf("{%lld,%lld}: On entry to %6s, parameter number %lld had an illegal value\n",
+               (long long)(grid->iam / grid->npcol), (long long)(grid->iam % grid->npcol), name,
+               (long long)-*info);
+        return -1;
+    }
+    if (m == 0 || n == 0) return 0;
+    stat->ops[SLU_PHASE_FACT] = 0.0f;
+    stat->current_buffer = stat->peak_buffer = stat->gpu_buffer = 0.0f;
+    stat->num_look_aheads = std::max(0, std::min(options->num_lookaheads, SLU_MAX_LOOKAHEADS - 1));
+    slu_plan *plan = nullptr;
+    try {
+        SLU_REQUIRE(trf && trf->supernode2treeMap, "%s: no trf3Dpartition", name);
+        reap_join();
+        slu_comm *c = comm_for_grid3d(g3);
+        slu_engine_opts eo{};
+        eo.replace_tiny_pivot = options->ReplaceTinyPivot == SLU_YES;
+        eo.overlap_upload = 1;
+        eo.forest_map = (const int64_t *)trf->supernode2treeMap;
+        char err[512] = {0};
+        plan = slu_plan_create(dtype, LUstruct, n, (int)g3->nprow, (int)g3->npcol, grid->iam, c,
+                               &eo, err, sizeof err);
+        if (!plan) throw slu::Error(err);
+        int myinfo = 0, tiny = 0;
+        if (slu_plan_upload(plan) || slu_plan_factor(plan, anorm, &myinfo, &tiny) ||
+            slu_plan_download(plan))
+            throw slu::Error(slu_last_error());
+        slu_plan_stats st;
+        slu_plan_get_stats(plan, &st);
+        // reduceStat(FACT, ...) (SRC/util.c:1283-1296): the layers' sum on layer 0
+        float mine = (float)(st.schur_flops + st.panel_flops), all = mine;
+        mpi().allreduce(&mine, &all, 1, MPI_FLOAT, MPI_SUM, g3->zscp.comm);
+        stat->ops[SLU_PHASE_FACT] = g3->zscp.Iam == 0 ? all : mine;
+        stat->TinyPivots += tiny;
+        stat->gpu_buffer = (float)(st.lu_bytes + st.index_bytes);
+        reap_later(plan);
+        plan = nullptr;
+        *info = myinfo; // the engine's MIN over every layer and rank
+        return 0;
+    } catch (const std::exception &e) {
+        if (plan) slu_plan_destroy(plan);
+        fprintf(stderr, "%s (MI355X engine): %s\n", name, e.what());
+        fflush(stderr);
+        abort();
+    }
+}
+
 // ------------------------------------------------------------------ scatter
 // Host implementations with the reference prototypes and semantics of
 // SRC/dscatter.c:28-277 (s/z are type substitutions).
@@ -426,6 +583,25 @@ int_t psgstrf(superlu_dist_options_t *options, int m, int n, float anorm,
 int_t pzgstrf(superlu_dist_options_t *options, int m, int n, double anorm,
               zLUstruct_t *LUstruct, gridinfo_t *grid, SuperLUStat_t *stat, int *info) {
     return pxgstrf(SLU_Z, "PZGSTRF", options, m, n, anorm, LUstruct, grid, stat, info);
+}
+
+int_t pdgstrf3d(superlu_dist_options_t *options, int m, int n, double anorm,
+                dtrf3Dpartition_t *trf3Dpartition, SCT_t *, dLUstruct_t *LUstruct,
+                gridinfo3d_t *grid3d, SuperLUStat_t *stat, int *info) {
+    return pxgstrf3d(SLU_D, "PDGSTRF3D", options, m, n, anorm, trf3Dpartition, LUstruct, grid3d,
+                     stat, info);
+}
+int_t psgstrf3d(superlu_dist_options_t *options, int m, int n, float anorm,
+                strf3Dpartition_t *trf3Dpartition, SCT_t *, sLUstruct_t *LUstruct,
+                gridinfo3d_t *grid3d, SuperLUStat_t *stat, int *info) {
+    return pxgstrf3d(SLU_S, "PSGSTRF3D", options, m, n, (double)anorm, trf3Dpartition, LUstruct,
+                     grid3d, stat, info);
+}
+int_t pzgstrf3d(superlu_dist_options_t *options, int m, int n, double anorm,
+                ztrf3Dpartition_t *trf3Dpartition, SCT_t *, zLUstruct_t *LUstruct,
+                gridinfo3d_t *grid3d, SuperLUStat_t *stat, int *info) {
+    return pxgstrf3d(SLU_Z, "PZGSTRF3D", options, m, n, anorm, trf3Dpartition, LUstruct, grid3d,
+                     stat, info);
 }
 
 #define SLU_SCATTER_EXPORTS(P, T)                                                              \

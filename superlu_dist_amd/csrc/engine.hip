@@ -1196,6 +1196,15 @@ struct Plan : PlanBase {
         }
         const int nf = (1 << maxlvl) - 1;
         forest_of.assign(ns, -1);
+        if (opts.forest_map) { // the caller's partition (pdgstrf3d: supernode2treeMap)
+            for (int k = 0; k < ns; ++k) {
+                SLU_REQUIRE(opts.forest_map[k] >= 0 && opts.forest_map[k] < nf,
+                            "forest map: supernode %d in forest %lld of %d", k,
+                            (long long)opts.forest_map[k], nf);
+                forest_of[k] = (int)opts.forest_map[k];
+            }
+            return;
+        }
         vector<vector<int>> heads((size_t)nf);
         heads[0] = roots;
         auto split2 = [&](vector<int> set, vector<int> *out) {

@@ -58,7 +58,7 @@ class SluLuView(C.Structure):
 class EngineOpts(C.Structure):
     _fields_ = [("replace_tiny_pivot", C.c_int), ("timing", C.c_int), ("serial", C.c_int),
                 ("overlap_upload", C.c_int), ("overlap_download", C.c_int),
-                ("schedule_only", C.c_int), ("reserved", C.c_int * 2)]
+                ("schedule_only", C.c_int), ("forest_map", C.c_void_p)]
 
 
 class PlanStats(C.Structure):

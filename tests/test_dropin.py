@@ -112,3 +112,35 @@ def test_reference_driver_default_ordering_through_our_metis(drv, matrix):
     my_err, _, out = _run(f"{drv}_mi355x_full", 1, ["-r", "1", "-c", "1"], matrix)
     print(f"{drv} {matrix} METIS_AT_PLUS_A via the library: {my_err:.3e} (reference, MMD: {ref_err:.3e})")
     assert my_err <= max(10 * ref_err, 1e-12), (my_err, ref_err)
+
+
+# ---- 3D (pdgstrf3d): the reference's EXAMPLE/pddrive3d.c
+# (pdgssvx3d: 3D matrix distribution, dinitTrf3Dpartition's forests, its
+# ancestor zeroing, pdgstrf3d, dgatherAllFactoredLU, pdgstrs / pdgsrfs on
+# layer 0) with pdgstrf3d from libslu_mi355x_3d.so (oracle/_ref/
+# pddrive3d_mi355x, `make -C oracle dropin3d`) against the all-reference
+# driver (pddrive3d_ref, `make -C oracle ref3d`).  Several ranks share the
+# box's GPU: the library carries the layer exchanges and the ancestor
+# reductions over MPI point to point.
+
+@pytest.mark.skipif(not _have("pddrive3d_mi355x"), reason="3D drop-in driver not built")
+def test_dropin3d_driver_binds_our_pdgstrf3d():
+    dyn, und, defined = _binding("pddrive3d_mi355x")
+    assert "libslu_mi355x_3d.so" in dyn
+    assert "pdgstrf3d" in und and not re.search(r"\bT pdgstrf3d\b", defined)
+    for sym in ("pdgssvx3d", "dinitTrf3Dpartition", "dgatherAllFactoredLU", "pdgstrs"):
+        assert re.search(rf"\bT {sym}\b", defined), sym   # the reference's own
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not _have("pddrive3d_mi355x", "pddrive3d_ref"), reason="3D drivers not built")
+@pytest.mark.parametrize("grid", [(1, 1, 2), (1, 2, 2), (2, 1, 2), (1, 1, 4)])
+@pytest.mark.parametrize("matrix", ["big.rua", "g20.rua"])
+def test_reference_3d_driver_with_our_pdgstrf3d(matrix, grid):
+    r, c, d = grid
+    args = ["-r", str(r), "-c", str(c), "-d", str(d), "-q", "2"]
+    ref_err, ref_t, _ = _run("pddrive3d_ref", r * c * d, args, matrix)
+    my_err, my_t, out = _run("pddrive3d_mi355x", r * c * d, args, matrix)
+    print(f"pddrive3d {matrix} {r}x{c}x{d}: ||x-xtrue||/||x|| ref {ref_err:.3e} mi355x {my_err:.3e}; "
+          f"FACTOR time ref {ref_t} s, mi355x {my_t} s")
+    assert my_err <= max(10 * ref_err, 1e-12), (my_err, ref_err)
