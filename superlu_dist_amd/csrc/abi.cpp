@@ -15,7 +15,10 @@
 // process at run time (this library has no link-time MPI dependency).  A 1x1
 // grid makes no MPI call.
 #include <dlfcn.h>
+#include <execinfo.h>
 #include <hip/hip_runtime.h>
+#include <signal.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <cstdio>
@@ -67,6 +70,21 @@ const Mpi &mpi() {
         return x;
     }();
     return m;
+}
+
+// SUPERLU_MI355X_SEGV_TRACE=1 (diagnostics): a host backtrace on SIGSEGV
+void segv_trace(int sig) {
+    void *fr[64];
+    const int n = backtrace(fr, 64);
+    static const char msg[] = "[slu] SIGSEGV, host backtrace:\n";
+    (void)!write(2, msg, sizeof msg - 1);
+    backtrace_symbols_fd(fr, n, 2);
+    signal(sig, SIG_DFL);
+    raise(sig);
+}
+void maybe_trace_segv() {
+    const char *e = getenv("SUPERLU_MI355X_SEGV_TRACE");
+    if (e && atoi(e) == 1) signal(SIGSEGV, segv_trace);
 }
 
 int pick_device(int iam) {
@@ -381,6 +399,15 @@ int grid3_attr_delete(MPI_Comm, int, void *val, void *) {
 }
 int g_keyval3 = MPI_KEYVAL_INVALID;
 
+// SUPERLU_MI355X_SCHEDULE_ONLY=1 (test hook, no GPU needed): pdgstrf3d builds
+// schedule-only plans over the MPI point-to-point transport, replays every
+// exchange of the factorization with checked bytes (slu_plan_check_exchange)
+// and returns without factoring.
+bool schedule_only_3d() {
+    const char *e = getenv("SUPERLU_MI355X_SCHEDULE_ONLY");
+    return e && atoi(e) == 1;
+}
+
 slu_comm *comm_for_grid3d(gridinfo3d_t *g3) {
     std::lock_guard<std::mutex> lk(g_mu);
     const Mpi &M = mpi();
@@ -397,13 +424,14 @@ slu_comm *comm_for_grid3d(gridinfo3d_t *g3) {
     }
     SLU_REQUIRE(g3->rankorder == 0, "pdgstrf3d: only the default Z-major rank order");
     const int P = nprow * npcol * npdep;
-    const int dev = pick_device(g3->iam);
+    const bool dry = schedule_only_3d();
+    const int dev = dry ? -1 : pick_device(g3->iam);
     std::vector<int> devs(P, -1);
     M.allgather(&dev, 1, MPI_INT, devs.data(), 1, MPI_INT, g3->comm);
     std::vector<int> sorted(devs);
     std::sort(sorted.begin(), sorted.end());
-    bool host = std::adjacent_find(sorted.begin(), sorted.end()) != sorted.end();
-    if (const char *t = getenv("SUPERLU_MI355X_TRANSPORT")) host = !strcmp(t, "mpi");
+    bool host = dry || std::adjacent_find(sorted.begin(), sorted.end()) != sorted.end();
+    if (const char *t = getenv("SUPERLU_MI355X_TRANSPORT")) host = host || !strcmp(t, "mpi");
     auto *g = new Grid3Comm;
     g->nprow = nprow;
     g->npcol = npcol;
@@ -451,6 +479,7 @@ int_t pxgstrf3d(int dtype, const char *name, superlu_dist_options_t *options, in
     stat->num_look_aheads = std::max(0, std::min(options->num_lookaheads, SLU_MAX_LOOKAHEADS - 1));
     slu_plan *plan = nullptr;
     try {
+        maybe_trace_segv();
         SLU_REQUIRE(trf && trf->supernode2treeMap, "%s: no trf3Dpartition", name);
         reap_join();
         slu_comm *c = comm_for_grid3d(g3);
@@ -458,6 +487,26 @@ int_t pxgstrf3d(int dtype, const char *name, superlu_dist_options_t *options, in
         eo.replace_tiny_pivot = options->ReplaceTinyPivot == SLU_YES;
         eo.overlap_upload = 1;
         eo.forest_map = (const int64_t *)trf->supernode2treeMap;
+        if (schedule_only_3d()) {
+            eo.overlap_upload = 0;
+            eo.schedule_only = 1;
+            char err[512] = {0};
+            plan = slu_plan_create(dtype, LUstruct, n, (int)g3->nprow, (int)g3->npcol, grid->iam,
+                                   c, &eo, err, sizeof err);
+            if (!plan) throw slu::Error(err);
+            int64_t ns = 0, nb = 0;
+            if (slu_plan_check_exchange(plan, &ns, &nb)) throw slu::Error(slu_last_error());
+            slu_plan_stats st;
+            slu_plan_get_stats(plan, &st);
+            printf("[%s schedule] rank %d layer %lld: %lld supernodes factored in %lld levels, "
+                   "%lld sections / %lld bytes received, exchange checked\n",
+                   name, g3->iam, (long long)st.zlayer, (long long)st.nsupers,
+                   (long long)st.nlevels, (long long)ns, (long long)nb);
+            fflush(stdout);
+            slu_plan_destroy(plan);
+            plan = nullptr;
+            return 0;
+        }
         char err[512] = {0};
         plan = slu_plan_create(dtype, LUstruct, n, (int)g3->nprow, (int)g3->npcol, grid->iam, c,
                                &eo, err, sizeof err);

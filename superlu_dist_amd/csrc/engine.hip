@@ -1590,7 +1590,8 @@ struct Plan : PlanBase {
         }
         if (!xmode) return;
         // odd levels use the second panel slot
-        const i64 slot = *std::max_element(pan_level.begin(), pan_level.end());
+        // (a 3D layer may factor nothing: no levels)
+        const i64 slot = pan_level.empty() ? 0 : *std::max_element(pan_level.begin(), pan_level.end());
         for (size_t L = 1; L < levels.size(); L += 2) {
             const LevelRange &R = levels[L];
             for (int k : bylev[L]) {

@@ -132,15 +132,55 @@ def test_dropin3d_driver_binds_our_pdgstrf3d():
         assert re.search(rf"\bT {sym}\b", defined), sym   # the reference's own
 
 
+def _run_schedule(exe, nprocs, args, matrix, timeout=240):
+    """SUPERLU_MI355X_SCHEDULE_ONLY=1: pdgstrf3d builds schedule-only plans
+    (no GPU) over the MPI point-to-point transport and replays every
+    exchange with checked bytes, then returns without factoring."""
+    env = dict(os.environ, OMP_NUM_THREADS="1", MKL_NUM_THREADS="1",
+               SUPERLU_MI355X_SCHEDULE_ONLY="1")
+    cmd = [MPIEXEC, "-n", str(nprocs), os.path.join(REF, exe)] + args + [os.path.join(MAT, matrix)]
+    r = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=timeout)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, f"{exe} failed ({r.returncode}):\n{out[-3000:]}"
+    return re.findall(r"layer (\d+): (\d+) supernodes factored in (\d+) levels, (\d+) sections / "
+                      r"(\d+) bytes received, exchange checked", out)
+
+
+# (driver, matrix, ordering args): MMD (-q 2) and the default METIS_AT_PLUS_A
+# served by libslu_mi355x_metis.so (the _nd drivers)
+CASES3D = [("pddrive3d", "big.rua", ["-q", "2"]), ("pddrive3d", "g20.rua", ["-q", "2"]),
+           ("pddrive3d", "lap3d12.rua", ["-q", "2"]), ("pddrive3d_nd", "lap3d12.rua", [])]
+GRIDS3D = [(1, 1, 2), (1, 2, 2), (2, 1, 2), (1, 1, 4), (2, 2, 2)]
+
+
+@pytest.mark.skipif(not _have("pddrive3d_mi355x", "pddrive3d_mi355x_nd"), reason="3D drivers not built")
+@pytest.mark.parametrize("grid", GRIDS3D)
+@pytest.mark.parametrize("drv,matrix,order", CASES3D)
+def test_dropin3d_exchange_schedule_cpu(drv, matrix, order, grid):
+    """No GPU: the reference's pdgssvx3d up to pdgstrf3d (its forests, its
+    3D LUstruct from dp3dScatter on every layer), then our schedule-only
+    plans replay the layer exchanges and the ancestor reductions over MPI."""
+    r, c, d = grid
+    exe = drv.replace("pddrive3d", "pddrive3d_mi355x")
+    rows = _run_schedule(exe, r * c * d, ["-r", str(r), "-c", str(c), "-d", str(d)] + order, matrix)
+    assert len(rows) == r * c * d
+    layers = {}
+    for z, ns, nl, nsec, nb in rows:
+        layers.setdefault(int(z), set()).add(int(ns))
+    assert sorted(layers) == list(range(d))
+    assert all(len(v) == 1 for v in layers.values())     # one count per layer
+    assert sum(next(iter(v)) for v in layers.values()) > 0
+
+
 @pytest.mark.gpu
 @pytest.mark.skipif(not _have("pddrive3d_mi355x", "pddrive3d_ref"), reason="3D drivers not built")
-@pytest.mark.parametrize("grid", [(1, 1, 2), (1, 2, 2), (2, 1, 2), (1, 1, 4)])
-@pytest.mark.parametrize("matrix", ["big.rua", "g20.rua"])
-def test_reference_3d_driver_with_our_pdgstrf3d(matrix, grid):
+@pytest.mark.parametrize("grid", GRIDS3D)
+@pytest.mark.parametrize("drv,matrix,order", CASES3D)
+def test_reference_3d_driver_with_our_pdgstrf3d(drv, matrix, order, grid):
     r, c, d = grid
-    args = ["-r", str(r), "-c", str(c), "-d", str(d), "-q", "2"]
-    ref_err, ref_t, _ = _run("pddrive3d_ref", r * c * d, args, matrix)
-    my_err, my_t, out = _run("pddrive3d_mi355x", r * c * d, args, matrix)
-    print(f"pddrive3d {matrix} {r}x{c}x{d}: ||x-xtrue||/||x|| ref {ref_err:.3e} mi355x {my_err:.3e}; "
+    args = ["-r", str(r), "-c", str(c), "-d", str(d)] + order
+    ref_err, ref_t, _ = _run(drv.replace("pddrive3d", "pddrive3d_ref"), r * c * d, args, matrix)
+    my_err, my_t, out = _run(drv.replace("pddrive3d", "pddrive3d_mi355x"), r * c * d, args, matrix)
+    print(f"{drv} {matrix} {r}x{c}x{d}: ||x-xtrue||/||x|| ref {ref_err:.3e} mi355x {my_err:.3e}; "
           f"FACTOR time ref {ref_t} s, mi355x {my_t} s")
     assert my_err <= max(10 * ref_err, 1e-12), (my_err, ref_err)

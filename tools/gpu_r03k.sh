@@ -4,5 +4,5 @@
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/${1:-r03k}; mkdir -p $O
-timeout -k 10 600 python -u -m pytest tests/test_dropin.py tests/test_grid3d.py -m gpu -v -s --timeout 300 \
-    --timeout-method thread > $O/pytest.log 2>&1; rc=$?; grep -E "PASS|FAIL|ERROR|pddrive3d|passed|failed" $O/pytest.log | tail -60; exit $rc
+timeout -k 10 800 python -u -m pytest tests/test_dropin.py tests/test_grid3d.py -m gpu -v -s --timeout 300 \
+    --timeout-method thread > $O/pytest.log 2>&1; rc=$?; grep -E "pddrive|passed|failed" $O/pytest.log | tail -70; exit $rc
