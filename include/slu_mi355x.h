@@ -195,6 +195,10 @@ int slu_plan_upload(slu_plan *p);
 /* Numeric factorization on the device (inputs resident in HBM).
  * anorm is used for the tiny-pivot threshold as in SRC/pdgstrf.c:412-413. */
 int slu_plan_factor(slu_plan *p, double anorm, int *info, int *tiny_pivots);
+/* Upload the host LUstruct's values as FINISHED factors (e.g. from an
+ * earlier pdgstrf): the device storage then serves slu_plan_solve / refine
+ * without a factorization. */
+int slu_plan_adopt_factors(slu_plan *p);
 /* Keep a pristine device copy of the uploaded values (snapshot) and restore
  * the working factor storage from it (benchmark repetitions; device-to-device). */
 int slu_plan_snapshot(slu_plan *p);

@@ -21,6 +21,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -227,6 +228,7 @@ struct CachedPlan {
     slu_plan *plan = nullptr;
     uint64_t digest = 0;
     int dtype = -1, n = -1, replace_tiny = -1;
+    const void *lu = nullptr; // the LUstruct the cached factors belong to (pdgstrs)
 };
 CachedPlan g_cache;
 std::mutex g_cache_mu;
@@ -334,6 +336,7 @@ int_t pxgstrf(int dtype, const char *name, superlu_dist_options_t *options, int 
             g_cache.dtype = dtype;
             g_cache.n = n;
             g_cache.replace_tiny = rt;
+            g_cache.lu = LUstruct;
         } else {
             reap_later(plan);
         }
@@ -535,6 +538,116 @@ int_t pxgstrf3d(int dtype, const char *name, superlu_dist_options_t *options, in
     }
 }
 
+// ------------------------------------------------------------------ solve
+// pdgstrs (SRC/pdgstrs.c:1035-3139) on the device-resident factors: the
+// plan the last pdgstrf on this LUstruct left in the cache (1x1 grids; its
+// factors never left HBM), else a plan that adopts the LUstruct's host
+// factors (grids: collective over grid->comm).  B holds rows fst_row ..
+// fst_row + m_loc - 1 of the right-hand sides; as pdReDistribute_B_to_X /
+// X_to_B (:59-72 of each), row i goes to position perm_c[perm_r[i]] of the
+// LUstruct's coordinates, L U y = P b is solved (slu_plan_solve), and the
+// same rows of y come back in B (pdgssvx undoes perm_c afterwards).
+// Exported by libslu_mi355x_solve.so with p[dsz]Compute_Diag_Inv, which the
+// device solve does not need (the reference's is empty without
+// SLU_HAVE_LAPACK, SRC/pdgstrs.c:4550).  pdgsrfs stays the reference's and
+// calls this pdgstrs for every refinement step.
+struct Mpi2 {
+    int (*allgatherv)(const void *, int, MPI_Datatype, void *, const int *, const int *,
+                      MPI_Datatype, MPI_Comm) = nullptr;
+};
+const Mpi2 &mpi2() {
+    static Mpi2 m = [] {
+        Mpi2 x;
+        mpi_sym(x.allgatherv, "MPI_Allgatherv");
+        return x;
+    }();
+    return m;
+}
+
+template <typename LUS, typename HT>
+void pxgstrs(int dtype, const char *name, int_t n, LUS *LU, xScalePermstruct_t *sp,
+             gridinfo_t *grid, HT *B, int_t m_loc, int_t fst_row, int_t ldb, int nrhs,
+             SuperLUStat_t *stat, int *info) {
+    const auto t0 = std::chrono::steady_clock::now();
+    *info = 0;
+    if (n < 0) *info = -1;
+    else if (nrhs < 0) *info = -9;
+    if (*info) {
+        printf("{%lld,%lld}: On entry to %6s, parameter number %lld had an illegal value\n",
+               (long long)(grid->iam / grid->npcol), (long long)(grid->iam % grid->npcol), name,
+               (long long)-*info);
+        return;
+    }
+    if (n == 0 || nrhs == 0) return;
+    slu_plan *plan = nullptr;
+    bool cached = false;
+    try {
+        const bool one = grid->nprow * grid->npcol == 1;
+        if (one) {
+            std::lock_guard<std::mutex> lk(g_cache_mu);
+            if (g_cache.plan && g_cache.lu == LU && g_cache.dtype == dtype && g_cache.n == n) {
+                plan = g_cache.plan;
+                cached = true;
+            }
+        }
+        if (!plan) {
+            reap_join();
+            slu_comm *c = comm_for_grid(grid);
+            slu_engine_opts eo{};
+            char err[512] = {0};
+            plan = slu_plan_create(dtype, LU, (int)n, (int)grid->nprow, (int)grid->npcol, grid->iam,
+                                   c, &eo, err, sizeof err);
+            if (!plan) throw slu::Error(err);
+            if (slu_plan_adopt_factors(plan)) throw slu::Error(slu_last_error());
+        }
+        // the whole right-hand side on every rank, in the LUstruct's order
+        std::vector<HT> y((size_t)n * nrhs), bl;
+        const int_t *pr = sp->perm_r, *pc = sp->perm_c;
+        auto place = [&](const HT *src, int_t ld, int_t r0, int_t cnt) {
+            for (int j = 0; j < nrhs; ++j)
+                for (int_t i = 0; i < cnt; ++i) y[(size_t)j * n + pc[pr[r0 + i]]] = src[i + (size_t)j * ld];
+        };
+        if (one) {
+            place(B, ldb, 0, n);
+        } else {
+            const int P = (int)(grid->nprow * grid->npcol);
+            std::vector<int64_t> mine = {fst_row, m_loc}, all(2 * (size_t)P);
+            mpi().allgather(mine.data(), 2, MPI_INT64_T, all.data(), 2, MPI_INT64_T, grid->comm);
+            // rows go as bytes, one right-hand side at a time
+            std::vector<int> cnt(P), dsp(P);
+            for (int r = 0; r < P; ++r) {
+                cnt[r] = (int)(all[2 * r + 1] * sizeof(HT));
+                dsp[r] = (int)(all[2 * r] * sizeof(HT));
+            }
+            std::vector<HT> col(n), glob((size_t)n * nrhs);
+            for (int j = 0; j < nrhs; ++j) {
+                for (int_t i = 0; i < m_loc; ++i) col[i] = B[i + (size_t)j * ldb];
+                mpi2().allgatherv(col.data(), (int)(m_loc * sizeof(HT)), MPI_BYTE,
+                                  glob.data() + (size_t)j * n, cnt.data(), dsp.data(), MPI_BYTE,
+                                  grid->comm);
+            }
+            place(glob.data(), n, 0, n);
+        }
+        if (slu_plan_solve(plan, y.data(), n, nrhs)) throw slu::Error(slu_last_error());
+        for (int j = 0; j < nrhs; ++j)
+            for (int_t i = 0; i < m_loc; ++i) B[i + (size_t)j * ldb] = y[(size_t)j * n + fst_row + i];
+        slu_plan_stats st;
+        slu_plan_get_stats(plan, &st);
+        // reference accounting: 2 flops per stored factor entry per right-hand side
+        const double vals = st.lu_bytes / (double)sizeof(HT);
+        stat->ops[SLU_PHASE_SOLVE] = (float)(2.0 * vals * nrhs * (dtype == SLU_Z ? 4 : 1));
+        if (!cached) reap_later(plan);
+        plan = nullptr;
+        stat->utime[SLU_PHASE_SOLVE] =
+            std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    } catch (const std::exception &e) {
+        if (plan && !cached) slu_plan_destroy(plan);
+        fprintf(stderr, "%s (MI355X engine): %s\n", name, e.what());
+        fflush(stderr);
+        abort();
+    }
+}
+
 // ------------------------------------------------------------------ scatter
 // Host implementations with the reference prototypes and semantics of
 // SRC/dscatter.c:28-277 (s/z are type substitutions).
@@ -651,6 +764,37 @@ int_t pzgstrf3d(superlu_dist_options_t *options, int m, int n, double anorm,
                 gridinfo3d_t *grid3d, SuperLUStat_t *stat, int *info) {
     return pxgstrf3d(SLU_Z, "PZGSTRF3D", options, m, n, anorm, trf3Dpartition, LUstruct, grid3d,
                      stat, info);
+}
+
+void pdgstrs(superlu_dist_options_t *, int_t n, dLUstruct_t *LUstruct,
+             xScalePermstruct_t *ScalePermstruct, gridinfo_t *grid, double *B, int_t m_loc,
+             int_t fst_row, int_t ldb, int nrhs, xSOLVEstruct_t *, SuperLUStat_t *stat,
+             int *info) {
+    pxgstrs(SLU_D, "PDGSTRS", n, LUstruct, ScalePermstruct, grid, B, m_loc, fst_row, ldb, nrhs,
+            stat, info);
+}
+void psgstrs(superlu_dist_options_t *, int_t n, sLUstruct_t *LUstruct,
+             xScalePermstruct_t *ScalePermstruct, gridinfo_t *grid, float *B, int_t m_loc,
+             int_t fst_row, int_t ldb, int nrhs, xSOLVEstruct_t *, SuperLUStat_t *stat,
+             int *info) {
+    pxgstrs(SLU_S, "PSGSTRS", n, LUstruct, ScalePermstruct, grid, B, m_loc, fst_row, ldb, nrhs,
+            stat, info);
+}
+void pzgstrs(superlu_dist_options_t *, int_t n, zLUstruct_t *LUstruct,
+             xScalePermstruct_t *ScalePermstruct, gridinfo_t *grid, doublecomplex *B,
+             int_t m_loc, int_t fst_row, int_t ldb, int nrhs, xSOLVEstruct_t *,
+             SuperLUStat_t *stat, int *info) {
+    pxgstrs(SLU_Z, "PZGSTRS", n, LUstruct, ScalePermstruct, grid, B, m_loc, fst_row, ldb, nrhs,
+            stat, info);
+}
+void pdCompute_Diag_Inv(int_t, dLUstruct_t *, gridinfo_t *, SuperLUStat_t *, int *info) {
+    if (info) *info = 0;
+}
+void psCompute_Diag_Inv(int_t, sLUstruct_t *, gridinfo_t *, SuperLUStat_t *, int *info) {
+    if (info) *info = 0;
+}
+void pzCompute_Diag_Inv(int_t, zLUstruct_t *, gridinfo_t *, SuperLUStat_t *, int *info) {
+    if (info) *info = 0;
 }
 
 #define SLU_SCATTER_EXPORTS(P, T)                                                              \

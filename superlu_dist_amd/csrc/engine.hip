@@ -396,6 +396,7 @@ struct PlanBase {
     virtual void refine(const void *b, void *x, int64_t ld, int nrhs, double *berr, int *steps) = 0;
     virtual void check_exchange(int64_t *nsec, int64_t *nbytes) = 0;
     virtual void gather_layers() { throw Error("gather_layers: not a 3D plan"); }
+    virtual void adopt_factors() = 0; // upload host values that are already factors
     slu_plan_stats stats{};
 };
 
@@ -2489,6 +2490,11 @@ struct Plan : PlanBase {
         opts.timing = timing;
         opts.serial = serial;
     }
+    void adopt_factors() override {
+        upload();
+        sync();
+        vstate = 2;
+    }
     void sync() override {
         HIPCHK(hipStreamSynchronize(pstream));
         HIPCHK(hipStreamSynchronize(stream));
@@ -3856,6 +3862,13 @@ struct AmalgPlan : PlanBase {
         sync_stats();
         stats.t_upload_wait_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
     }
+    void adopt_factors() override {
+        upload();
+        in->sync();
+        in->vstate = 2;
+        coarse_current = true;
+        host_done = true; // the caller's arrays hold these factors already
+    }
     void factor(double anorm, int *info, int *tiny) override {
         compressed_to = 0;
         in->factor(anorm, info, tiny);
@@ -4158,6 +4171,16 @@ slu_plan *slu_plan_create(int dtype, void *LU, int n, int nprow, int npcol, int 
 int slu_plan_gather3d(slu_plan *p) {
     try {
         p->impl->gather_layers();
+        return 0;
+    } catch (const std::exception &e) {
+        set_last_error(e.what());
+        return -1;
+    }
+}
+
+int slu_plan_adopt_factors(slu_plan *p) {
+    try {
+        p->impl->adopt_factors();
         return 0;
     } catch (const std::exception &e) {
         set_last_error(e.what());

@@ -114,6 +114,40 @@ def test_reference_driver_default_ordering_through_our_metis(drv, matrix):
     assert my_err <= max(10 * ref_err, 1e-12), (my_err, ref_err)
 
 
+# ---- device solve behind pdgssvx: p?drive_mi355x_solve
+# links libslu_mi355x_solve.so, whose p?gstrs solves on the factors the
+# preceding p?gstrf left in HBM (1 rank; on the 2x2 grid a plan adopts the
+# host factors); the reference's pdgsrfs calls it for every refinement step.
+
+@pytest.mark.skipif(not _have("pddrive_mi355x_solve"), reason="solve drop-in drivers not built")
+def test_dropin_solve_driver_binds_our_pdgstrs():
+    dyn, und, defined = _binding("pddrive_mi355x_solve")
+    assert "libslu_mi355x_solve.so" in dyn
+    for sym in ("pdgstrf", "pdgstrs", "pdCompute_Diag_Inv"):
+        assert sym in und and not re.search(rf"\bT {sym}\b", defined), sym
+    for sym in ("pdgsrfs", "pdgssvx", "pddistribute"):
+        assert re.search(rf"\bT {sym}\b", defined), sym   # the reference's own
+    assert not re.search(r"\bT pdReDistribute_B_to_X\b", defined)  # pdgstrs.o not linked
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not _have("pddrive_mi355x_solve", "pddrive_ref"), reason="drivers not built")
+@pytest.mark.parametrize("nprocs,grid", [(1, ["-r", "1", "-c", "1"]), (4, ["-r", "2", "-c", "2"])])
+@pytest.mark.parametrize("drv,matrix,extra", CASES)
+def test_reference_driver_with_our_factorization_and_solve(drv, matrix, extra, nprocs, grid):
+    args = grid + ["-q", "2"] + extra
+    ref_err, _, ref_out = _run(f"{drv}_ref", nprocs, args, matrix)
+    my_err, _, out = _run(f"{drv}_mi355x_solve", nprocs, args, matrix)
+    tol = 1e-4 if drv == "psdrive" else 1e-12
+    t = lambda o, k: (re.search(rf"{k} time\s+([0-9.]+)", o) or [None, None])[1]  # noqa: E731
+    steps = lambda o: (re.search(r"REFINEMENT time\s+[0-9.]+\s+Steps\s+(\d+)", o) or [None, None])[1]  # noqa: E731
+    print(f"{drv} {matrix} {nprocs} ranks: ||x-xtrue||/||x|| ref {ref_err:.3e} mi355x {my_err:.3e}; "
+          f"SOLVE ref {t(ref_out, 'SOLVE')} s / mi355x {t(out, 'SOLVE')} s, REFINEMENT ref "
+          f"{t(ref_out, 'REFINEMENT')} s ({steps(ref_out)} steps) / mi355x {t(out, 'REFINEMENT')} s "
+          f"({steps(out)} steps)")
+    assert my_err <= max(10 * ref_err, tol), (my_err, ref_err)
+
+
 # ---- 3D (pdgstrf3d): the reference's EXAMPLE/pddrive3d.c
 # (pdgssvx3d: 3D matrix distribution, dinitTrf3Dpartition's forests, its
 # ancestor zeroing, pdgstrf3d, dgatherAllFactoredLU, pdgstrs / pdgsrfs on
