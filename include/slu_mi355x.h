@@ -445,6 +445,13 @@ void *slu_distribute_glu(int dtype, int64_t n, const int_t *xsup, const int_t *s
                          const int_t *usub, const int64_t *xa, const int64_t *asub,
                          const void *a, int nprow, int npcol, int myrow, int mycol);
 
+/* pddistribute's SamePattern_SameRowPerm branch on a library-built (or any
+ * layout-compatible) LUstruct: zero its L / U values and drop in A's entries
+ * (CSC in the LUstruct's coordinates, as slu_distribute_glu takes them). */
+int slu_refill_values(int dtype, void *LUstruct, int64_t n, const int64_t *xa,
+                      const int64_t *asub, const void *a, int nprow, int npcol,
+                      int myrow, int mycol);
+
 /* Permuted-matrix helpers for tests: B = P*A*P^T in CSC. */
 slu_csc *slu_permute(const slu_csc *A, const int64_t *perm_c);
 

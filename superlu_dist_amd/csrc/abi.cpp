@@ -648,6 +648,139 @@ void pxgstrs(int dtype, const char *name, int_t n, LUS *LU, xScalePermstruct_t *
     }
 }
 
+// ------------------------------------------------------------------ distribute
+// pddistribute (SRC/pddistribute.c:327-2398) for callers that also take
+// pdgstrs from this library (libslu_mi355x_solve.so).  The LU storage is the
+// restated structural distribute (csrc/distribute.cpp: index arrays, block
+// order, values, ToRecv / ToSendD / ToSendR and bufmax bit for bit with the
+// reference's), built on host threads from Glu_persist + Glu_freeable and A
+// -- the caller's NRformat_loc rows, row i going to perm_c[perm_r[i]] as in
+// dReDistribute_A (:113-116; pdgssvx has already mapped the column indices
+// through perm_c, SRC/pdgssvx.c:1140), gathered to every rank on grids.  The
+// reference's triangular-solve metadata (trees, fmod / bmod, send lists,
+// :1543-2236) is only read by the reference's pdgstrs, which the same library
+// replaces; its fields are left as valid empty placeholders (every tree
+// marked empty, the send lists allocated) so that dDestroy_LU frees them as
+// usual.  Fact == SamePattern_SameRowPerm refills the values of the existing
+// structure (:545-672).
+template <typename T, typename LUS>
+float pxdistribute(int dtype, const char *name, superlu_dist_options_t *options, int_t n,
+                   SuperMatrix *A, xScalePermstruct_t *sp, Glu_freeable_t *glu, LUS *LU,
+                   gridinfo_t *grid) {
+    try {
+        const NRformat_loc *As = (const NRformat_loc *)A->Store;
+        const int_t *pr = sp->perm_r, *pc = sp->perm_c;
+        const int Pr = (int)grid->nprow, Pc = (int)grid->npcol, P = Pr * Pc;
+        const int myrow = grid->iam / Pc, mycol = grid->iam % Pc;
+        // ---- A in the LUstruct's coordinates, as CSC (every rank: all of it)
+        const i64 nl = As->rowptr[As->m_loc] - As->rowptr[0];
+        std::vector<int64_t> ri, ci;
+        std::vector<T> vv;
+        {
+            std::vector<int64_t> r((size_t)nl), c((size_t)nl);
+            std::vector<T> v((size_t)nl);
+            const T *av = (const T *)As->nzval;
+            i64 e = 0;
+            for (i64 i = 0; i < As->m_loc; ++i)
+                for (i64 p = As->rowptr[i]; p < As->rowptr[i + 1]; ++p, ++e) {
+                    r[e] = pc[pr[i + As->fst_row]];
+                    c[e] = As->colind[p];
+                    v[e] = av[p];
+                }
+            if (P == 1) {
+                ri.swap(r);
+                ci.swap(c);
+                vv.swap(v);
+            } else {
+                std::vector<int64_t> cnt(P);
+                int64_t mine = nl;
+                mpi().allgather(&mine, 1, MPI_INT64_T, cnt.data(), 1, MPI_INT64_T, grid->comm);
+                i64 tot = 0;
+                std::vector<int> bc(P), bd(P);
+                for (int q = 0; q < P; ++q) tot += cnt[q];
+                ri.resize(tot);
+                ci.resize(tot);
+                vv.resize(tot);
+                auto gather = [&](const void *src, void *dst, int esz) {
+                    i64 off = 0;
+                    for (int q = 0; q < P; ++q) {
+                        SLU_REQUIRE(cnt[q] * esz < (1ll << 31), "%s: rank %d holds too many entries", name, q);
+                        bc[q] = (int)(cnt[q] * esz);
+                        bd[q] = (int)std::min<i64>(off, (1ll << 31) - 1);
+                        off += cnt[q] * esz;
+                    }
+                    SLU_REQUIRE(off < (1ll << 31), "%s: A too large to gather", name);
+                    mpi2().allgatherv(src, (int)(mine * esz), MPI_BYTE, dst, bc.data(), bd.data(),
+                                      MPI_BYTE, grid->comm);
+                };
+                gather(r.data(), ri.data(), 8);
+                gather(c.data(), ci.data(), 8);
+                gather(v.data(), vv.data(), (int)sizeof(T));
+            }
+        }
+        std::vector<int64_t> xa(n + 1, 0), asub(ri.size());
+        std::vector<T> aval(ri.size());
+        for (int64_t c : ci) xa[c + 1]++;
+        for (i64 j = 0; j < n; ++j) xa[j + 1] += xa[j];
+        {
+            std::vector<int64_t> f(xa.begin(), xa.end() - 1);
+            for (size_t e = 0; e < ri.size(); ++e) {
+                const i64 q = f[ci[e]]++;
+                asub[q] = ri[e];
+                aval[q] = vv[e];
+            }
+        }
+        if (options->Fact == 2 /* SamePattern_SameRowPerm */) {
+            if (slu_refill_values(dtype, LU, n, xa.data(), asub.data(), aval.data(), Pr, Pc, myrow,
+                                  mycol))
+                throw slu::Error(slu_last_error());
+            return 0.0f;
+        }
+        // ---- first-time branch: the restated structural distribute
+        const Glu_persist_t *gp = LU->Glu_persist;
+        LUS *tmp = (LUS *)slu_distribute_glu(dtype, n, gp->xsup, gp->supno, glu->xlsub, glu->lsub,
+                                             glu->xusub, glu->usub, xa.data(), asub.data(),
+                                             aval.data(), Pr, Pc, myrow, mycol);
+        if (!tmp) throw slu::Error(slu_last_error());
+        *LU->Llu = *tmp->Llu; // the arrays move over (malloc'ed: SUPERLU_FREE frees them)
+        free(tmp->Glu_persist->xsup);
+        free(tmp->Glu_persist->supno);
+        free(tmp->Glu_persist);
+        free(tmp->Llu);
+        free(tmp);
+        auto *Llu = LU->Llu;
+        const i64 ns = gp->supno[n - 1] + 1, nlc = (ns + Pc - 1) / Pc, nlr = (ns + Pr - 1) / Pr;
+        auto trees = [](i64 cnt) {
+            auto *t = (slu_ctree_mirror_t *)calloc((size_t)std::max<i64>(cnt, 1), sizeof(slu_ctree_mirror_t));
+            for (i64 i = 0; i < cnt; ++i) t[i].empty_ = SLU_YES;
+            return (C_Tree *)t;
+        };
+        Llu->LBtree_ptr = trees(nlc);
+        Llu->UBtree_ptr = trees(nlc);
+        Llu->LRtree_ptr = trees(nlr);
+        Llu->URtree_ptr = trees(nlr);
+        Llu->fsendx_plist = (int **)calloc(1, sizeof(int *));
+        Llu->fsendx_plist[0] = (int *)calloc(1, sizeof(int));
+        Llu->bsendx_plist = (int **)calloc(1, sizeof(int *));
+        Llu->bsendx_plist[0] = (int *)calloc(1, sizeof(int));
+        Llu->mod_bit = (int *)calloc((size_t)std::max<i64>(nlr, 1), sizeof(int));
+        // ilsum / ldalsum as the reference sets them (:1530-1540): my block rows' offsets
+        Llu->ilsum = (int_t *)malloc((size_t)(nlr + 1) * sizeof(int_t));
+        Llu->ilsum[0] = 0;
+        for (i64 lb = 0; lb < nlr; ++lb) {
+            const i64 gb = lb * Pr + myrow;
+            Llu->ilsum[lb + 1] = Llu->ilsum[lb] + (gb < ns ? gp->xsup[gb + 1] - gp->xsup[gb] : 0);
+        }
+        Llu->ldalsum = Llu->ilsum[nlr];
+        return (float)((double)Llu->Lnzval_bc_cnt * sizeof(T) + (double)Llu->Unzval_br_cnt * sizeof(T) +
+                       (double)(Llu->Lrowind_bc_cnt + Llu->Ufstnz_br_cnt) * sizeof(int_t));
+    } catch (const std::exception &e) {
+        fprintf(stderr, "%s (MI355X library): %s\n", name, e.what());
+        fflush(stderr);
+        abort();
+    }
+}
+
 // ------------------------------------------------------------------ scatter
 // Host implementations with the reference prototypes and semantics of
 // SRC/dscatter.c:28-277 (s/z are type substitutions).
@@ -786,6 +919,24 @@ void pzgstrs(superlu_dist_options_t *, int_t n, zLUstruct_t *LUstruct,
              SuperLUStat_t *stat, int *info) {
     pxgstrs(SLU_Z, "PZGSTRS", n, LUstruct, ScalePermstruct, grid, B, m_loc, fst_row, ldb, nrhs,
             stat, info);
+}
+float pddistribute(superlu_dist_options_t *options, int_t n, SuperMatrix *A,
+                   xScalePermstruct_t *ScalePermstruct, Glu_freeable_t *Glu_freeable,
+                   dLUstruct_t *LUstruct, gridinfo_t *grid) {
+    return pxdistribute<double>(SLU_D, "PDDISTRIBUTE", options, n, A, ScalePermstruct, Glu_freeable,
+                                LUstruct, grid);
+}
+float psdistribute(superlu_dist_options_t *options, int_t n, SuperMatrix *A,
+                   xScalePermstruct_t *ScalePermstruct, Glu_freeable_t *Glu_freeable,
+                   sLUstruct_t *LUstruct, gridinfo_t *grid) {
+    return pxdistribute<float>(SLU_S, "PSDISTRIBUTE", options, n, A, ScalePermstruct, Glu_freeable,
+                               LUstruct, grid);
+}
+float pzdistribute(superlu_dist_options_t *options, int_t n, SuperMatrix *A,
+                   xScalePermstruct_t *ScalePermstruct, Glu_freeable_t *Glu_freeable,
+                   zLUstruct_t *LUstruct, gridinfo_t *grid) {
+    return pxdistribute<doublecomplex>(SLU_Z, "PZDISTRIBUTE", options, n, A, ScalePermstruct,
+                                       Glu_freeable, LUstruct, grid);
 }
 void pdCompute_Diag_Inv(int_t, dLUstruct_t *, gridinfo_t *, SuperLUStat_t *, int *info) {
     if (info) *info = 0;

@@ -362,9 +362,99 @@ void *distribute_glu_t(i64 n, const int_t *xsup_in, const int_t *supno_in, const
     return LU;
 }
 
+// pddistribute's Fact == SamePattern_SameRowPerm branch
+// (SRC/pddistribute.c:545-672): the structure stays, L and U are zeroed and
+// A's entries (CSC of the LUstruct's coordinates) dropped into it.
+template <typename T, typename LocalLU, typename LUstruct>
+void refill_values_t(LUstruct *LU, i64 n, const i64 *xa, const i64 *asub, const T *a, int Pr,
+                     int Pc, int myrow, int mycol) {
+    const int_t *xsup = LU->Glu_persist->xsup, *supno = LU->Glu_persist->supno;
+    LocalLU *Llu = LU->Llu;
+    const i64 ns = supno[n - 1] + 1, nlc = (ns + Pc - 1) / Pc, nlr = (ns + Pr - 1) / Pr;
+    auto W = [&](i64 k) { return (i64)(xsup[k + 1] - xsup[k]); };
+    const i64 gen = next_generation();
+    slu::parallel_for((int)nlr, [&](int lb) {
+        const int_t *index = Llu->Ufstnz_br_ptr[lb];
+        if (!index) return;
+        T *uval = (T *)Llu->Unzval_br_ptr[lb];
+        const i64 gb = (i64)lb * Pr + myrow, klst = xsup[gb + 1];
+        i64 ip = SLU_BR_HEADER, vo = 0;
+        for (i64 b = 0; b < index[0]; ++b) {
+            const i64 jb = index[ip];
+            for (i64 c = 0; c < W(jb); ++c) {
+                const i64 j = xsup[jb] + c, irow = index[ip + SLU_UB_DESCRIPTOR + c], k = klst - irow;
+                T *seg = uval + vo;
+                std::fill(seg, seg + k, zero_of<T>());
+                for (i64 p = xa[j]; p < xa[j + 1]; ++p) {
+                    const i64 r = asub[p];
+                    if (r >= irow && r < klst) seg[r - irow] = a[p];
+                }
+                vo += k;
+            }
+            ip += SLU_UB_DESCRIPTOR + W(jb);
+        }
+    }, 16);
+    slu::parallel_for((int)nlc, [&](int ljb) {
+        const int_t *index = Llu->Lrowind_bc_ptr[ljb];
+        if (!index) return;
+        thread_local Scratch pos_s;
+        pos_s.fresh(gen, n);
+        vector<i64> &pos = pos_s.v;
+        T *lusup = (T *)Llu->Lnzval_bc_ptr[ljb];
+        const i64 jb = (i64)ljb * Pc + mycol, f = xsup[jb], w = W(jb), len = index[1];
+        i64 ip = SLU_BC_HEADER, r = 0;
+        for (i64 b = 0; b < index[0]; ++b) {
+            const i64 nr = index[ip + 1];
+            for (i64 i = 0; i < nr; ++i) pos[index[ip + SLU_LB_DESCRIPTOR + i]] = r++;
+            ip += SLU_LB_DESCRIPTOR + nr;
+        }
+        std::fill(lusup, lusup + len * w, zero_of<T>());
+        for (i64 c = 0; c < w; ++c) {
+            const i64 j = f + c;
+            for (i64 p = xa[j]; p < xa[j + 1]; ++p) {
+                const i64 row = asub[p];
+                if (supno[row] < jb || supno[row] % Pr != myrow) continue;
+                const i64 q = pos[row];
+                if (q >= 0) lusup[q + c * len] = a[p];
+            }
+        }
+        ip = SLU_BC_HEADER;
+        for (i64 b = 0; b < index[0]; ++b) {
+            const i64 nr = index[ip + 1];
+            for (i64 i = 0; i < nr; ++i) pos[index[ip + SLU_LB_DESCRIPTOR + i]] = -1;
+            ip += SLU_LB_DESCRIPTOR + nr;
+        }
+    }, 16);
+}
+
 } // namespace
 
 extern "C" {
+
+int slu_refill_values(int dtype, void *LU, int64_t n, const int64_t *xa, const int64_t *asub,
+                      const void *a, int nprow, int npcol, int myrow, int mycol) {
+    try {
+        switch (dtype) {
+        case SLU_D:
+            refill_values_t<double, dLocalLU_t>((dLUstruct_t *)LU, n, xa, asub, (const double *)a,
+                                                nprow, npcol, myrow, mycol);
+            return 0;
+        case SLU_S:
+            refill_values_t<float, sLocalLU_t>((sLUstruct_t *)LU, n, xa, asub, (const float *)a,
+                                               nprow, npcol, myrow, mycol);
+            return 0;
+        case SLU_Z:
+            refill_values_t<doublecomplex, zLocalLU_t>((zLUstruct_t *)LU, n, xa, asub,
+                                                       (const doublecomplex *)a, nprow, npcol,
+                                                       myrow, mycol);
+            return 0;
+        }
+        throw slu::Error(slu::fmt("refill: bad dtype %d", dtype));
+    } catch (const std::exception &e) {
+        slu::set_last_error(e.what());
+        return -1;
+    }
+}
 
 void *slu_distribute_glu(int dtype, int64_t n, const int_t *xsup, const int_t *supno,
                          const int_t *xlsub, const int_t *lsub, const int_t *xusub,

@@ -123,9 +123,9 @@ def test_reference_driver_default_ordering_through_our_metis(drv, matrix):
 def test_dropin_solve_driver_binds_our_pdgstrs():
     dyn, und, defined = _binding("pddrive_mi355x_solve")
     assert "libslu_mi355x_solve.so" in dyn
-    for sym in ("pdgstrf", "pdgstrs", "pdCompute_Diag_Inv"):
+    for sym in ("pdgstrf", "pdgstrs", "pdCompute_Diag_Inv", "pddistribute"):
         assert sym in und and not re.search(rf"\bT {sym}\b", defined), sym
-    for sym in ("pdgsrfs", "pdgssvx", "pddistribute"):
+    for sym in ("pdgsrfs", "pdgssvx", "symbfact"):
         assert re.search(rf"\bT {sym}\b", defined), sym   # the reference's own
     assert not re.search(r"\bT pdReDistribute_B_to_X\b", defined)  # pdgstrs.o not linked
 
@@ -146,6 +146,29 @@ def test_reference_driver_with_our_factorization_and_solve(drv, matrix, extra, n
           f"{t(ref_out, 'REFINEMENT')} s ({steps(ref_out)} steps) / mi355x {t(out, 'REFINEMENT')} s "
           f"({steps(out)} steps)")
     assert my_err <= max(10 * ref_err, tol), (my_err, ref_err)
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not _have("pddrive3_mi355x_solve", "pddrive3_ref_nd"), reason="drivers not built")
+@pytest.mark.parametrize("nprocs,grid", [(1, ["-r", "1", "-c", "1"]), (4, ["-r", "2", "-c", "2"])])
+@pytest.mark.parametrize("drv", ["pddrive1", "pddrive2", "pddrive3"])
+@pytest.mark.parametrize("matrix", ["big.rua", "g20.rua"])
+def test_reference_reentry_drivers_with_our_distribute_factor_solve(drv, matrix, nprocs, grid):
+    """pdgssvx called again on one LUstruct: pddrive1 (Fact = FACTORED, new
+    right-hand sides on the kept factors), pddrive2 (SamePattern: new
+    distribute), pddrive3 (SamePattern_SameRowPerm: pddistribute's value
+    refill on the existing structure, then the plan cache's refactorization)
+    with pddistribute, pdgstrf and pdgstrs from libslu_mi355x_solve.so."""
+    ref_err, _, ref_out = _run(f"{drv}_ref_nd", nprocs, grid, matrix)
+    my_err, _, out = _run(f"{drv}_mi355x_solve", nprocs, grid, matrix)
+    ref_all = [float(x) for x in re.findall(r"\|\|X-Xtrue\|\|/\|\|X\|\| = ([0-9.eE+-]+)", ref_out)]
+    my_all = [float(x) for x in re.findall(r"\|\|X-Xtrue\|\|/\|\|X\|\| = ([0-9.eE+-]+)", out)]
+    dist = lambda o: re.findall(r"DISTRIBUTE time\s+([0-9.]+)", o)  # noqa: E731
+    print(f"{drv} {matrix} {nprocs} ranks: errors ref {ref_all} mi355x {my_all}; "
+          f"DISTRIBUTE ref {dist(ref_out)} mi355x {dist(out)}")
+    assert len(my_all) == len(ref_all) > 0
+    for m, r in zip(my_all, ref_all):
+        assert m <= max(10 * r, 1e-12), (my_all, ref_all)
 
 
 # ---- 3D (pdgstrf3d, SURVEY 8(f) row 4): the reference's EXAMPLE/pddrive3d.c
