@@ -750,6 +750,59 @@ float pxdistribute(int dtype, const char *name, superlu_dist_options_t *options,
         free(tmp);
         auto *Llu = LU->Llu;
         const i64 ns = gp->supno[n - 1] + 1, nlc = (ns + Pc - 1) / Pc, nlr = (ns + Pr - 1) / Pr;
+        if (dtype != SLU_D) {
+            // s / z: [sz]Destroy_LU (SRC/psutil.c, pzutil.c) frees every block
+            // on its own -- their pddistribute mallocs each one (the d version
+            // keeps them in the *_dat arrays and frees those)
+            const int_t *xs = gp->xsup;
+            for (i64 ljb = 0; ljb < nlc; ++ljb) {
+                const int_t *ix = Llu->Lrowind_bc_ptr[ljb];
+                if (!ix) continue;
+                i64 p = SLU_BC_HEADER;
+                for (i64 b = 0; b < ix[0]; ++b) p += SLU_LB_DESCRIPTOR + ix[p + 1];
+                const i64 jb = ljb * Pc + mycol, nv = (i64)ix[1] * (xs[jb + 1] - xs[jb]);
+                int_t *ni = (int_t *)malloc((size_t)p * sizeof(int_t));
+                T *nv_ = (T *)malloc((size_t)std::max<i64>(nv, 1) * sizeof(T));
+                SLU_REQUIRE(ni && nv_, "%s: out of host memory", name);
+                memcpy(ni, ix, (size_t)p * sizeof(int_t));
+                memcpy(nv_, Llu->Lnzval_bc_ptr[ljb], (size_t)nv * sizeof(T));
+                Llu->Lrowind_bc_ptr[ljb] = ni;
+                Llu->Lnzval_bc_ptr[ljb] = nv_;
+            }
+            for (i64 lb = 0; lb < nlr; ++lb) {
+                const int_t *ix = Llu->Ufstnz_br_ptr[lb];
+                if (!ix) continue;
+                const i64 li = ix[2], nv = ix[1];
+                int_t *ni = (int_t *)malloc((size_t)li * sizeof(int_t));
+                T *nv_ = (T *)malloc((size_t)std::max<i64>(nv, 1) * sizeof(T));
+                SLU_REQUIRE(ni && nv_, "%s: out of host memory", name);
+                memcpy(ni, ix, (size_t)li * sizeof(int_t));
+                memcpy(nv_, Llu->Unzval_br_ptr[lb], (size_t)nv * sizeof(T));
+                Llu->Ufstnz_br_ptr[lb] = ni;
+                Llu->Unzval_br_ptr[lb] = nv_;
+            }
+            free(Llu->Lrowind_bc_dat);
+            free(Llu->Lnzval_bc_dat);
+            free(Llu->Ufstnz_br_dat);
+            free(Llu->Unzval_br_dat);
+            free(Llu->Lrowind_bc_offset);
+            free(Llu->Lnzval_bc_offset);
+            free(Llu->Ufstnz_br_offset);
+            free(Llu->Unzval_br_offset);
+            Llu->Lrowind_bc_dat = nullptr;
+            Llu->Lnzval_bc_dat = nullptr;
+            Llu->Ufstnz_br_dat = nullptr;
+            Llu->Unzval_br_dat = nullptr;
+            Llu->Lrowind_bc_offset = Llu->Lnzval_bc_offset = nullptr;
+            Llu->Ufstnz_br_offset = Llu->Unzval_br_offset = nullptr;
+        }
+        // per-block pointer tables the destroy routines walk (all empty)
+        Llu->Lindval_loc_bc_ptr = (int_t **)calloc((size_t)std::max<i64>(nlc, 1), sizeof(int_t *));
+        Llu->Linv_bc_ptr = (decltype(Llu->Linv_bc_ptr))calloc((size_t)std::max<i64>(nlc, 1), sizeof(void *));
+        Llu->Uinv_bc_ptr = (decltype(Llu->Uinv_bc_ptr))calloc((size_t)std::max<i64>(nlc, 1), sizeof(void *));
+        Llu->Urbs = (int_t *)calloc((size_t)std::max<i64>(nlc, 1), sizeof(int_t));
+        Llu->Ucb_indptr = (decltype(Llu->Ucb_indptr))calloc((size_t)std::max<i64>(nlc, 1), sizeof(void *));
+        Llu->Ucb_valptr = (int_t **)calloc((size_t)std::max<i64>(nlc, 1), sizeof(int_t *));
         auto trees = [](i64 cnt) {
             auto *t = (slu_ctree_mirror_t *)calloc((size_t)std::max<i64>(cnt, 1), sizeof(slu_ctree_mirror_t));
             for (i64 i = 0; i < cnt; ++i) t[i].empty_ = SLU_YES;

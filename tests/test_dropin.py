@@ -151,12 +151,13 @@ def test_reference_driver_with_our_factorization_and_solve(drv, matrix, extra, n
 @pytest.mark.gpu
 @pytest.mark.skipif(not _have("pddrive3_mi355x_solve", "pddrive3_ref_nd"), reason="drivers not built")
 @pytest.mark.parametrize("nprocs,grid", [(1, ["-r", "1", "-c", "1"]), (4, ["-r", "2", "-c", "2"])])
-@pytest.mark.parametrize("drv", ["pddrive1", "pddrive2", "pddrive3"])
+# (EXAMPLE/pddrive2.c, SamePattern, fails with the reference library alone:
+# its second pdgssvx call reports an illegal parameter 5 and aborts)
+@pytest.mark.parametrize("drv", ["pddrive1", "pddrive3"])
 @pytest.mark.parametrize("matrix", ["big.rua", "g20.rua"])
 def test_reference_reentry_drivers_with_our_distribute_factor_solve(drv, matrix, nprocs, grid):
     """pdgssvx called again on one LUstruct: pddrive1 (Fact = FACTORED, new
-    right-hand sides on the kept factors), pddrive2 (SamePattern: new
-    distribute), pddrive3 (SamePattern_SameRowPerm: pddistribute's value
+    right-hand sides on the kept factors), pddrive3 (SamePattern_SameRowPerm: pddistribute's value
     refill on the existing structure, then the plan cache's refactorization)
     with pddistribute, pdgstrf and pdgstrs from libslu_mi355x_solve.so."""
     ref_err, _, ref_out = _run(f"{drv}_ref_nd", nprocs, grid, matrix)
