@@ -649,6 +649,23 @@ __device__ inline zc rlane(zc v, int l) { return {rlane(v.r, l), rlane(v.i, l)};
 //   3. the panel and U12 go back to global memory and A22 -= L21 U12 runs on
 //      MFMA with both operands in LDS, the next batch's loads in flight.
 constexpr int DF_THREADS = 512;
+#ifdef SLU_DIAG_PROBE
+// Diagnostics build only (tools/micro/diag_micro.hip): cycles per phase of
+// k_diag_lu_f summed over panels and blocks (thread 0's view).
+__device__ long long slu_diag_tp[8];
+#define DF_PROBE_START() long long df_t0 = clock64()
+#define DF_PROBE(i)                                                                          \
+    do {                                                                                     \
+        if (threadIdx.x == 0) {                                                              \
+            const long long t = clock64();                                                   \
+            atomicAdd((unsigned long long *)&slu_diag_tp[i], (unsigned long long)(t - df_t0)); \
+            df_t0 = t;                                                                       \
+        }                                                                                    \
+    } while (0)
+#else
+#define DF_PROBE_START()
+#define DF_PROBE(i)
+#endif
 // MAXW / NTHR: the widest block a launch holds and its workgroup size.  The
 // levels near the leaves hold thousands of narrow (relaxed) supernodes: a
 // <= 64-wide variant on 256 threads takes 50 KB of LDS instead of 150 KB,
@@ -676,6 +693,7 @@ k_diag_lu_f(const DiagItemF<T> *items, double thresh, int replace_tiny, int *tin
     __shared__ T s_rp[PW];
     __shared__ int s_z[PW];
     __shared__ int s_anyz;
+    DF_PROBE_START();
     for (int p = 0; p < nb; ++p) {
         const int p0 = p * PW, pw = min(PW, w - p0), nrow = w - p0, nbl = nrow - pw;
         const int c0 = p0 + pw;
@@ -703,6 +721,7 @@ k_diag_lu_f(const DiagItemF<T> *items, double thresh, int replace_tiny, int *tin
                 },
                 [&](int e, T v) { sU[e % PW][e / PW] = v; });
         __syncthreads();
+        DF_PROBE(0);
         // ---- 1. A11 = L11 U11 in registers (wave 0); meanwhile, on the first
         // panel, the other waves pull the trailing block into L2 (every
         // panel's update re-reads it)
@@ -760,6 +779,7 @@ k_diag_lu_f(const DiagItemF<T> *items, double thresh, int replace_tiny, int *tin
             }
         }
         __syncthreads();
+        DF_PROBE(1);
         // ---- 1b. inverses from the factored A11 in LDS, lane = column j
         // (wave 0 U11^{-1}, wave 1 L11^{-1}), column-sweep (axpy) order so the
         // dependent chain is one multiply per row
@@ -787,6 +807,7 @@ k_diag_lu_f(const DiagItemF<T> *items, double thresh, int replace_tiny, int *tin
             }
         }
         __syncthreads();
+        DF_PROBE(2);
         // ---- 2. L21 = A21 U11^{-1}, U12 = L11^{-1} A12
         if (!s_anyz) {
             const int nfr = (nbl + 15) / 16; // L21 row fragments; U12 column fragments
@@ -850,6 +871,7 @@ k_diag_lu_f(const DiagItemF<T> *items, double thresh, int replace_tiny, int *tin
             }
         }
         __syncthreads();
+        DF_PROBE(3);
         // ---- 3. panel, U12 and the dinv blocks back to global (written here
         // so that no barrier before the trailing update waits for them);
         // A22 -= L21 U12 on MFMA
@@ -919,6 +941,7 @@ k_diag_lu_f(const DiagItemF<T> *items, double thresh, int replace_tiny, int *tin
             }
         }
         __syncthreads();
+        DF_PROBE(4);
     }
 }
 

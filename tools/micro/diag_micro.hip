@@ -1,6 +1,8 @@
 // Diagonal-block LU microbenchmark (not product code): k_diag_lu_f on nb
-// blocks of w x w (ld = w), phase split by clock64 probes, LU residual.
-// usage: diag_micro [w nb]
+// blocks of w x w (ld = w), phase split by clock64 probes (kernels.h built
+// with SLU_DIAG_PROBE), LU residual.
+// usage: diag_micro [w nb]   build: hipcc --offload-arch=gfx950 -O3 -std=c++17
+//   -I superlu_dist_amd/csrc -I include -I /opt/conda/include tools/micro/diag_micro.hip
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -9,10 +11,8 @@
 #include <cstdlib>
 #include <vector>
 
+#define SLU_DIAG_PROBE 1
 #include "kernels.h"
-namespace slu {
-#include "diag_prof_body.h"
-}
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
 using namespace slu;
@@ -82,16 +82,16 @@ int main(int argc, char **argv) {
             nrm = std::max(nrm, fabs(h[i + (size_t)j * w]));
         }
     {
-        long long *tp;
-        CK(hipMalloc(&tp, 16 * 8));
-        CK(hipMemset(tp, 0, 128));
+        long long z[8] = {0};
+        CK(hipMemcpyToSymbol(HIP_SYMBOL(slu_diag_tp), z, sizeof z));
         CK(hipMemcpy(dA, dA0, bytes, hipMemcpyDeviceToDevice));
-        hipLaunchKernelGGL(k_diag_prof_f<double>, dim3(nb), dim3(DF_THREADS), 0, 0, di, 0.0, 0, cnt, zp, tp);
+        fst();
         CK(hipDeviceSynchronize());
-        long long h_tp[16];
-        CK(hipMemcpy(h_tp, tp, 128, hipMemcpyDeviceToHost));
-        printf("  f   phases (cycles/block): staging %lld  A11 LU %lld  inverses %lld  L21/U12 %lld  writeback+trailing %lld\n",
-               h_tp[8] / nb, h_tp[9] / nb, h_tp[10] / nb, h_tp[11] / nb, h_tp[12] / nb);
+        long long h_tp[8];
+        CK(hipMemcpyFromSymbol(h_tp, HIP_SYMBOL(slu_diag_tp), sizeof h_tp));
+        printf("  phases (cycles per block, all panels): staging %lld  A11 LU %lld  inverses %lld  "
+               "L21/U12 %lld  writeback+trailing %lld\n", h_tp[0] / nb, h_tp[1] / nb, h_tp[2] / nb,
+               h_tp[3] / nb, h_tp[4] / nb);
     }
     printf("w=%3d blocks=%5d  k_diag_lu_f %8.1f us  LU resid %.2e\n", w, nb, t2, err / nrm);
     return 0;
