@@ -901,7 +901,10 @@ k_diag_lu_f(const DiagItemF<T> *items, double thresh, int replace_tiny, int *tin
                     const int f = f0 + q, fr = f % nf, fc = f / nf;
 #pragma unroll
                     for (int i = 0; i < 4; ++i) {
-                        const int r = fr * 16 + M::row(lane, i), c = fc * 16 + (lane & 15);
+                        // transposed fragment (operands swapped below): lane
+                        // l&15 holds row fr*16 + (l&15) -- 16 consecutive rows
+                        // of 4 columns per load, 4 cache lines instead of 16
+                        const int r = fr * 16 + (lane & 15), c = fc * 16 + M::row(lane, i);
                         // unconditional load from a clamped address + branch-free
                         // mask: the next batch's loads stay ahead of the MFMAs
                         const bool ok = (f < nff) & (r < nbl) & (c < nbl);
@@ -914,24 +917,35 @@ k_diag_lu_f(const DiagItemF<T> *items, double thresh, int replace_tiny, int *tin
             for (; f0 < nff; f0 += NW * FB) {
                 const int f1 = f0 + NW * FB;
                 if (f1 < nff) cload(cn, f1);
+                // the FB fragments' accumulation chains interleaved (one
+                // dependent MFMA chain per fragment would wait out the MFMA
+                // and LDS latencies at every k step)
+                typename M::acc_t acc[FB];
+#pragma unroll
+                for (int q = 0; q < FB; ++q) acc[q] = M::zero();
+#pragma unroll
+                for (int ks = 0; ks < PW; ks += M::KSTEP) {
+                    const int k = ks + (lane >> 4);
+                    T av[FB], bv[FB];
+#pragma unroll
+                    for (int q = 0; q < FB; ++q) {
+                        const int f = f0 + q, fr = f % nf, fc = f / nf;
+                        const int r = fr * 16 + (lane & 15), c = fc * 16 + (lane & 15);
+                        av[q] = keep_if(r < nbl, sP[pw + min(r, nbl - 1)][k]);
+                        bv[q] = keep_if(c < nbl, sU[k][min(c, nbl - 1)]);
+                    }
+#pragma unroll
+                    for (int q = 0; q < FB; ++q) M::step(acc[q], bv[q], av[q]); // C^T = U12^T L21^T
+                }
 #pragma unroll
                 for (int q = 0; q < FB; ++q) {
                     const int f = f0 + q, fr = f % nf, fc = f / nf;
-                    typename M::acc_t acc = M::zero();
-                    const int r = fr * 16 + (lane & 15), c = fc * 16 + (lane & 15);
-#pragma unroll
-                    for (int ks = 0; ks < PW; ks += M::KSTEP) {
-                        const int k = ks + (lane >> 4);
-                        const T av = (r < nbl) ? sP[pw + r][k] : Sx::zero();
-                        const T bv = (c < nbl) ? sU[k][c] : Sx::zero();
-                        M::step(acc, av, bv);
-                    }
 #pragma unroll
                     for (int i = 0; i < 4; ++i) {
-                        const int rr = fr * 16 + M::row(lane, i), cc = fc * 16 + (lane & 15);
+                        const int rr = fr * 16 + (lane & 15), cc = fc * 16 + M::row(lane, i);
                         if (f < nff && rr < nbl && cc < nbl)
                             A22[rr + (int64_t)cc * ld] =
-                                Sx::fms(cv[q][i], M::get(acc, i), one_of(cv[q][i]));
+                                Sx::fms(cv[q][i], M::get(acc[q], i), one_of(cv[q][i]));
                     }
                 }
 #pragma unroll
