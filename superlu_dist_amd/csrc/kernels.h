@@ -893,7 +893,7 @@ k_diag_lu_f(const DiagItemF<T> *items, double thresh, int replace_tiny, int *tin
             // batch's C loads are issued before this batch's MFMAs
             const int nf = (nbl + 15) / 16, nff = nf * nf;
             T *A22 = A + c0 + (int64_t)c0 * ld;
-            constexpr int FB = 4;
+            constexpr int FB = sizeof(T) == 16 ? 2 : 4; // complex: fewer live accumulators
             T cv[FB][4], cn[FB][4];
             auto cload = [&](T (&dst)[FB][4], int f0) {
 #pragma unroll
