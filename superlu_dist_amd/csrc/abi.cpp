@@ -229,9 +229,30 @@ struct CachedPlan {
     uint64_t digest = 0;
     int dtype = -1, n = -1, replace_tiny = -1;
     const void *lu = nullptr; // the LUstruct the cached factors belong to (pdgstrs)
+    bool a_pattern = false;   // the plan holds DevA's pattern (fill_a ready)
+    bool host_factors = true; // the host L / U arrays hold these factors
 };
 CachedPlan g_cache;
 std::mutex g_cache_mu;
+
+// A in the LUstruct's coordinates (CSC), kept by this library's pddistribute
+// for the pdgstrf that follows: the factor storage is then built on the
+// device (zero + scatter of A's nnz values, the plan's fill_a) instead of
+// copying the distributed L / U values over PCIe, and on a 1x1 grid the
+// factors stay in HBM for this library's pdgstrs (the host L / U arrays keep
+// A's values unless SUPERLU_MI355X_HOST_FACTORS=1).  Keyed by the LUstruct
+// and its index tables, so an LUstruct distributed elsewhere never matches.
+struct DevA {
+    const void *lu = nullptr, *llu = nullptr, *lrow = nullptr;
+    int dtype = -1;
+    int64_t n = 0;
+    std::vector<int64_t> xa, asub;
+    std::vector<char> a; // nnz values of the dtype
+    uint64_t gen = 0;    // bumps with every refill (SamePattern_SameRowPerm)
+};
+DevA g_deva;
+std::mutex g_deva_mu;
+uint64_t g_deva_gen = 0;
 
 inline uint64_t mix(uint64_t h, uint64_t v) {
     h ^= v + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2);
@@ -304,6 +325,21 @@ int_t pxgstrf(int dtype, const char *name, superlu_dist_options_t *options, int 
                 g_cache.plan = nullptr;
             }
         }
+        // built by this library's pddistribute: A is at hand for a device fill
+        DevA *da = nullptr;
+        {
+            std::lock_guard<std::mutex> lk(g_deva_mu);
+            if (g_deva.lu == LUstruct && g_deva.llu == LUstruct->Llu &&
+                g_deva.lrow == LUstruct->Llu->Lrowind_bc_ptr && g_deva.dtype == dtype && g_deva.n == n)
+                da = &g_deva;
+        }
+        const char *hf = getenv("SUPERLU_MI355X_HOST_FACTORS");
+        const bool keep_on_device = da && cache && !(hf && atoi(hf) == 1);
+        bool pattern_ready = false;
+        if (plan) {
+            std::lock_guard<std::mutex> lk(g_cache_mu);
+            pattern_ready = g_cache.a_pattern;
+        }
         if (!plan) {
             reap_join(); // the previous call's device memory is free again
             slu_comm *c = comm_for_grid(grid);
@@ -312,18 +348,29 @@ int_t pxgstrf(int dtype, const char *name, superlu_dist_options_t *options, int 
             // utime[FACT] (SRC/pdgssvx.c:1174-1180) covers the copies too: the
             // H2D of the values runs beside the plan build, and each level's
             // finished factors go back to the host arrays while later levels
-            // are factored (SUPERLU_MI355X_OVERLAP=0 turns both off)
+            // are factored (SUPERLU_MI355X_OVERLAP=0 turns both off).  With A
+            // at hand nothing but A goes up, and on 1x1 nothing comes down.
             const char *ov = getenv("SUPERLU_MI355X_OVERLAP");
-            eo.overlap_upload = eo.overlap_download = !(ov && !strcmp(ov, "0"));
+            const bool ovl = !(ov && !strcmp(ov, "0"));
+            eo.overlap_upload = ovl && !da;
+            eo.overlap_download = ovl && !keep_on_device;
             char err[512] = {0};
             plan = slu_plan_create(dtype, LUstruct, n, (int)grid->nprow, (int)grid->npcol,
                                    grid->iam, c, &eo, err, sizeof err);
             if (!plan) throw slu::Error(err);
         }
         int myinfo = 0, tiny = 0;
-        if (slu_plan_upload(plan) || slu_plan_factor(plan, anorm, &myinfo, &tiny) ||
-            slu_plan_download(plan))
+        if (da) {
+            if (!pattern_ready &&
+                slu_plan_set_a_pattern(plan, n, da->xa.data(), da->asub.data()))
+                throw slu::Error(slu_last_error());
+            pattern_ready = true;
+            if (slu_plan_fill_a(plan, da->a.data(), 0)) throw slu::Error(slu_last_error());
+        } else if (slu_plan_upload(plan)) {
             throw slu::Error(slu_last_error());
+        }
+        if (slu_plan_factor(plan, anorm, &myinfo, &tiny)) throw slu::Error(slu_last_error());
+        if (!keep_on_device && slu_plan_download(plan)) throw slu::Error(slu_last_error());
         slu_plan_stats st;
         slu_plan_get_stats(plan, &st);
         stat->ops[SLU_PHASE_FACT] = (float)(st.schur_flops + st.panel_flops);
@@ -337,6 +384,8 @@ int_t pxgstrf(int dtype, const char *name, superlu_dist_options_t *options, int 
             g_cache.n = n;
             g_cache.replace_tiny = rt;
             g_cache.lu = LUstruct;
+            g_cache.a_pattern = pattern_ready;
+            g_cache.host_factors = !keep_on_device;
         } else {
             reap_later(plan);
         }
@@ -730,10 +779,23 @@ float pxdistribute(int dtype, const char *name, superlu_dist_options_t *options,
                 aval[q] = vv[e];
             }
         }
+        auto stash = [&] { // A for the device fill of the following pdgstrf
+            std::lock_guard<std::mutex> lk(g_deva_mu);
+            g_deva.lu = LU;
+            g_deva.llu = LU->Llu;
+            g_deva.lrow = LU->Llu->Lrowind_bc_ptr;
+            g_deva.dtype = dtype;
+            g_deva.n = n;
+            g_deva.xa = xa;
+            g_deva.asub = asub;
+            g_deva.a.assign((const char *)aval.data(), (const char *)(aval.data() + aval.size()));
+            g_deva.gen = ++g_deva_gen;
+        };
         if (options->Fact == 2 /* SamePattern_SameRowPerm */) {
             if (slu_refill_values(dtype, LU, n, xa.data(), asub.data(), aval.data(), Pr, Pc, myrow,
                                   mycol))
                 throw slu::Error(slu_last_error());
+            stash();
             return 0.0f;
         }
         // ---- first-time branch: the restated structural distribute
@@ -825,6 +887,7 @@ float pxdistribute(int dtype, const char *name, superlu_dist_options_t *options,
             Llu->ilsum[lb + 1] = Llu->ilsum[lb] + (gb < ns ? gp->xsup[gb + 1] - gp->xsup[gb] : 0);
         }
         Llu->ldalsum = Llu->ilsum[nlr];
+        stash();
         return (float)((double)Llu->Lnzval_bc_cnt * sizeof(T) + (double)Llu->Unzval_br_cnt * sizeof(T) +
                        (double)(Llu->Lrowind_bc_cnt + Llu->Ufstnz_br_cnt) * sizeof(int_t));
     } catch (const std::exception &e) {
