@@ -307,6 +307,12 @@ int_t pxgstrf(int dtype, const char *name, superlu_dist_options_t *options, int 
     stat->current_buffer = stat->peak_buffer = stat->gpu_buffer = 0.0f;
     stat->num_look_aheads = std::max(0, std::min(options->num_lookaheads, SLU_MAX_LOOKAHEADS - 1));
     slu_plan *plan = nullptr;
+    // SUPERLU_MI355X_TIMING=1: wall-clock breakdown of the call on stderr
+    const char *tm = getenv("SUPERLU_MI355X_TIMING");
+    const bool timing = tm && atoi(tm) == 1;
+    using clk = std::chrono::steady_clock;
+    clk::time_point tp[6];
+    tp[0] = clk::now();
     try {
         const bool one = grid->nprow * grid->npcol == 1;
         const char *pc = getenv("SUPERLU_MI355X_PLAN_CACHE");
@@ -336,6 +342,8 @@ int_t pxgstrf(int dtype, const char *name, superlu_dist_options_t *options, int 
         const char *hf = getenv("SUPERLU_MI355X_HOST_FACTORS");
         const bool keep_on_device = da && cache && !(hf && atoi(hf) == 1);
         bool pattern_ready = false;
+        const bool reused = plan != nullptr;
+        tp[1] = clk::now();
         if (plan) {
             std::lock_guard<std::mutex> lk(g_cache_mu);
             pattern_ready = g_cache.a_pattern;
@@ -360,6 +368,7 @@ int_t pxgstrf(int dtype, const char *name, superlu_dist_options_t *options, int 
             if (!plan) throw slu::Error(err);
         }
         int myinfo = 0, tiny = 0;
+        tp[2] = clk::now();
         if (da) {
             if (!pattern_ready &&
                 slu_plan_set_a_pattern(plan, n, da->xa.data(), da->asub.data()))
@@ -369,10 +378,26 @@ int_t pxgstrf(int dtype, const char *name, superlu_dist_options_t *options, int 
         } else if (slu_plan_upload(plan)) {
             throw slu::Error(slu_last_error());
         }
+        tp[3] = clk::now();
         if (slu_plan_factor(plan, anorm, &myinfo, &tiny)) throw slu::Error(slu_last_error());
+        tp[4] = clk::now();
         if (!keep_on_device && slu_plan_download(plan)) throw slu::Error(slu_last_error());
+        tp[5] = clk::now();
         slu_plan_stats st;
         slu_plan_get_stats(plan, &st);
+        if (timing) {
+            auto ms = [&](int a, int b) {
+                return std::chrono::duration<double, std::milli>(tp[b] - tp[a]).count();
+            };
+            fprintf(stderr,
+                    "[%s rank %d] digest %.1f ms, plan %s %.1f ms (amalg %.1f), %s %.1f ms "
+                    "(device fill %.1f, upload wait %.1f), factor %.1f ms (device %.1f), "
+                    "download %.1f ms (tail %.1f)%s\n",
+                    name, (int)grid->iam, ms(0, 1), reused ? "reused" : "built", ms(1, 2),
+                    st.t_amalg_ms, da ? "fill_a" : "upload", ms(2, 3), st.t_fill_ms,
+                    st.t_upload_wait_ms, ms(3, 4), st.t_total_ms, ms(4, 5), st.t_d2h_tail_ms,
+                    keep_on_device ? " [factors kept in HBM]" : "");
+        }
         stat->ops[SLU_PHASE_FACT] = (float)(st.schur_flops + st.panel_flops);
         stat->TinyPivots += tiny;
         stat->gpu_buffer = (float)(st.lu_bytes + st.index_bytes);

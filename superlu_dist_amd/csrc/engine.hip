@@ -3410,11 +3410,13 @@ struct Plan : PlanBase {
         const int_t *supno = LU->Glu_persist->supno;
         const i64 nnz = xa[n];
         vector<i64> map((size_t)nnz, -1);
-        vector<std::pair<i64, i64>> col; // (destination, nonzero) of one column
-        for (int j = 0; j < n; ++j) {
+        // columns on the host threads: each nonzero belongs to one column, so
+        // the writes to map are disjoint
+        parallel_for(n, [&](int j) {
+            thread_local vector<std::pair<i64, i64>> col; // (destination, nonzero) of one column
             const int jb = (int)supno[j];
             SLU_REQUIRE(xa[j + 1] >= xa[j], "A: column pointers decrease at %d", j);
-            if (jb % Pc != mycol) continue;
+            if (jb % Pc != mycol) return;
             const int jc = (int)(j - xsup[jb]);
             col.clear();
             for (i64 e = xa[j]; e < xa[j + 1]; ++e) {
@@ -3445,7 +3447,7 @@ struct Plan : PlanBase {
             for (size_t i = 0; i < col.size(); ++i)
                 if (i + 1 == col.size() || col[i + 1].first != col[i].first)
                     map[col[i].second] = col[i].first;
-        }
+        }, 512);
         d_amap.upload(map.empty() ? vector<i64>(1, -1) : map);
         d_aval.alloc(std::max<i64>(nnz, 1));
         a_nnz = nnz;
