@@ -362,6 +362,7 @@ int_t pxgstrf(int dtype, const char *name, superlu_dist_options_t *options, int 
             const bool ovl = !(ov && !strcmp(ov, "0"));
             eo.overlap_upload = ovl && !da;
             eo.overlap_download = ovl && !keep_on_device;
+            eo.timing = timing; // device-time breakdown for SUPERLU_MI355X_TIMING
             char err[512] = {0};
             plan = slu_plan_create(dtype, LUstruct, n, (int)grid->nprow, (int)grid->npcol,
                                    grid->iam, c, &eo, err, sizeof err);
@@ -391,11 +392,12 @@ int_t pxgstrf(int dtype, const char *name, superlu_dist_options_t *options, int 
             };
             fprintf(stderr,
                     "[%s rank %d] digest %.1f ms, plan %s %.1f ms (amalg %.1f), %s %.1f ms "
-                    "(device fill %.1f, upload wait %.1f), factor %.1f ms (device %.1f), "
-                    "download %.1f ms (tail %.1f)%s\n",
+                    "(device fill %.1f, upload wait %.1f), factor %.1f ms (device %.1f: diag %.1f, "
+                    "trsm %.1f, schur %.1f), download %.1f ms (tail %.1f)%s\n",
                     name, (int)grid->iam, ms(0, 1), reused ? "reused" : "built", ms(1, 2),
                     st.t_amalg_ms, da ? "fill_a" : "upload", ms(2, 3), st.t_fill_ms,
-                    st.t_upload_wait_ms, ms(3, 4), st.t_total_ms, ms(4, 5), st.t_d2h_tail_ms,
+                    st.t_upload_wait_ms, ms(3, 4), st.t_total_ms, st.t_diag_ms, st.t_trsm_ms,
+                    st.t_schur_ms, ms(4, 5), st.t_d2h_tail_ms,
                     keep_on_device ? " [factors kept in HBM]" : "");
         }
         stat->ops[SLU_PHASE_FACT] = (float)(st.schur_flops + st.panel_flops);

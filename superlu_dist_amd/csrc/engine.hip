@@ -73,20 +73,31 @@ template <typename T> struct RawVec {
 
 template <typename T> struct DevBuf {
     T *p = nullptr;
-    size_t n = 0;
+    size_t n = 0, guard = 0;
     DevBuf() = default;
     DevBuf(const DevBuf &) = delete;
     DevBuf &operator=(const DevBuf &) = delete;
     ~DevBuf() { release(); }
     void release() {
-        if (p) (void)hipFree(p);
+        if (p) (void)hipFree(p - guard);
         p = nullptr;
-        n = 0;
+        n = guard = 0;
     }
     void alloc(size_t cnt) {
         release();
         n = cnt;
         if (cnt) HIPCHK(hipMalloc(&p, cnt * sizeof(T)));
+    }
+    // cnt elements with g more allocated on either side: a kernel may read
+    // (and mask) up to g elements outside [p, p + cnt) without a clamp
+    void alloc_guarded(size_t cnt, size_t g) {
+        release();
+        HIPCHK(hipMalloc(&p, (cnt + 2 * g) * sizeof(T)));
+        HIPCHK(hipMemset(p, 0, g * sizeof(T)));
+        HIPCHK(hipMemset(p + g + cnt, 0, g * sizeof(T)));
+        p += g;
+        n = cnt;
+        guard = g;
     }
     void upload(const vector<T> &v) { upload(v.data(), v.size()); }
     void upload(const RawVec<T> &v) { upload(v.data(), v.size()); }
@@ -601,7 +612,7 @@ struct Plan : PlanBase {
         tprev = t0;
         value_layout();
         d_L.alloc(std::max<i64>(lval_total, 1));
-        d_U.alloc(std::max<i64>(uval_total, 1));
+        d_U.alloc_guarded(std::max<i64>(uval_total, 1), SB_UGUARD);
         tick("layout + alloc");
         if (opts.overlap_upload) {
             // the H2D copy of the values runs beside the rest of the plan
@@ -1684,7 +1695,7 @@ struct Plan : PlanBase {
     void build_schedule() {
         // value buffers first: work items point straight into them
         d_dpk.alloc(std::max<i64>(dpk_total, 1));
-        d_pan.alloc(std::max<i64>(pan_total, 1));
+        d_pan.alloc_guarded(std::max<i64>(pan_total, 1), SB_UGUARD);
         d_dinv.alloc(std::max<i64>(dscr_max, 1));
         vector<int> owner(lblk.size() + ublk.size(), -1), touched;
         for (size_t L = 0; L < levels.size(); ++L) {

@@ -16,6 +16,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "slu_abi.h"
 
 namespace slu {
@@ -133,6 +135,14 @@ template <> __device__ __forceinline__ zc gld<zc>(const zc *p) {
     typedef double d2 __attribute__((ext_vector_type(2)));
     const d2 v = *(const __attribute__((address_space(1))) d2 *)p; // one 16-byte load
     return {v.x, v.y};
+}
+// Four consecutive elements through 16-byte global loads from an address
+// that is only element-aligned (gfx950 global loads need dword alignment).
+typedef double d2u8 __attribute__((ext_vector_type(2), aligned(8)));
+__device__ __forceinline__ void gld4(const double *p, double (&r)[4]) {
+    const auto *q = (const __attribute__((address_space(1))) d2u8 *)p;
+    const d2u8 a = q[0], b = q[1];
+    r[0] = a.x; r[1] = a.y; r[2] = b.x; r[3] = b.y;
 }
 
 // ------------------------------------------------------------ MFMA
@@ -1329,6 +1339,11 @@ k_trsm_blk(const TrsmItemF<T> *items) {
 // MFMAs per stage and LDS per workgroup as the real tile, at twice the
 // MFMAs per LDS operand; the epilogue stages 16 columns per pass.
 constexpr int SB_BM = 128;
+// Elements allocated on either side of the U value and panel buffers
+// (DevBuf::alloc_guarded): k_schur_big's B loads read a column's 4
+// consecutive k without clamping them to its segment (the mask drops what
+// lies outside), i.e. up to the panel width before a segment and 15 past it.
+constexpr size_t SB_UGUARD = 1024;
 // THREADS / WN: workgroup size and waves along N; MINW: waves per SIMD the
 // register budget must allow (workgroups per CU x waves per workgroup / 4).
 template <typename T> struct BigCfg {
@@ -1458,6 +1473,13 @@ k_schur_big(const TileItem *tiles, const KInfo<T> *kinfo, T *Lval, T *Uval,
         for (int s = 0; s < AE; ++s) {
             const int kk = k0 + ak + (SB_THREADS / SB_BM) * s;
             ra[s] = gld(ap + (int64_t)(ki.kmin + min(kk, ki.kw - 1)) * ki.lda);
+        }
+        // a column's 4 consecutive k through 16-byte loads, unclamped (the
+        // buffers carry SB_UGUARD guards; 315.2 -> 310.7 ms at 100^3, Schur
+        // 56.3 -> 57.0 %, and no spilled VGPRs, profiles/r03w_ab)
+        if constexpr (BE == 4 && std::is_same<T, double>::value) { // (fp32: more spills)
+            gld4(ub + ki.kmin + k0 + bk, rb);
+            return;
         }
 #pragma unroll
         for (int s = 0; s < BE; ++s) {

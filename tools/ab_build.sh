@@ -1,6 +1,8 @@
 #!/bin/bash
-# Builds libslu_mi355x.so variants with extra compile flags into ablib/NAME/
-# for A/B runs (bench.py / tests pick one with SLU_LIB=ablib/NAME/libslu_mi355x.so).
+# Builds libslu_mi355x_full.so variants with extra compile flags into
+# ablib/NAME/ for A/B runs (bench.py / tests pick one with
+# SLU_LIB=ablib/NAME/libslu_mi355x_full.so).  Host objects come from the
+# product build (superlu_dist_amd/lib/obj); only engine.hip is recompiled.
 # usage: bash tools/ab_build.sh NAME "-DFLAG=..."
 set -e
 NAME=$1; FLAGS=$2
@@ -8,9 +10,13 @@ ROOT=$(cd $(dirname $0)/.. && pwd)
 OUT=$ROOT/ablib/$NAME
 mkdir -p $OUT/obj
 cd $ROOT/superlu_dist_amd/csrc
+make -s -j8 >/dev/null
 INC="-I../../include -I/opt/conda/include -I."
-g++ -O3 -fPIC -std=c++17 $INC -I/opt/rocm/include -D__HIP_PLATFORM_AMD__ -c frontend.cpp -o $OUT/obj/frontend.o
-g++ -O3 -fPIC -std=c++17 $INC -I/opt/rocm/include -D__HIP_PLATFORM_AMD__ -c abi.cpp -o $OUT/obj/abi.o
-/opt/rocm/bin/hipcc -O3 -fPIC -std=c++17 --offload-arch=gfx950 -munsafe-fp-atomics $INC -Wno-unused-result $FLAGS -c engine.hip -o $OUT/obj/engine.o
-/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o $OUT/libslu_mi355x.so $OUT/obj/*.o -L/opt/rocm/lib -lamdhip64 -lrccl -ldl -Wl,-rpath,/opt/rocm/lib
-echo built $OUT/libslu_mi355x.so
+/opt/rocm/bin/hipcc -O3 -gline-tables-only -fPIC -std=c++17 --offload-arch=gfx950 -munsafe-fp-atomics \
+    $INC -Wno-unused-result $FLAGS -c engine.hip -o $OUT/obj/engine.o
+HOST=""
+for o in abi amalg distribute frontend symbolic ordering amalg_api; do HOST="$HOST ../lib/obj/$o.o"; done
+/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -Wl,--version-script=full.map \
+    -o $OUT/libslu_mi355x_full.so $HOST $OUT/obj/engine.o -L/opt/rocm/lib -lamdhip64 -lrccl -ldl \
+    -Wl,-rpath,/opt/rocm/lib
+echo built $OUT/libslu_mi355x_full.so
