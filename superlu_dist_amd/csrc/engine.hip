@@ -611,7 +611,7 @@ struct Plan : PlanBase {
         prof = getenv("SLU_PROFILE_PLAN") != nullptr;
         tprev = t0;
         value_layout();
-        d_L.alloc(std::max<i64>(lval_total, 1));
+        d_L.alloc_guarded(std::max<i64>(lval_total, 1), SB_UGUARD);
         d_U.alloc_guarded(std::max<i64>(uval_total, 1), SB_UGUARD);
         tick("layout + alloc");
         if (opts.overlap_upload) {
@@ -3588,8 +3588,11 @@ struct AmalgPlan : PlanBase {
             P->usrc[s + 1] = uv;
         }
         HIPCHK(hipSetDevice(0));
-        P->d_oL.alloc(std::max<i64>(lv, 1));
-        P->d_oU.alloc(std::max<i64>(uv, 1));
+        P->o_lv = lv;
+        P->o_uv = uv;
+        // the caller-layout copies only where values cross PCIe: a plan fed
+        // by fill_a and read by solve never allocates them
+        if (P->opts.overlap_upload || P->opts.overlap_download) P->ensure_o();
         if (P->opts.overlap_upload) {
             AmalgPlan *raw = P.get();
             P->up_thread = std::thread([raw] {
@@ -3792,8 +3795,15 @@ struct AmalgPlan : PlanBase {
         P.opts.overlap_download = 1;
     }
 
+    i64 o_lv = 0, o_uv = 0;
+    void ensure_o() {
+        if (d_oL.p) return;
+        d_oL.alloc(std::max<i64>(o_lv, 1));
+        d_oU.alloc(std::max<i64>(o_uv, 1));
+    }
     // caller layout: host arrays <-> d_oL / d_oU
     vector<Xfer> xfers() {
+        ensure_o();
         LocalLU *L = LU->Llu;
         vector<Xfer> xs;
         const int_t *xsup = LU->Glu_persist->xsup;
@@ -3820,6 +3830,7 @@ struct AmalgPlan : PlanBase {
     }
 
     void relayout(int dir) {
+        ensure_o();
         hipStream_t st = in->stream;
         if (dir == 0) {
             HIPCHK(hipMemsetAsync(in->d_L.p, 0, in->d_L.bytes(), st));

@@ -139,6 +139,13 @@ template <> __device__ __forceinline__ zc gld<zc>(const zc *p) {
 // Four consecutive elements through 16-byte global loads from an address
 // that is only element-aligned (gfx950 global loads need dword alignment).
 typedef double d2u8 __attribute__((ext_vector_type(2), aligned(8)));
+__device__ __forceinline__ void gld2(const double *p, double &x, double &y) {
+    const d2u8 a = *(const __attribute__((address_space(1))) d2u8 *)p;
+    x = a.x;
+    y = a.y;
+}
+__device__ __forceinline__ void gld2(const float *, float &, float &) {}
+__device__ __forceinline__ void gld2(const zc *, zc &, zc &) {}
 __device__ __forceinline__ void gld4(const double *p, double (&r)[4]) {
     const auto *q = (const __attribute__((address_space(1))) d2u8 *)p;
     const d2u8 a = q[0], b = q[1];
@@ -1340,9 +1347,10 @@ k_trsm_blk(const TrsmItemF<T> *items) {
 // MFMAs per LDS operand; the epilogue stages 16 columns per pass.
 constexpr int SB_BM = 128;
 // Elements allocated on either side of the U value and panel buffers
-// (DevBuf::alloc_guarded): k_schur_big's B loads read a column's 4
-// consecutive k without clamping them to its segment (the mask drops what
-// lies outside), i.e. up to the panel width before a segment and 15 past it.
+// (DevBuf::alloc_guarded; the L values too): k_schur_big's B loads read a
+// column's 4 consecutive k without clamping them to its segment (the mask
+// drops what lies outside), i.e. up to the panel width before a segment and
+// 15 past it; the A loads (SLU_SB_A16) read up to 127 rows past a column.
 constexpr size_t SB_UGUARD = 1024;
 // THREADS / WN: workgroup size and waves along N; MINW: waves per SIMD the
 // register budget must allow (workgroups per CU x waves per workgroup / 4).
@@ -1409,7 +1417,7 @@ k_schur_big(const TileItem *tiles, const KInfo<T> *kinfo, T *Lval, T *Uval,
     // the epilogue tables go in the stage buffers' tail past the C staging
     // where it is large enough, else in arrays of their own
     constexpr bool TAIL = (2 * STAGE - PASSW * CLD) * (int)sizeof(T) >= CPN * 8 + RLN * 4;
-    __shared__ T smem[2 * STAGE];
+    __shared__ __attribute__((aligned(16))) T smem[2 * STAGE];
     __shared__ int s_rg[SB_BM], s_ra[SB_BM], s_cg[SB_BN], s_cb[SB_BN];
     __shared__ int64_t s_db[SB_TB * SB_TB], s_dmb[SB_TB * SB_TB]; // destination records
     __shared__ int s_dld[SB_TB * SB_TB];                          // ld (L) or -1 (U)
@@ -1455,9 +1463,16 @@ k_schur_big(const TileItem *tiles, const KInfo<T> *kinfo, T *Lval, T *Uval,
     // A: thread owns row ar and k = ak + 4s (s < 4); B: column bc, k = bk..bk+3.
     // Loads are unconditional from clamped in-bounds addresses; out-of-range
     // elements are zeroed afterwards (no per-element branches).
-    const int ar = tid & (SB_BM - 1), ak = tid / SB_BM;
+#ifdef SLU_SB_A16
+    // fp64: thread owns rows ar, ar + 1 and k = ak + 8s (s < 2): one 16-byte
+    // load per k along the column, unclamped rows (guarded L / panel buffers)
+    constexpr bool A16 = AE == 4 && std::is_same<T, double>::value;
+#else
+    constexpr bool A16 = false;
+#endif
+    const int ar = A16 ? 2 * (tid & 63) : tid & (SB_BM - 1), ak = A16 ? tid >> 6 : tid / SB_BM;
     const bool avalid = ar < mrows;
-    const T *ap = ki.a + row0 + (avalid ? ar : 0);
+    const T *ap = ki.a + row0 + (A16 || avalid ? ar : 0);
     const int bc = tid / (SB_BK / BE), bk = (tid % (SB_BK / BE)) * BE;
     const bool bvalid = bc < ncols;
     const int bcc = col0 + (bvalid ? bc : 0);
@@ -1469,6 +1484,13 @@ k_schur_big(const TileItem *tiles, const KInfo<T> *kinfo, T *Lval, T *Uval,
     // before them.
     T ra[AE], rb[BE];
     auto gload = [&](int k0) {
+        if constexpr (A16) {
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                const int kk = k0 + ak + 8 * s;
+                gld2(ap + (int64_t)(ki.kmin + min(kk, ki.kw - 1)) * ki.lda, ra[2 * s], ra[2 * s + 1]);
+            }
+        } else
 #pragma unroll
         for (int s = 0; s < AE; ++s) {
             const int kk = k0 + ak + (SB_THREADS / SB_BM) * s;
@@ -1489,6 +1511,15 @@ k_schur_big(const TileItem *tiles, const KInfo<T> *kinfo, T *Lval, T *Uval,
     };
     auto lstore = [&](int buf, int k0) {
         T *sA = smem + buf * STAGE, *sB = sA + SB_BK * LDS_A;
+        if constexpr (A16) {
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                const bool okk = k0 + ak + 8 * s < ki.kw;
+                typedef double d2 __attribute__((ext_vector_type(2)));
+                *(d2 *)&sA[(ak + 8 * s) * LDS_A + ar] =
+                    d2{keep_if(okk & (ar < mrows), ra[2 * s]), keep_if(okk & (ar + 1 < mrows), ra[2 * s + 1])};
+            }
+        } else
 #pragma unroll
         for (int s = 0; s < AE; ++s) {
             const int kk = k0 + ak + (SB_THREADS / SB_BM) * s;
