@@ -1350,7 +1350,7 @@ constexpr int SB_BM = 128;
 // (DevBuf::alloc_guarded; the L values too): k_schur_big's B loads read a
 // column's 4 consecutive k without clamping them to its segment (the mask
 // drops what lies outside), i.e. up to the panel width before a segment and
-// 15 past it; the A loads (SLU_SB_A16) read up to 127 rows past a column.
+// 15 past it; the A loads read up to 127 rows past a column.
 constexpr size_t SB_UGUARD = 1024;
 // THREADS / WN: workgroup size and waves along N; MINW: waves per SIMD the
 // register budget must allow (workgroups per CU x waves per workgroup / 4).
@@ -1463,13 +1463,11 @@ k_schur_big(const TileItem *tiles, const KInfo<T> *kinfo, T *Lval, T *Uval,
     // A: thread owns row ar and k = ak + 4s (s < 4); B: column bc, k = bk..bk+3.
     // Loads are unconditional from clamped in-bounds addresses; out-of-range
     // elements are zeroed afterwards (no per-element branches).
-#ifdef SLU_SB_A16
     // fp64: thread owns rows ar, ar + 1 and k = ak + 8s (s < 2): one 16-byte
-    // load per k along the column, unclamped rows (guarded L / panel buffers)
+    // load per k along the column, unclamped rows (guarded L / panel
+    // buffers), one 16-byte LDS store (312.4 -> 307.1 ms at 100^3, Schur
+    // 56.1 -> 57.3 %, profiles/r03x_ab)
     constexpr bool A16 = AE == 4 && std::is_same<T, double>::value;
-#else
-    constexpr bool A16 = false;
-#endif
     const int ar = A16 ? 2 * (tid & 63) : tid & (SB_BM - 1), ak = A16 ? tid >> 6 : tid / SB_BM;
     const bool avalid = ar < mrows;
     const T *ap = ki.a + row0 + (A16 || avalid ? ar : 0);
