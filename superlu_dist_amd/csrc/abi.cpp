@@ -18,6 +18,7 @@
 #include <execinfo.h>
 #include <hip/hip_runtime.h>
 #include <signal.h>
+#include <sys/resource.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -290,6 +291,23 @@ template <typename LUS> uint64_t structure_digest(LUS *lu, int n) {
     return h;
 }
 
+// process CPU time (all threads) and thread count, for SUPERLU_MI355X_TIMING
+double process_cpu_ms() {
+    struct rusage ru;
+    getrusage(RUSAGE_SELF, &ru);
+    return (ru.ru_utime.tv_sec + ru.ru_stime.tv_sec) * 1e3 + (ru.ru_utime.tv_usec + ru.ru_stime.tv_usec) * 1e-3;
+}
+int process_threads() {
+    FILE *f = fopen("/proc/self/status", "r");
+    if (!f) return -1;
+    char line[256];
+    int t = -1;
+    while (fgets(line, sizeof line, f))
+        if (!strncmp(line, "Threads:", 8)) t = atoi(line + 8);
+    fclose(f);
+    return t;
+}
+
 template <typename LUS>
 int_t pxgstrf(int dtype, const char *name, superlu_dist_options_t *options, int m, int n,
               double anorm, LUS *LUstruct, gridinfo_t *grid, SuperLUStat_t *stat, int *info) {
@@ -344,6 +362,7 @@ int_t pxgstrf(int dtype, const char *name, superlu_dist_options_t *options, int 
         bool pattern_ready = false;
         const bool reused = plan != nullptr;
         tp[1] = clk::now();
+        const double cpu1 = timing ? process_cpu_ms() : 0;
         if (plan) {
             std::lock_guard<std::mutex> lk(g_cache_mu);
             pattern_ready = g_cache.a_pattern;
@@ -370,6 +389,7 @@ int_t pxgstrf(int dtype, const char *name, superlu_dist_options_t *options, int 
         }
         int myinfo = 0, tiny = 0;
         tp[2] = clk::now();
+        const double cpu2 = timing ? process_cpu_ms() : 0;
         if (da) {
             if (!pattern_ready &&
                 slu_plan_set_a_pattern(plan, n, da->xa.data(), da->asub.data()))
@@ -391,11 +411,12 @@ int_t pxgstrf(int dtype, const char *name, superlu_dist_options_t *options, int 
                 return std::chrono::duration<double, std::milli>(tp[b] - tp[a]).count();
             };
             fprintf(stderr,
-                    "[%s rank %d] digest %.1f ms, plan %s %.1f ms (amalg %.1f), %s %.1f ms "
+                    "[%s rank %d] digest %.1f ms, plan %s %.1f ms (amalg %.1f; process cpu %.0f ms, "
+                    "%d threads), %s %.1f ms "
                     "(device fill %.1f, upload wait %.1f), factor %.1f ms (device %.1f: diag %.1f, "
                     "trsm %.1f, schur %.1f), download %.1f ms (tail %.1f)%s\n",
                     name, (int)grid->iam, ms(0, 1), reused ? "reused" : "built", ms(1, 2),
-                    st.t_amalg_ms, da ? "fill_a" : "upload", ms(2, 3), st.t_fill_ms,
+                    st.t_amalg_ms, cpu2 - cpu1, process_threads(), da ? "fill_a" : "upload", ms(2, 3), st.t_fill_ms,
                     st.t_upload_wait_ms, ms(3, 4), st.t_total_ms, st.t_diag_ms, st.t_trsm_ms,
                     st.t_schur_ms, ms(4, 5), st.t_d2h_tail_ms,
                     keep_on_device ? " [factors kept in HBM]" : "");

@@ -607,6 +607,9 @@ struct Plan : PlanBase {
         nlr = (nsupers + Pr - 1) / Pr;
         for (int k = 0; k < nsupers; ++k)
             SLU_REQUIRE(W(k) <= 512, "supernode %d has %d columns (> MAX_SUPER_SIZE 512)", k, W(k));
+        // k_schur_big reads up to a panel width before a U segment and 127
+        // rows past an L column, unclamped, inside the buffers' guards
+        static_assert(SB_UGUARD >= 512 + 128, "guards too small for the widest panel");
         const auto t0 = std::chrono::steady_clock::now();
         prof = getenv("SLU_PROFILE_PLAN") != nullptr;
         tprev = t0;
