@@ -1405,19 +1405,33 @@ k_schur_big(const TileItem *tiles, const KInfo<T> *kinfo, T *Lval, T *Uval,
     constexpr int WN = BigCfg<T>::WN;       // waves along N
     constexpr int FM = 2, FN = BigCfg<T>::FN; // fragments per wave (32 x 16*FN)
     constexpr int PASSW = BigCfg<T>::PASSW; // epilogue columns per pass
-    constexpr int LDS_A = SB_BM + 4, LDS_B = SB_BN + 4;
+#ifdef SLU_SB_SWZ
+    // fp64: unpadded [k][row] / [k][col] stages with the row (column) index
+    // XOR 16 on odd k.  A ds_read_b64 half-wave reads rows r..r+15 at k and
+    // at k + 1: at a 132-double pitch those 32-dword runs overlap on 24 of
+    // the 64 banks (2-way conflicts); unpadded + swizzled they take disjoint
+    // halves of the bank row.
+    constexpr bool SWZ = std::is_same<T, double>::value;
+#else
+    constexpr bool SWZ = false;
+#endif
+    constexpr int LDS_A = SWZ ? SB_BM : SB_BM + 4, LDS_B = SWZ ? SB_BN : SB_BN + 4;
     constexpr int STAGE = SB_BK * LDS_A + SB_BK * LDS_B;
     constexpr int CLD = SB_BM + 1; // C staging: [PASSW cols][CLD]
     constexpr int AE = SB_BM * SB_BK / SB_THREADS, BE = SB_BN * SB_BK / SB_THREADS;
-    static_assert(PASSW * CLD <= 2 * STAGE, "C staging must fit in the stage buffers");
     static_assert(WN * 16 * FN == SB_BN && AE >= 1 && BE >= 1, "tile shape");
     static_assert((SB_THREADS / 64 / WN) * 16 * FM == SB_BM, "waves along M");
     constexpr int CPN = SB_TB * SB_BN, RLN = SB_TB * SB_BM;
     static_assert(CPN <= SB_THREADS && RLN % SB_THREADS == 0, "table entries per thread");
     // the epilogue tables go in the stage buffers' tail past the C staging
     // where it is large enough, else in arrays of their own
-    constexpr bool TAIL = (2 * STAGE - PASSW * CLD) * (int)sizeof(T) >= CPN * 8 + RLN * 4;
-    __shared__ __attribute__((aligned(16))) T smem[2 * STAGE];
+    // one LDS buffer: the two stages, then (epilogue) the C staging and, where
+    // the swizzled layout leaves room for them, the destination tables
+    constexpr int TBL_T = (CPN * 8 + RLN * 4 + (int)sizeof(T) - 1) / (int)sizeof(T);
+    constexpr int SMEM = SWZ && 2 * STAGE < PASSW * CLD + TBL_T ? PASSW * CLD + TBL_T : 2 * STAGE;
+    static_assert(PASSW * CLD <= SMEM, "C staging must fit in the stage buffers");
+    constexpr bool TAIL = (SMEM - PASSW * CLD) * (int)sizeof(T) >= CPN * 8 + RLN * 4;
+    __shared__ __attribute__((aligned(16))) T smem[SMEM];
     __shared__ int s_rg[SB_BM], s_ra[SB_BM], s_cg[SB_BN], s_cb[SB_BN];
     __shared__ int64_t s_db[SB_TB * SB_TB], s_dmb[SB_TB * SB_TB]; // destination records
     __shared__ int s_dld[SB_TB * SB_TB];                          // ld (L) or -1 (U)
@@ -1514,7 +1528,7 @@ k_schur_big(const TileItem *tiles, const KInfo<T> *kinfo, T *Lval, T *Uval,
             for (int s = 0; s < 2; ++s) {
                 const bool okk = k0 + ak + 8 * s < ki.kw;
                 typedef double d2 __attribute__((ext_vector_type(2)));
-                *(d2 *)&sA[(ak + 8 * s) * LDS_A + ar] =
+                *(d2 *)&sA[(ak + 8 * s) * LDS_A + (ar ^ (SWZ ? (ak & 1) << 4 : 0))] =
                     d2{keep_if(okk & (ar < mrows), ra[2 * s]), keep_if(okk & (ar + 1 < mrows), ra[2 * s + 1])};
             }
         } else
@@ -1527,7 +1541,8 @@ k_schur_big(const TileItem *tiles, const KInfo<T> *kinfo, T *Lval, T *Uval,
 #pragma unroll
         for (int s = 0; s < BE; ++s) {
             const int t = ki.kmin + k0 + bk + s;
-            sB[(bk + s) * LDS_B + bc] = keep_if(bvalid & (t <= tlast) & (t >= bt0), rb[s]);
+            sB[(bk + s) * LDS_B + (bc ^ (SWZ ? (s & 1) << 4 : 0))] =
+                keep_if(bvalid & (t <= tlast) & (t >= bt0), rb[s]);
         }
     };
 
@@ -1549,9 +1564,11 @@ k_schur_big(const TileItem *tiles, const KInfo<T> *kinfo, T *Lval, T *Uval,
             const int kl = ks + (lane >> 4);
             T av[FM], bv[FN];
 #pragma unroll
-            for (int f = 0; f < FM; ++f) av[f] = sA[kl * LDS_A + wr * (16 * FM) + f * 16 + (lane & 15)];
+            for (int f = 0; f < FM; ++f)
+                av[f] = sA[kl * LDS_A + ((wr * (16 * FM) + f * 16 + (lane & 15)) ^ (SWZ ? (kl & 1) << 4 : 0))];
 #pragma unroll
-            for (int f = 0; f < FN; ++f) bv[f] = sB[kl * LDS_B + wc * (16 * FN) + f * 16 + (lane & 15)];
+            for (int f = 0; f < FN; ++f)
+                bv[f] = sB[kl * LDS_B + ((wc * (16 * FN) + f * 16 + (lane & 15)) ^ (SWZ ? (kl & 1) << 4 : 0))];
 #pragma unroll
             for (int fm = 0; fm < FM; ++fm)
 #pragma unroll
