@@ -1561,7 +1561,15 @@ k_schur_big(const TileItem *tiles, const KInfo<T> *kinfo, T *Lval, T *Uval,
         const T *sA = smem + (st & 1) * STAGE, *sB = sA + SB_BK * LDS_A;
 #pragma unroll
         for (int ks = 0; ks < SB_BK; ks += M::KSTEP) {
+#ifdef SLU_SB_KSTRIDE
+            // k-step j takes k = j + 4g in lane group g: the two groups of a
+            // ds_read_b64 half-wave read k rows 4 apart, 4 x 132 doubles =
+            // 32 banks apart at this pitch, so their 32-dword runs never share
+            // a bank (k and k + 1, 8 banks apart, overlapped on 24)
+            const int kl = ks / M::KSTEP + (SB_BK / M::KSTEP) * (lane >> 4);
+#else
             const int kl = ks + (lane >> 4);
+#endif
             T av[FM], bv[FN];
 #pragma unroll
             for (int f = 0; f < FM; ++f)
