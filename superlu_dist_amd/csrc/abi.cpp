@@ -230,11 +230,39 @@ struct CachedPlan {
     uint64_t digest = 0;
     int dtype = -1, n = -1, replace_tiny = -1;
     const void *lu = nullptr; // the LUstruct the cached factors belong to (pdgstrs)
+    struct Key {
+        const void *lu, *llu, *lrow;
+        bool operator==(const Key &o) const { return lu == o.lu && llu == o.llu && lrow == o.lrow; }
+    } key{};
     bool a_pattern = false;   // the plan holds DevA's pattern (fill_a ready)
+    uint64_t a_pattern_gen = 0; // ... of this DevA pattern generation
     bool host_factors = true; // the host L / U arrays hold these factors
 };
 CachedPlan g_cache;
 std::mutex g_cache_mu;
+
+// LUstructs whose factors lived only in the HBM of a cached plan that a later
+// pdgstrf evicted (the host L / U arrays still hold A's values).  The plan
+// cannot write them back at eviction: the caller may have destroyed the
+// LUstruct by then (dDestroy_LU frees its arrays without telling this
+// library).  A pdgstrs on such an LUstruct fails loudly instead of solving
+// with A as if it were its factors; a new pdgstrf / pddistribute on it clears
+// the mark.  Guarded by g_cache_mu.
+using LuKey = CachedPlan::Key;
+std::vector<LuKey> g_evicted;
+template <typename LUS> LuKey lu_key(LUS *lu) {
+    return {lu, lu->Llu, lu->Llu ? (const void *)lu->Llu->Lrowind_bc_ptr : nullptr};
+}
+void unmark_evicted(const LuKey &k) {
+    g_evicted.erase(std::remove(g_evicted.begin(), g_evicted.end(), k), g_evicted.end());
+}
+// the cache entry goes: its plan is reaped, device-only factors are marked
+void evict_cached() {
+    if (!g_cache.plan) return;
+    if (!g_cache.host_factors) g_evicted.push_back(g_cache.key);
+    reap_later(g_cache.plan);
+    g_cache.plan = nullptr;
+}
 
 // A in the LUstruct's coordinates (CSC), kept by this library's pddistribute
 // for the pdgstrf that follows: the factor storage is then built on the
@@ -249,7 +277,8 @@ struct DevA {
     int64_t n = 0;
     std::vector<int64_t> xa, asub;
     std::vector<char> a; // nnz values of the dtype
-    uint64_t gen = 0;    // bumps with every refill (SamePattern_SameRowPerm)
+    uint64_t gen = 0;         // bumps with every stash (values)
+    uint64_t pattern_gen = 0; // bumps with every first-time distribute (pattern, perm_r)
 };
 DevA g_deva;
 std::mutex g_deva_mu;
@@ -344,10 +373,13 @@ int_t pxgstrf(int dtype, const char *name, superlu_dist_options_t *options, int 
                 g_cache.replace_tiny == rt) {
                 plan = g_cache.plan; // same structure: reuse (values are uploaded again below)
                 g_cache.plan = nullptr;
-            } else if (g_cache.plan) {
-                reap_later(g_cache.plan);
-                g_cache.plan = nullptr;
+            } else {
+                evict_cached();
             }
+        }
+        {
+            std::lock_guard<std::mutex> lk(g_cache_mu);
+            unmark_evicted(lu_key(LUstruct)); // this call writes its factors anew
         }
         // built by this library's pddistribute: A is at hand for a device fill
         DevA *da = nullptr;
@@ -363,9 +395,12 @@ int_t pxgstrf(int dtype, const char *name, superlu_dist_options_t *options, int 
         const bool reused = plan != nullptr;
         tp[1] = clk::now();
         const double cpu1 = timing ? process_cpu_ms() : 0;
-        if (plan) {
+        if (plan && da) {
+            // the plan's A-to-factor map holds for the pattern it was built
+            // from: a new pddistribute (new perm_r, same index arrays) bumps
+            // the pattern generation and the map is built again
             std::lock_guard<std::mutex> lk(g_cache_mu);
-            pattern_ready = g_cache.a_pattern;
+            pattern_ready = g_cache.a_pattern && g_cache.a_pattern_gen == da->pattern_gen;
         }
         if (!plan) {
             reap_join(); // the previous call's device memory is free again
@@ -433,7 +468,9 @@ int_t pxgstrf(int dtype, const char *name, superlu_dist_options_t *options, int 
             g_cache.replace_tiny = rt;
             g_cache.lu = LUstruct;
             g_cache.a_pattern = pattern_ready;
+            g_cache.a_pattern_gen = da ? da->pattern_gen : 0;
             g_cache.host_factors = !keep_on_device;
+            g_cache.key = lu_key(LUstruct);
         } else {
             reap_later(plan);
         }
@@ -688,6 +725,15 @@ void pxgstrs(int dtype, const char *name, int_t n, LUS *LU, xScalePermstruct_t *
             }
         }
         if (!plan) {
+            {
+                std::lock_guard<std::mutex> lk(g_cache_mu);
+                const LuKey k = lu_key(LU);
+                SLU_REQUIRE(std::find(g_evicted.begin(), g_evicted.end(), k) == g_evicted.end(),
+                            "the factors of this LUstruct were kept only in GPU memory, and a later "
+                            "pdgstrf on another LUstruct replaced them (its host L / U arrays still "
+                            "hold A); factor it again, or set SUPERLU_MI355X_HOST_FACTORS=1 so that "
+                            "pdgstrf writes the factors back");
+            }
             reap_join();
             slu_comm *c = comm_for_grid(grid);
             slu_engine_opts eo{};
@@ -827,8 +873,14 @@ float pxdistribute(int dtype, const char *name, superlu_dist_options_t *options,
                 aval[q] = vv[e];
             }
         }
-        auto stash = [&] { // A for the device fill of the following pdgstrf
+        auto stash = [&](bool first_time) { // A for the device fill of the following pdgstrf
             std::lock_guard<std::mutex> lk(g_deva_mu);
+            const bool same = g_deva.lu == LU && g_deva.llu == LU->Llu &&
+                              g_deva.lrow == LU->Llu->Lrowind_bc_ptr && g_deva.dtype == dtype &&
+                              g_deva.n == n && g_deva.xa == xa && g_deva.asub == asub;
+            // a SamePattern_SameRowPerm refill keeps the pattern (and the
+            // plan's map of it); anything else starts a new generation
+            if (first_time || !same) g_deva.pattern_gen = ++g_deva_gen;
             g_deva.lu = LU;
             g_deva.llu = LU->Llu;
             g_deva.lrow = LU->Llu->Lrowind_bc_ptr;
@@ -843,7 +895,7 @@ float pxdistribute(int dtype, const char *name, superlu_dist_options_t *options,
             if (slu_refill_values(dtype, LU, n, xa.data(), asub.data(), aval.data(), Pr, Pc, myrow,
                                   mycol))
                 throw slu::Error(slu_last_error());
-            stash();
+            stash(false);
             return 0.0f;
         }
         // ---- first-time branch: the restated structural distribute
@@ -935,7 +987,11 @@ float pxdistribute(int dtype, const char *name, superlu_dist_options_t *options,
             Llu->ilsum[lb + 1] = Llu->ilsum[lb] + (gb < ns ? gp->xsup[gb + 1] - gp->xsup[gb] : 0);
         }
         Llu->ldalsum = Llu->ilsum[nlr];
-        stash();
+        {
+            std::lock_guard<std::mutex> lk(g_cache_mu);
+            unmark_evicted(lu_key(LU)); // new storage: A's values, no factors yet
+        }
+        stash(true);
         return (float)((double)Llu->Lnzval_bc_cnt * sizeof(T) + (double)Llu->Unzval_br_cnt * sizeof(T) +
                        (double)(Llu->Lrowind_bc_cnt + Llu->Ufstnz_br_cnt) * sizeof(int_t));
     } catch (const std::exception &e) {

@@ -2565,11 +2565,6 @@ struct Plan : PlanBase {
     // CUs and run beside the second (100^3: 363 -> 345 ms; more split points
     // gain nothing further, tools/ab_env.sh).
     int rest_split = getenv("SLU_REST_SPLIT") ? atoi(getenv("SLU_REST_SPLIT")) : 30;
-    // SLU_DIAG_CO=1 (A/B): fp64 diagonal blocks on k_diag_lu_c, which fits
-    // beside a Schur workgroup; measured 335 vs 326 ms at 100^3 (its 4 waves
-    // and column chunks cost more than the overlap gains), so k_diag_lu_f
-    bool diag_co = std::is_same<T, double>::value && getenv("SLU_DIAG_CO") &&
-                   atoi(getenv("SLU_DIAG_CO")) == 1;
     int rest_chunks = getenv("SLU_REST_CHUNKS") ? atoi(getenv("SLU_REST_CHUNKS")) : 1;
     void launch_big(const LevelRange &R, int off, int cnt, hipStream_t st) {
         hipLaunchKernelGGL(k_schur_big<T>, dim3(cnt), dim3(BigCfg<T>::THREADS), 0, st,
@@ -2674,11 +2669,7 @@ struct Plan : PlanBase {
                 });
             if (R.df_n)
                 span(0, P, [&] {
-                    if (diag_co)
-                        hipLaunchKernelGGL(k_diag_lu_c<T>, dim3(R.df_n), dim3(DC_THREADS), 0, P,
-                                           d_df.p + R.df_off, thresh, opts.replace_tiny_pivot,
-                                           d_counters.p, d_zpiv.p);
-                    else if (R.df_maxw <= DF_SMALLW)
+                    if (R.df_maxw <= DF_SMALLW)
                         hipLaunchKernelGGL((k_diag_lu_f<T, DF_SMALLW, DF_SMALL_THREADS>), dim3(R.df_n),
                                            dim3(DF_SMALL_THREADS), 0, P, d_df.p + R.df_off, thresh,
                                            opts.replace_tiny_pivot, d_counters.p, d_zpiv.p);

@@ -976,246 +976,6 @@ k_diag_lu_f(const DiagItemF<T> *items, double thresh, int replace_tiny, int *tin
     }
 }
 
-// Co-resident variant of k_diag_lu_f: the same factorization, arithmetic
-// and outputs, on 4 waves with <= 256 VGPRs and 84 KB of LDS, so that it fits
-// on a CU where one Schur workgroup finished (k_schur_big holds 76 KB and 2
-// waves x 128 VGPRs per SIMD) instead of waiting for a CU no Schur workgroup
-// holds.  What it gives up for that: U11^{-1} and L11^{-1} share one LDS
-// tile (formed one after the other), and U12 / the trailing update go
-// through LDS in chunks of DC_CH columns instead of all at once.
-constexpr int DC_THREADS = 256, DC_CH = 16;
-template <typename T>
-__global__ void __launch_bounds__(DC_THREADS, 2)
-k_diag_lu_c(const DiagItemF<T> *items, double thresh, int replace_tiny, int *tiny_count,
-            int *zpiv) {
-    constexpr int PW = PWOf<T>::v;
-    constexpr int NW = DC_THREADS / 64;
-    using Sx = S<T>;
-    using M = Mma<T>;
-    const DiagItemF<T> it = items[blockIdx.x];
-    T *A = it.a;
-    const int ld = it.ld, w = it.w, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int nb = (w + PW - 1) / PW;
-    T *dinvU = it.dinv, *dinvLT = it.dinv + (int64_t)nb * PW * PW;
-    __shared__ T sP[FAST_MAXW][PW + 1]; // panel rows (row 0 = row p0), PW columns
-    __shared__ T sX[PW][PW + 1];        // U11^{-1}, then L11^{-1}
-    __shared__ T sC[PW][DC_CH + 1];     // a chunk of U12
-    __shared__ T s_rp[PW];
-    __shared__ int s_z[PW];
-    __shared__ int s_anyz;
-    for (int p = 0; p < nb; ++p) {
-        const int p0 = p * PW, pw = min(PW, w - p0), nrow = w - p0, nbl = nrow - pw;
-        T *A11 = A + p0 + (int64_t)p0 * ld;
-        // ---- 0. stage the panel (zero outside pw / below nrow, as k_diag_lu_f)
-        const int nrs = max(nrow, PW);
-        for (int e = tid; e < nrs * PW; e += DC_THREADS) {
-            const int r = e % nrs, c = e / nrs;
-            sP[r][c] = (c < pw && r < nrow) ? A11[r + (int64_t)c * ld] : Sx::zero();
-        }
-        __syncthreads();
-        // ---- 1. A11 = L11 U11 in registers (wave 0), as k_diag_lu_f
-        if (wid == 0) {
-            const int row = lane & (PW - 1);
-            T xr[PW];
-#pragma unroll
-            for (int c = 0; c < PW; ++c) xr[c] = (row < pw) ? sP[row][c] : Sx::zero();
-            int anyz = 0;
-#pragma unroll
-            for (int j = 0; j < PW; ++j) {
-                if (j < pw) {
-                    T piv = rlane(xr[j], j);
-                    if (replace_tiny && Sx::abs1(piv) < thresh) {
-                        piv = Sx::thresh(piv, thresh);
-                        if (lane == 0) atomicAdd(tiny_count, 1);
-                    }
-                    const int z = Sx::iszero(piv);
-                    if (z) {
-                        anyz = 1;
-                        if (lane == 0) atomicMax(&zpiv[it.k], it.fcol + p0 + j + 1);
-                    }
-                    const T rp = z ? Sx::zero() : Sx::recip(piv);
-                    const bool below = row > j;
-                    const T l = below ? (z ? xr[j] : Sx::mul(xr[j], rp)) : Sx::zero();
-                    xr[j] = below ? l : (row == j ? piv : xr[j]);
-                    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                    for (int c = j + 1; c < PW; ++c) {
-                        xr[c] = Sx::fms(xr[c], l, rlane(xr[c], j));
-                        if ((c & 3) == 3) __builtin_amdgcn_sched_barrier(0);
-                    }
-                    __builtin_amdgcn_sched_barrier(0);
-                    if (lane == 0) {
-                        s_rp[j] = rp;
-                        s_z[j] = z;
-                    }
-                }
-            }
-            if (lane < pw) {
-#pragma unroll
-                for (int c = 0; c < PW; ++c) sP[lane][c] = xr[c];
-            }
-            if (lane == 0) s_anyz = anyz;
-            if (lane >= pw && lane < PW) {
-                s_rp[lane] = Sx::zero();
-                s_z[lane] = 0;
-            }
-        }
-        __syncthreads();
-        // ---- 1b. U11^{-1} (wave 0, lane = column, column-sweep order)
-        if (wid == 0 && lane < PW) {
-            const int j = lane;
-            T x[PW];
-#pragma unroll
-            for (int i = 0; i < PW; ++i) x[i] = (i == j) ? one_of(Sx::zero()) : Sx::zero();
-#pragma unroll
-            for (int i = PW - 1; i >= 0; --i) {
-                x[i] = Sx::mul(x[i], s_rp[i]);
-#pragma unroll
-                for (int k = 0; k < i; ++k) x[k] = Sx::fms(x[k], sP[k][i], x[i]);
-            }
-#pragma unroll
-            for (int i = 0; i < PW; ++i) sX[i][j] = (i <= j && j < pw) ? x[i] : Sx::zero();
-        }
-        __syncthreads();
-        const bool anyz = s_anyz;
-        // ---- 2a. L21 = A21 U11^{-1} (or the substitution with the zero-pivot semantics)
-        if (!anyz) {
-            const int nfr = (nbl + 15) / 16;
-            for (int f = wid; f < nfr; f += NW) {
-                typename M::acc_t acc0 = M::zero(), acc1 = M::zero();
-                const int r = f * 16 + (lane & 15);
-#pragma unroll
-                for (int ks = 0; ks < PW; ks += M::KSTEP) {
-                    const int k = ks + (lane >> 4);
-                    const T av = r < nbl ? sP[pw + r][k] : Sx::zero();
-                    M::step(acc0, av, sX[k][lane & 15]);
-                    if (PW > 16) M::step(acc1, av, sX[k][16 + (lane & 15)]);
-                }
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int rr = f * 16 + M::row(lane, i), cc = lane & 15;
-                    if (rr < nbl) {
-                        sP[pw + rr][cc] = cc < pw ? M::get(acc0, i) : Sx::zero();
-                        if (PW > 16) sP[pw + rr][16 + cc] = 16 + cc < pw ? M::get(acc1, i) : Sx::zero();
-                    }
-                }
-            }
-        } else {
-            for (int t = tid; t < nbl; t += DC_THREADS) { // row t of L21: x U11 = a, column by column
-                for (int c = 0; c < PW; ++c) {
-                    T v = sP[pw + t][c];
-                    for (int i = 0; i < c; ++i) v = Sx::fms(v, sP[pw + t][i], sP[i][c]);
-                    sP[pw + t][c] = c >= pw ? Sx::zero() : s_z[c] ? v : Sx::mul(v, s_rp[c]);
-                }
-            }
-        }
-        for (int e = tid; e < PW * PW; e += DC_THREADS)
-            dinvU[(int64_t)p * PW * PW + e] = sX[e / PW][e % PW]; // row-major U11^{-1}
-        __syncthreads();
-        // ---- 1c. L11^{-1} into the same tile (wave 0), and the panel to global
-        if (wid == 0 && lane < PW) {
-            const int j = lane;
-            T x[PW];
-#pragma unroll
-            for (int i = 0; i < PW; ++i) x[i] = (i == j) ? one_of(Sx::zero()) : Sx::zero();
-#pragma unroll
-            for (int i = 0; i < PW; ++i)
-#pragma unroll
-                for (int k = i + 1; k < PW; ++k) x[k] = Sx::fms(x[k], sP[k][i], x[i]);
-#pragma unroll
-            for (int i = 0; i < PW; ++i) sX[i][j] = (i >= j && i < pw && j < pw) ? x[i] : Sx::zero();
-        }
-        for (int e = tid; e < nrow * pw; e += DC_THREADS) {
-            const int r = e % nrow, c = e / nrow;
-            A11[r + (int64_t)c * ld] = sP[r][c];
-        }
-        __syncthreads();
-        for (int e = tid; e < PW * PW; e += DC_THREADS) {
-            const int i = e / PW, jj = e % PW;
-            dinvLT[(int64_t)p * PW * PW + e] = sX[jj][i]; // row-major (L11^{-1})^T
-        }
-        // ---- 2b/3. per chunk of DC_CH columns right of the panel:
-        // U12 = L11^{-1} A12 (LDS), back to global, A22(:, chunk) -= L21 U12
-        for (int q0 = 0; q0 < nbl; q0 += DC_CH) {
-            const int qn = min(DC_CH, nbl - q0);
-            T *A12 = A11 + (int64_t)(pw + q0) * ld;
-            for (int e = tid; e < PW * DC_CH; e += DC_THREADS) {
-                const int i = e % PW, c = e / PW;
-                sC[i][c] = (i < pw && c < qn) ? A12[i + (int64_t)c * ld] : Sx::zero();
-            }
-            __syncthreads();
-            if (!anyz) {
-                constexpr int NG = DC_CH / 16;
-                if (wid < NG) {
-                    const int g = wid, c = g * 16 + (lane & 15);
-                    typename M::acc_t acc0 = M::zero(), acc1 = M::zero();
-#pragma unroll
-                    for (int ks = 0; ks < PW; ks += M::KSTEP) {
-                        const int k = ks + (lane >> 4);
-                        const T bv = sC[k][c];
-                        M::step(acc0, sX[lane & 15][k], bv);
-                        if (PW > 16) M::step(acc1, sX[16 + (lane & 15)][k], bv);
-                    }
-                    // each wave owns its 16 columns of the chunk: no other wave reads them meanwhile
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const int ii = M::row(lane, i), cc = g * 16 + (lane & 15);
-                        sC[ii][cc] = ii < pw ? M::get(acc0, i) : Sx::zero();
-                        if (PW > 16) sC[16 + ii][cc] = 16 + ii < pw ? M::get(acc1, i) : Sx::zero();
-                    }
-                }
-            } else {
-                for (int cc = tid; cc < qn; cc += DC_THREADS) { // column cc: L11 y = a
-                    for (int i = 0; i < PW; ++i) {
-                        T v = sC[i][cc];
-                        for (int k = 0; k < i; ++k) v = Sx::fms(v, sP[i][k], sC[k][cc]);
-                        sC[i][cc] = i < pw ? v : Sx::zero();
-                    }
-                }
-            }
-            __syncthreads();
-            for (int e = tid; e < pw * qn; e += DC_THREADS) {
-                const int i = e % pw, c = e / pw;
-                A12[i + (int64_t)c * ld] = sC[i][c];
-            }
-            // A22(:, chunk) -= L21 U12(:, chunk): 16 x 16 fragments over the waves
-            const int nf = (nbl + 15) / 16, nfc = (qn + 15) / 16, nff = nf * nfc;
-            T *A22 = A11 + pw + (int64_t)(pw + q0) * ld;
-            for (int f = wid; f < nff; f += NW) {
-                const int fr = f % nf, fc = f / nf;
-                T cv[4];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int r = fr * 16 + M::row(lane, i), c = fc * 16 + (lane & 15);
-                    cv[i] = (r < nbl && c < qn) ? A22[r + (int64_t)c * ld] : Sx::zero();
-                }
-                typename M::acc_t acc = M::zero();
-                const int r = fr * 16 + (lane & 15), c = fc * 16 + (lane & 15);
-#pragma unroll
-                for (int ks = 0; ks < PW; ks += M::KSTEP) {
-                    const int k = ks + (lane >> 4);
-                    const T av = (r < nbl) ? sP[pw + r][k] : Sx::zero();
-                    M::step(acc, av, sC[k][c]);
-                }
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int rr = fr * 16 + M::row(lane, i), cc = fc * 16 + (lane & 15);
-                    if (rr < nbl && cc < qn)
-                        A22[rr + (int64_t)cc * ld] = Sx::fms(cv[i], M::get(acc, i), one_of(cv[i]));
-                }
-            }
-            __syncthreads();
-        }
-        __syncthreads();
-    }
-}
-
-// Blocked TRSM with inverted PW x PW diagonal blocks, RB rows per workgroup:
-//   MODE 0 (L panel):  X := X U_kk^{-1}      (SRC/pdgstrf2.c:311,352 dtrsm R,U,N,N)
-//   MODE 1 (U panel):  Y := L_kk^{-1} Y as Y^T := Y^T (L_kk^T)^{-1}, rows of
-//                      Y^T = U column segments zero-padded above their first
-//                      row                  (SRC/pdgstrf2.c:871 dtrsv L,N,U)
-// For column block b:  X_b := (X_b - X_{<b} T_{<b,b}) Dinv_b  (MFMA both).
 template <typename T> struct TrsmItemF {
     T *x;                // MODE 0: first row, column-major ld ldx; MODE 1: U value base
     const int64_t *voff; // MODE 1: per row (U column) segment offset
@@ -1357,13 +1117,6 @@ constexpr size_t SB_UGUARD = 1024;
 template <typename T> struct BigCfg {
     static constexpr int THREADS = 512, WN = 2, MINW = 4, BN = 128, BK = 16, FN = 4, PASSW = 64;
 };
-#ifdef SLU_SB_NARROW
-// A/B (tools/ab_build.sh narrow "-DSLU_SB_NARROW"): fp64 tiles of 128 x 64 on
-// 4 waves (each 32 x 64 as in the wide tile), three workgroups per CU
-template <> struct BigCfg<double> {
-    static constexpr int THREADS = 256, WN = 1, MINW = 3, BN = 64, BK = 16, FN = 4, PASSW = 32;
-};
-#endif
 template <> struct BigCfg<zc> {
     static constexpr int THREADS = 512, WN = 2, MINW = 4, BN = 64, BK = 8, FN = 2, PASSW = 16;
 };
@@ -1374,9 +1127,7 @@ template <> struct BigCfg<float> {
 constexpr int SB_BN = BigCfg<double>::BN;
 constexpr int SB_THREADS = 512; // the 512-thread configurations (k_schur_big<float>, <zc>)
 constexpr int SB_TB = 4; // epilogue tables: row blocks x column blocks per tile
-#ifndef SLU_SB_AEB
-#define SLU_SB_AEB 4 // atomic scatters formed per batch (A/B builds: -DSLU_SB_AEB=8)
-#endif
+constexpr int SB_AEB = 4; // atomic scatters formed per batch (8: slower)
 
 #ifdef SLU_SB_STAMP
 // Diagnostics build only (tools/ab_build.sh NAME "-DSLU_SB_STAMP"): per-tile
@@ -1405,17 +1156,7 @@ k_schur_big(const TileItem *tiles, const KInfo<T> *kinfo, T *Lval, T *Uval,
     constexpr int WN = BigCfg<T>::WN;       // waves along N
     constexpr int FM = 2, FN = BigCfg<T>::FN; // fragments per wave (32 x 16*FN)
     constexpr int PASSW = BigCfg<T>::PASSW; // epilogue columns per pass
-#ifdef SLU_SB_SWZ
-    // fp64: unpadded [k][row] / [k][col] stages with the row (column) index
-    // XOR 16 on odd k.  A ds_read_b64 half-wave reads rows r..r+15 at k and
-    // at k + 1: at a 132-double pitch those 32-dword runs overlap on 24 of
-    // the 64 banks (2-way conflicts); unpadded + swizzled they take disjoint
-    // halves of the bank row.
-    constexpr bool SWZ = std::is_same<T, double>::value;
-#else
-    constexpr bool SWZ = false;
-#endif
-    constexpr int LDS_A = SWZ ? SB_BM : SB_BM + 4, LDS_B = SWZ ? SB_BN : SB_BN + 4;
+    constexpr int LDS_A = SB_BM + 4, LDS_B = SB_BN + 4; // padded stages
     constexpr int STAGE = SB_BK * LDS_A + SB_BK * LDS_B;
     constexpr int CLD = SB_BM + 1; // C staging: [PASSW cols][CLD]
     constexpr int AE = SB_BM * SB_BK / SB_THREADS, BE = SB_BN * SB_BK / SB_THREADS;
@@ -1425,10 +1166,9 @@ k_schur_big(const TileItem *tiles, const KInfo<T> *kinfo, T *Lval, T *Uval,
     static_assert(CPN <= SB_THREADS && RLN % SB_THREADS == 0, "table entries per thread");
     // the epilogue tables go in the stage buffers' tail past the C staging
     // where it is large enough, else in arrays of their own
-    // one LDS buffer: the two stages, then (epilogue) the C staging and, where
-    // the swizzled layout leaves room for them, the destination tables
-    constexpr int TBL_T = (CPN * 8 + RLN * 4 + (int)sizeof(T) - 1) / (int)sizeof(T);
-    constexpr int SMEM = SWZ && 2 * STAGE < PASSW * CLD + TBL_T ? PASSW * CLD + TBL_T : 2 * STAGE;
+    // one LDS buffer: the two stages, then (epilogue) the C staging and,
+    // where it leaves room for them, the destination tables
+    constexpr int SMEM = 2 * STAGE;
     static_assert(PASSW * CLD <= SMEM, "C staging must fit in the stage buffers");
     constexpr bool TAIL = (SMEM - PASSW * CLD) * (int)sizeof(T) >= CPN * 8 + RLN * 4;
     __shared__ __attribute__((aligned(16))) T smem[SMEM];
@@ -1528,7 +1268,7 @@ k_schur_big(const TileItem *tiles, const KInfo<T> *kinfo, T *Lval, T *Uval,
             for (int s = 0; s < 2; ++s) {
                 const bool okk = k0 + ak + 8 * s < ki.kw;
                 typedef double d2 __attribute__((ext_vector_type(2)));
-                *(d2 *)&sA[(ak + 8 * s) * LDS_A + (ar ^ (SWZ ? (ak & 1) << 4 : 0))] =
+                *(d2 *)&sA[(ak + 8 * s) * LDS_A + ar] =
                     d2{keep_if(okk & (ar < mrows), ra[2 * s]), keep_if(okk & (ar + 1 < mrows), ra[2 * s + 1])};
             }
         } else
@@ -1541,7 +1281,7 @@ k_schur_big(const TileItem *tiles, const KInfo<T> *kinfo, T *Lval, T *Uval,
 #pragma unroll
         for (int s = 0; s < BE; ++s) {
             const int t = ki.kmin + k0 + bk + s;
-            sB[(bk + s) * LDS_B + (bc ^ (SWZ ? (s & 1) << 4 : 0))] =
+            sB[(bk + s) * LDS_B + bc] =
                 keep_if(bvalid & (t <= tlast) & (t >= bt0), rb[s]);
         }
     };
@@ -1561,22 +1301,14 @@ k_schur_big(const TileItem *tiles, const KInfo<T> *kinfo, T *Lval, T *Uval,
         const T *sA = smem + (st & 1) * STAGE, *sB = sA + SB_BK * LDS_A;
 #pragma unroll
         for (int ks = 0; ks < SB_BK; ks += M::KSTEP) {
-#ifdef SLU_SB_KSTRIDE
-            // k-step j takes k = j + 4g in lane group g: the two groups of a
-            // ds_read_b64 half-wave read k rows 4 apart, 4 x 132 doubles =
-            // 32 banks apart at this pitch, so their 32-dword runs never share
-            // a bank (k and k + 1, 8 banks apart, overlapped on 24)
-            const int kl = ks / M::KSTEP + (SB_BK / M::KSTEP) * (lane >> 4);
-#else
             const int kl = ks + (lane >> 4);
-#endif
             T av[FM], bv[FN];
 #pragma unroll
             for (int f = 0; f < FM; ++f)
-                av[f] = sA[kl * LDS_A + ((wr * (16 * FM) + f * 16 + (lane & 15)) ^ (SWZ ? (kl & 1) << 4 : 0))];
+                av[f] = sA[kl * LDS_A + wr * (16 * FM) + f * 16 + (lane & 15)];
 #pragma unroll
             for (int f = 0; f < FN; ++f)
-                bv[f] = sB[kl * LDS_B + ((wc * (16 * FN) + f * 16 + (lane & 15)) ^ (SWZ ? (kl & 1) << 4 : 0))];
+                bv[f] = sB[kl * LDS_B + wc * (16 * FN) + f * 16 + (lane & 15)];
 #pragma unroll
             for (int fm = 0; fm < FM; ++fm)
 #pragma unroll
@@ -1678,11 +1410,7 @@ k_schur_big(const TileItem *tiles, const KInfo<T> *kinfo, T *Lval, T *Uval,
                 for (int bl = 0; bl < SB_TB; ++bl) rl[bl] = s_rl[bl * SB_BM + r];
             }
             if (r < mrows) {
-#ifdef SLU_SB_RMW
-                constexpr int EB = CPT < 4 ? CPT : 4;
-#else
-                constexpr int EB = CPT < SLU_SB_AEB ? CPT : SLU_SB_AEB;
-#endif
+                constexpr int EB = CPT < SB_AEB ? CPT : SB_AEB;
 #pragma unroll
                 for (int j0 = 0; j0 < CPT; j0 += EB) {
                     T *dp[EB];
@@ -1705,24 +1433,9 @@ k_schur_big(const TileItem *tiles, const KInfo<T> *kinfo, T *Lval, T *Uval,
                             dp[j] = base + ((code >> 3) + rp);
                         }
                     }
-#ifdef SLU_SB_RMW
-                    if (ki.atomic) {
-#pragma unroll
-                        for (int j = 0; j < EB; ++j)
-                            if (dp[j]) Sx::atomic_sub(dp[j], v[j]);
-                    } else {
-                        T o[EB];
-#pragma unroll
-                        for (int j = 0; j < EB; ++j) o[j] = dp[j] ? *dp[j] : Sx::zero();
-#pragma unroll
-                        for (int j = 0; j < EB; ++j)
-                            if (dp[j]) *dp[j] = Sx::sub(o[j], v[j]);
-                    }
-#else
 #pragma unroll
                     for (int j = 0; j < EB; ++j)
                         if (dp[j]) Sx::atomic_sub(dp[j], v[j]);
-#endif
                 }
             }
             __syncthreads();
@@ -1730,10 +1443,7 @@ k_schur_big(const TileItem *tiles, const KInfo<T> *kinfo, T *Lval, T *Uval,
     } else {
         // slow path (tiles over more blocks): per-element table walk, EB
         // read-modify-writes in flight per thread
-#ifndef SLU_SB_EB
-#define SLU_SB_EB 4 // slow path read-modify-writes in flight per thread (A/B builds: -DSLU_SB_EB=8)
-#endif
-        constexpr int EB = CPT < SLU_SB_EB ? CPT : SLU_SB_EB;
+        constexpr int EB = CPT < 4 ? CPT : 4; // (8 in flight: slower)
         static_assert(CPT % EB == 0, "epilogue batches");
         const int *prow = ki.pair + (int64_t)a * ki.nub;
         int lastb = -1, h = 0, ldh = 0;
@@ -1829,15 +1539,9 @@ k_trsm_reg(const TrsmItemF<T> *items) {
     // sT, which the block's MFMAs have read by then (a barrier separates
     // them): 68 KB of LDS instead of 85, so the kernel fits beside a Schur
     // workgroup (engine.hip, rest_split)
-#ifdef SLU_TRSM_SEPARATE_W
-    __shared__ T sT[FAST_MAXW - PW][PW + 1];
-    __shared__ T sWx[TR_WAVES][16][PW + 1];
-    T (*W)[PW + 1] = sWx[wid];
-#else
     __shared__ T sT[FAST_MAXW - PW][PW + 1];
     static_assert(TR_WAVES * 16 <= FAST_MAXW - PW, "sW inside sT");
     T (*W)[PW + 1] = sT + wid * 16;
-#endif
     __shared__ T sD[PW][PW + 1];
     const int rl = lane & 15, kq = lane >> 4;
     const int myr = wid * 16 + rl;
@@ -1890,9 +1594,7 @@ k_trsm_reg(const TrsmItemF<T> *items) {
             M::step(a0, xa[s], b0);
             M::step(a1, xa[s], b1);
         }
-#ifndef SLU_TRSM_SEPARATE_W
         __syncthreads(); // every wave is done with sT before W (= its first rows) is written
-#endif
         // Z = X_b - acc: acc (C layout) -> LDS, read back in A layout
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
