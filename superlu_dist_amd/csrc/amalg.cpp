@@ -55,10 +55,9 @@ template <typename F> inline void for_ucols(const int_t *ux, const int_t *xsup, 
 
 } // namespace
 
-bool Amalg::build(int64_t n_, int ns, const int_t *xsup, const int_t *const *lidx,
-                  const int_t *const *uidx, double zero_frac, int maxw) {
-    n = n_;
-    ns1 = ns;
+std::vector<int> amalg_chains(int64_t n, int ns, const int_t *xsup, const int_t *const *lidx,
+                              const int_t *const *uidx, double zero_frac, int maxw, int a0, int a1,
+                              AmalgFlops *fl) {
     const bool prof = getenv("SLU_AMALG_TIME") != nullptr;
     auto t0 = std::chrono::steady_clock::now();
     auto tick = [&](const char *what) {
@@ -70,12 +69,14 @@ bool Amalg::build(int64_t n_, int ns, const int_t *xsup, const int_t *const *lid
     };
     auto W = [&](i64 k) { return (int)(xsup[k + 1] - xsup[k]); };
     SLU_REQUIRE(n < (1ll << 31), "amalgamation: n %lld does not fit int32", (long long)n);
+    const int nr = a1 - a0;
 
     // ---- pass 1: per supernode structure facts (parallel)
-    std::vector<SnInfo> inf(ns);
-    parallel_for(ns, [&](int s) {
+    std::vector<SnInfo> inf(nr);
+    parallel_for(nr, [&](int si) {
+        const int s = a0 + si;
         thread_local std::vector<int32_t> bl, uc, bl2;
-        SnInfo &I = inf[s];
+        SnInfo &I = inf[si];
         const int_t *ux = uidx[s];
         if (ux) {
             i64 p = SLU_BR_HEADER;
@@ -113,7 +114,7 @@ bool Amalg::build(int64_t n_, int ns, const int_t *xsup, const int_t *const *lid
         I.sym = bl == uc; // U columns come out ascending (blocks by jb)
         I.ok = true;
         // nested into s+1: below(s) within cols(s+1) u below(s+1)
-        if (I.parent == s + 1 && s + 1 < ns) {
+        if (I.parent == s + 1 && s + 1 < a1) {
             below_rows(lidx[s + 1], s + 1, bl2);
             std::sort(bl2.begin(), bl2.end());
             const i64 f1 = xsup[s + 1], l1 = xsup[s + 2];
@@ -128,26 +129,27 @@ bool Amalg::build(int64_t n_, int ns, const int_t *xsup, const int_t *const *lid
         }
     }, 16);
 
-    for (int s = 0; s < ns; ++s) {
-        const double w = W(s);
-        fl_w += w;
-        fl_s1 += w * (w - 1) / 2;
-        fl_s2 += (w - 1) * w * (2 * w - 1) / 6;
-        fl_trsm += w * (w + 1) * inf[s].b;
-        fl_trsv += inf[s].trsv;
-        fl_schur += inf[s].schur;
-    }
+    if (fl)
+        for (int si = 0; si < nr; ++si) {
+            const double w = W(a0 + si);
+            fl->w += w;
+            fl->s1 += w * (w - 1) / 2;
+            fl->s2 += (w - 1) * w * (2 * w - 1) / 6;
+            fl->trsm += w * (w + 1) * inf[si].b;
+            fl->trsv += inf[si].trsv;
+            fl->schur += inf[si].schur;
+        }
     tick("pass 1 (structure facts)");
-    // ---- pass 2: greedy chains
+    // ---- pass 2: greedy chains (never across a1)
     std::vector<int> gstart; // first original supernode of every group
     {
         std::vector<int32_t> ff((size_t)n, -1); // first-row of column g in the open chain
         std::vector<int32_t> touched;
-        int s = 0;
-        while (s < ns) {
+        int s = a0;
+        while (s < a1) {
             gstart.push_back(s);
             int e = s;
-            const SnInfo &I0 = inf[s];
+            const SnInfo &I0 = inf[s - a0];
             int wJ = W(s);
             i64 orig = (i64)W(s) * I0.nsupr + I0.ulen;
             touched.clear();
@@ -155,8 +157,9 @@ bool Amalg::build(int64_t n_, int ns, const int_t *xsup, const int_t *const *lid
                 for_ucols(uidx[s], xsup, [&](i64 g, i64 fst) {
                     if (fst < xsup[s + 1]) { ff[g] = (int32_t)fst; touched.push_back((int32_t)g); }
                 });
-            while (e + 1 < ns && inf[e].ok && inf[e].sym && inf[e].nested && inf[e].parent == e + 1 &&
-                   inf[e + 1].ok && inf[e + 1].sym && wJ + W(e + 1) <= maxw) {
+            while (e + 1 < a1 && inf[e - a0].ok && inf[e - a0].sym && inf[e - a0].nested &&
+                   inf[e - a0].parent == e + 1 && inf[e + 1 - a0].ok && inf[e + 1 - a0].sym &&
+                   wJ + W(e + 1) <= maxw) {
                 const int c = e + 1;
                 const i64 endc = xsup[c + 1];
                 double S = 0;
@@ -168,7 +171,7 @@ bool Amalg::build(int64_t n_, int ns, const int_t *xsup, const int_t *const *lid
                 });
                 const i64 w2 = wJ + W(c);
                 const double merged = (double)w2 * (double)(w2 + b) + (double)b * (double)endc - S;
-                const double orig2 = (double)orig + (double)W(c) * inf[c].nsupr + inf[c].ulen;
+                const double orig2 = (double)orig + (double)W(c) * inf[c - a0].nsupr + inf[c - a0].ulen;
                 if (merged - orig2 > zero_frac * merged) break;
                 for_ucols(uidx[c], xsup, [&](i64 g, i64 fst) {
                     if (fst < endc && ff[g] < 0) { ff[g] = (int32_t)fst; touched.push_back((int32_t)g); }
@@ -181,6 +184,42 @@ bool Amalg::build(int64_t n_, int ns, const int_t *xsup, const int_t *const *lid
             s = e + 1;
         }
     }
+    tick("pass 2 (chains)");
+    return gstart;
+}
+
+bool Amalg::build(int64_t n_, int ns, const int_t *xsup, const int_t *const *lidx,
+                  const int_t *const *uidx, double zero_frac, int maxw) {
+    n = n_;
+    ns1 = ns;
+    const bool prof = getenv("SLU_AMALG_TIME") != nullptr;
+    auto t0 = std::chrono::steady_clock::now();
+    auto tick = [&](const char *what) {
+        if (!prof) return;
+        const auto t = std::chrono::steady_clock::now();
+        fprintf(stderr, "[slu amalg] %s %.1f ms\n", what,
+                std::chrono::duration<double, std::milli>(t - t0).count());
+        t0 = t;
+    };
+    auto W = [&](i64 k) { return (int)(xsup[k + 1] - xsup[k]); };
+    AmalgFlops fl;
+    std::vector<int> gstart = amalg_chains(n, ns, xsup, lidx, uidx, zero_frac, maxw, 0, ns, &fl);
+    fl_w = fl.w;
+    fl_s1 = fl.s1;
+    fl_s2 = fl.s2;
+    fl_trsm = fl.trsm;
+    fl_trsv = fl.trsv;
+    fl_schur = fl.schur;
+    std::vector<SnInfo> inf(ns); // (pass 3 reads the per-supernode U column counts only)
+    parallel_for(ns, [&](int s) {
+        if (const int_t *ux = uidx[s]) {
+            i64 p = SLU_BR_HEADER;
+            for (i64 b = 0; b < ux[0]; ++b) {
+                inf[s].ucols += W(ux[p]);
+                p += SLU_UB_DESCRIPTOR + W(ux[p]);
+            }
+        }
+    }, 64);
     ns2 = (int)gstart.size();
     tick("pass 2 (chains)");
     if (ns2 == ns1) return false;

@@ -40,6 +40,49 @@
 
 namespace slu {
 
+// The original partition's algorithmic work (the reference's accounting,
+// SURVEY 8d): real-flop sums, weighted by value type in the plan.
+struct AmalgFlops {
+    double schur = 0; // sum over U columns of 2 * m * seglen
+    double trsm = 0;  // sum w (w + 1) m
+    double trsv = 0;  // sum seglen (seglen + 1)
+    double s1 = 0, s2 = 0, w = 0; // diagonal LU: w(w-1)/2, (w-1)w(2w-1)/6, w
+};
+
+// Passes 1 + 2 of the analysis over the supernodes [a0, a1): per-supernode
+// structure facts (parent, symmetric, nested) and the greedy chains, which
+// never cross a1.  lidx / uidx (1x1 reference format, every block of the
+// supernode) need to be valid for [a0, a1) only.  Returns the first
+// supernode of every group in the range; fl (if given) gets the range's
+// original-partition work added.
+std::vector<int> amalg_chains(int64_t n, int ns, const int_t *xsup, const int_t *const *lidx,
+                              const int_t *const *uidx, double zero_frac, int maxw, int a0, int a1,
+                              AmalgFlops *fl);
+
+// Relayout programs (device kernels in amalg_dev.h, host mirrors in the
+// apply functions).  A column range [c0, c1) of one L block column whose
+// rows go through a row map: k_amalg_l dir 0: m[dst + c ld2 + lrow[map + i]]
+// = o[src + c nsupr + i]; dir 1 the reverse.
+struct LColX {
+    int64_t src, dst, map;
+    int32_t nsupr, c0, c1, ld2;
+};
+// <= 64 column segments of one U block row: segment of column entry c0 + j
+// is o[src + ...] (segments back to back), rows [fst, end) with (D index,
+// fst) = ucol[2 (c0 + j)], landing at D[index] + fst in the coarse L (index
+// >= DL0) or U values.
+struct UChunk {
+    int64_t src; // value offset of the chunk's first segment (caller's layout)
+    int64_t c0;  // first column entry in ucol
+    int32_t nc;  // <= 64
+    int32_t end; // xsup[a + 1] of the row
+};
+// a contiguous range copy to[dst + i] = from[src + i], i < len (k_ranges)
+struct GaSpan {
+    int64_t src, dst;
+    int64_t len;
+};
+
 struct Amalg {
     int64_t n = 0;
     int ns1 = 0, ns2 = 0;            // original / merged supernodes
@@ -106,5 +149,89 @@ struct Amalg {
     // original values into zeroed merged arrays, dir 1 compresses back.
     template <typename T> void apply(T *oL, T *oU, T *mL, T *mU, int dir) const;
 };
+
+// ------------------------------------------------------------------ grids
+// Amalgamation of a caller's LUstruct on a Pr x Pc grid (the block-cyclic
+// layout of SRC/pddistribute.c: block (I, J) on rank (I mod Pr, J mod Pc)).
+// No rank holds the whole structure, and a coarse block (grp(I), grp(J))
+// lives on another rank than most of its fine blocks, so:
+//   1. every rank sends the structure of its blocks to the ANALYSIS OWNER of
+//      their supernode (contiguous supernode ranges, one per rank), which
+//      rebuilds the 1x1 index arrays of its range and runs passes 1 + 2 of
+//      the analysis (amalg_chains; chains never cross a range end);
+//   2. the ranges' group starts are all-gathered: every rank knows grp;
+//   3. every fine block goes to the owner of its coarse block -- its
+//      structure once at plan time (the receiver builds its local coarse
+//      LUstruct, the union of what arrives, and the unpack programs), its
+//      values at every upload (pack -> all-to-all -> unpack) and back at
+//      download (the reverse).
+// The phases are pure functions of their inputs, so the CPU tests run all
+// ranks of a grid in one process (ga_simulate) and the engine runs one rank
+// with the transport's all-to-all between them.
+struct GaFine { // one rank's view of the caller's (fine) LUstruct
+    int64_t n = 0;
+    int ns = 0, Pr = 1, Pc = 1, myrow = 0, mycol = 0;
+    const int_t *xsup = nullptr;
+    const int_t *const *lidx = nullptr; // nlc local block columns (reference format) or null
+    const int_t *const *uidx = nullptr; // nlr local block rows
+    int nlc() const { return (ns + Pc - 1) / Pc; }
+    int nlr() const { return (ns + Pr - 1) / Pr; }
+    int P() const { return Pr * Pc; }
+    int iam() const { return myrow * Pc + mycol; }
+};
+using GaStreams = std::vector<std::vector<int64_t>>; // one per peer rank
+
+// supernodes [ga_range(ns, P, r), ga_range(ns, P, r + 1)) are rank r's to analyse
+inline int ga_range(int ns, int P, int r) { return (int)((int64_t)ns * r / P); }
+int ga_owner(int ns, int P, int s);
+
+// phase 1: the structure of my blocks, per analysis owner
+GaStreams ga_structure_out(const GaFine &f);
+// phase 1 (owner): chains of my range from every rank's stream
+struct GaChains {
+    std::vector<int64_t> gstart; // first supernode of every group of my range
+    AmalgFlops fl;               // my range's original-partition work
+};
+GaChains ga_analyse(const GaFine &f, const GaStreams &in, double zero_frac, int maxw);
+// phase 2: the partition from every range's group starts (rank order)
+struct GaPartition {
+    int ns2 = 0;
+    std::vector<int> grp;        // fine supernode -> coarse
+    std::vector<int_t> xsup2, supno2;
+};
+GaPartition ga_partition(const GaFine &f, const std::vector<std::vector<int64_t>> &gstarts);
+// phase 3: one rank's relayout
+struct GaRelay {
+    // ---- send side (pack programs read the caller's local values)
+    GaStreams sstruct;           // per destination: structure of its pieces
+    std::vector<int64_t> scount; // per destination: values
+    std::vector<int64_t> soff;   // per destination: first value in the send buffer (P + 1)
+    std::vector<int64_t> lsrc, usrc; // caller value offset per local block column / row
+    int64_t lval = 0, uval = 0;      // caller local value counts
+    std::vector<LColX> pack_l;       // o = send buffer, m = caller L (k_amalg_l, dir 1)
+    std::vector<int32_t> pack_lrow;  // caller local row of every packed L row
+    std::vector<GaSpan> pack_u;      // caller U -> send buffer
+    // ---- receive side
+    std::vector<int64_t> rcount, roff; // per source: values, first value in the receive buffer
+    int nlc2 = 0, nlr2 = 0;
+    std::vector<std::vector<int_t>> Lidx2, Uidx2; // local coarse block columns / rows (empty: none)
+    std::vector<int64_t> Lvoff2, Uvoff2;          // -1 where empty
+    int64_t lval2 = 0, uval2 = 0;
+    std::vector<LColX> unpack_l;      // o = receive buffer, m = coarse L (k_amalg_l, dir 0)
+    std::vector<int32_t> unpack_lrow; // coarse local row of every received L row
+    std::vector<UChunk> unpack_u;     // o = receive buffer (k_amalg_u, dir 0)
+    std::vector<int32_t> unpack_ucol; // (D index, fst) per received U column
+    std::vector<int64_t> D;
+    int64_t DL0 = 0;
+    int64_t received = 0; // values in the receive buffer
+};
+void ga_send_side(const GaFine &f, const GaPartition &g, GaRelay &r);
+void ga_receive_side(const GaFine &f, const GaPartition &g, const GaStreams &in, GaRelay &r);
+
+// Host mirrors of the device programs (tests).  pack: caller L / U -> send
+// buffer; unpack: receive buffer -> coarse (zeroed by the caller); dir 1
+// of each runs the reverse copy.
+template <typename T> void ga_pack(const GaRelay &r, T *cL, T *cU, T *send, int dir);
+template <typename T> void ga_unpack(const GaRelay &r, T *recv, T *mL, T *mU, int dir);
 
 } // namespace slu

@@ -10,11 +10,6 @@
 
 namespace slu {
 
-// a column range [c0, c1) of one original L block column
-struct LColX {
-    int64_t src, dst, map;
-    int32_t nsupr, c0, c1, ld2;
-};
 
 // dir 0: caller -> coarse, 1: coarse -> caller
 template <typename T>
@@ -40,12 +35,6 @@ __global__ void __launch_bounds__(256) k_amalg_l(const LColX *items, const int32
 // per lane, each lane finding its column by binary search over the prefix
 // sums in LDS; a chunk of long segments goes column by column with the lanes
 // over the segment (coalesced on both sides).
-struct UChunk {
-    int64_t src; // value offset of the chunk's first segment (caller's layout)
-    int64_t c0;  // first column entry in ucol
-    int32_t nc;  // <= 64
-    int32_t end; // xsup[a + 1] of the row
-};
 
 template <typename T>
 __global__ void __launch_bounds__(256) k_amalg_u(const UChunk *chunks, int nchunks,

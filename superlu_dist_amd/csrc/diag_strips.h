@@ -1,0 +1,369 @@
+// Multi-workgroup diagonal-block LU for the levels near the root of the
+// elimination tree, where a level holds one or a few wide supernodes and the
+// diagonal LU -> TRSM -> Schur chain of every level is the critical path
+// (DESIGN §5).  Included by engine.hip after kernels.h.
+//
+// k_diag_lu_f factors a <= 256 x 256 block on ONE workgroup: eight 32-column
+// panels one after the other, each with a serial 32 x 32 register LU, two
+// serial triangular inverses and a trailing update of the whole remaining
+// block through that CU (365 us at w = 256, profiles/r03_diag_micro_phases.txt).
+// Here the block is cut into column strips of 32 and strip q is owned by its
+// own workgroup, which keeps the strip (all w rows) in LDS from start to end:
+//
+//   for p < q:  wait for strip p's flag; read its L part (rows 32p.., the
+//               unit-lower L_pp and L21_p below it) and L_pp^{-1};
+//               U_pq = L_pp^{-1} A_pq (MFMA), A(32p+32.., q) -= L21_p U_pq;
+//   own panel:  unblocked right-looking LU of the strip's rows 32q.. (all
+//               rows below the diagonal at once, one barrier per column,
+//               SRC/pdgstrf2.c:213-269 semantics: tiny-pivot replacement,
+//               reciprocal scaling, a zero pivot leaves its column unscaled
+//               and sets info), then U_qq^{-1} and L_qq^{-1} by 8 x 8 blocks;
+//   publish:    the strip and the two inverses (the TRSMs' dinv blocks) with
+//               write-through stores, then the strip's flag.
+//
+// The critical path per panel is the next strip's update with this panel
+// plus its own panel LU; the other strips apply earlier panels meanwhile.
+// Hand-off protocol (MI355X_MICROARCH.md, inter-workgroup visibility, first
+// row of the sc1 table): every payload byte is stored and loaded with sc1
+// (agent-scope relaxed atomics, 8 / 4 bytes), every storing wave waits for
+// its stores, a workgroup barrier, then one lane stores the flag (sc1); the
+// consumer's lane 0 polls the flag with sc1 loads, a workgroup barrier
+// releases the other waves.
+//
+// Placement: the strips of item i are blocks i % 8 + 8 s + 64 (i / 8), so
+// under the observed round-robin dealing they share one XCD (its L2 then
+// serves the hand-offs; placement is never needed for correctness).  A block
+// only waits for lower-numbered blocks of its own item, dispatched before it.
+// Every wait is bounded: after ~1 s the block records an error and returns,
+// so the grid always drains (the engine then fails the factorization).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "kernels.h"
+
+namespace slu {
+
+constexpr int DS_THREADS = 256, DS_PW = 32, DS_MAXS = FAST_MAXW / DS_PW;
+
+#ifdef SLU_DS_PROBE
+// Diagnostics build only (tools/micro/diag_strips_micro.hip): cycles per
+// phase summed over all working blocks (thread 0's view): 0 flag wait, 1
+// panel read, 2 panel update, 3 own panel LU, 4 inverses, 5 publish.
+__device__ long long slu_ds_tp[8];
+#define DS_PROBE_START() long long ds_t0 = clock64()
+#define DS_PROBE(i)                                                                          \
+    do {                                                                                     \
+        if (threadIdx.x == 0) {                                                              \
+            const long long t = clock64();                                                   \
+            atomicAdd((unsigned long long *)&slu_ds_tp[i], (unsigned long long)(t - ds_t0)); \
+            ds_t0 = t;                                                                       \
+        }                                                                                    \
+    } while (0)
+#else
+#define DS_PROBE_START()
+#define DS_PROBE(i)
+#endif
+
+template <typename T> struct DsBits;
+template <> struct DsBits<double> { using U = unsigned long long; };
+template <> struct DsBits<float> { using U = unsigned int; };
+
+// write-through (sc1) store / L1-bypassing (sc1) load of one element
+// (global_, never flat_: the sc1 forms replace the acquire only as global /
+// buffer instructions)
+template <typename T> __device__ __forceinline__ void st_sc1(T *p, T v) {
+    using U = typename DsBits<T>::U;
+    U u;
+    __builtin_memcpy(&u, &v, sizeof(T));
+    __hip_atomic_store((__attribute__((address_space(1))) U *)p, u, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename T> __device__ __forceinline__ T ld_sc1(const T *p) {
+    using U = typename DsBits<T>::U;
+    const U u = __hip_atomic_load((__attribute__((address_space(1))) U *)p, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT);
+    T v;
+    __builtin_memcpy(&v, &u, sizeof(T));
+    return v;
+}
+
+// lane 0 of wave 0 waits for *f >= epoch; false (and *err set) on timeout
+__device__ __forceinline__ bool ds_wait(const unsigned *f, unsigned epoch, int *err, int *s_ok) {
+    if (threadIdx.x == 0) {
+        int ok = 1;
+        unsigned n = 0;
+        while (__hip_atomic_load((const __attribute__((address_space(1))) unsigned *)f, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT) < epoch) {
+            __builtin_amdgcn_s_sleep(2);
+            if (++n > (1u << 23)) { // ~1 s
+                atomicExch(err, 1);
+                ok = 0;
+                break;
+            }
+        }
+        *s_ok = ok;
+    }
+    __syncthreads();
+    return *s_ok != 0;
+}
+
+// publish: every wave's stores have completed, then one lane sets the flag
+__device__ __forceinline__ void ds_publish(unsigned *f, unsigned epoch) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)
+        __hip_atomic_store((__attribute__((address_space(1))) unsigned *)f, epoch, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Block -> (item, strip) of the XCD-grouped layout above; grid = 64 *
+// ceil(nitems / 8).
+__host__ __device__ inline int ds_grid(int nitems) { return 64 * ((nitems + 7) / 8); }
+
+template <typename T>
+__global__ void __launch_bounds__(DS_THREADS, 1)
+k_diag_strips(const DiagItemF<T> *items, int nitems, unsigned *flags, unsigned epoch, int *err,
+              double thresh, int replace_tiny, int *tiny_count, int *zpiv) {
+    static_assert(std::is_same<T, double>::value || std::is_same<T, float>::value, "real types");
+    constexpr int PW = DS_PW, MW = FAST_MAXW, LD = PW + 1;
+    using Sx = S<T>;
+    using M = Mma<T>;
+    const int b = blockIdx.x, item = (b >> 6) * 8 + (b & 7), q = (b >> 3) & 7;
+    if (item >= nitems) return;
+    const DiagItemF<T> it = items[item];
+    const int w = it.w, ns = (w + PW - 1) / PW;
+    if (q >= ns) return;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int ld = it.ld, c0 = q * PW, pw = min(PW, w - c0);
+    T *A = it.a;
+    unsigned *fl = flags + (size_t)item * DS_MAXS;
+    const int nb = ns;
+    T *dinvU = it.dinv, *dinvLT = it.dinv + (int64_t)nb * PW * PW;
+
+    __shared__ T sS[MW][LD];  // my strip, all w rows
+    __shared__ T sP[MW][LD];  // a received panel's L part (rows 32p..)
+    __shared__ T sLi[PW][LD]; // L_pp^{-1}; later my L_qq^{-1}
+    __shared__ T sUi[PW][LD]; // my U_qq^{-1}
+    __shared__ T sT[2][4][64]; // 8 x 8 block products of the inverse (L, U)
+    __shared__ T s_prow[2][PW];
+    __shared__ T s_rp[PW];
+    __shared__ int s_ok;
+    DS_PROBE_START();
+
+    // ---- my strip (values of earlier kernels: plain loads)
+    stage_loop<DS_THREADS, 4, T>(
+        tid, w * PW,
+        [&](int e, bool ok) {
+            const int r = e % w, c = min(e / w, pw - 1);
+            return keep_if(ok & (e / w < pw), gld(A + min(r, w - 1) + (int64_t)(c0 + c) * ld));
+        },
+        [&](int e, T v) { sS[e % w][e / w] = v; });
+
+    // ---- apply the panels of the strips to my left, in order
+    for (int p = 0; p < q; ++p) {
+        if (!ds_wait(fl + p, epoch, err, &s_ok)) return;
+        const int r0 = p * PW, nr = w - r0;
+        DS_PROBE(0);
+        stage_loop<DS_THREADS, 8, T>(
+            tid, nr * PW,
+            [&](int e, bool ok) {
+                const int ee = min(e, nr * PW - 1);
+                return keep_if(ok, ld_sc1(A + r0 + ee % nr + (int64_t)(r0 + ee / nr) * ld));
+            },
+            [&](int e, T v) { sP[e % nr][e / nr] = v; });
+        stage_loop<DS_THREADS, 4, T>( // dinvLT: [b][a] = Linv[a][b]
+            tid, PW * PW, [&](int e, bool ok) { return keep_if(ok, ld_sc1(dinvLT + (int64_t)p * PW * PW + min(e, PW * PW - 1))); },
+            [&](int e, T v) { sLi[e % PW][e / PW] = v; });
+        __syncthreads();
+        DS_PROBE(1);
+        // U_pq = L_pp^{-1} A(r0:r0+32, strip): 2 x 2 fragments, one per wave
+        {
+            const int fr = wv >> 1, fc = wv & 1;
+            typename M::acc_t acc = M::zero();
+#pragma unroll
+            for (int ks = 0; ks < PW; ks += M::KSTEP) {
+                const int k = ks + (lane >> 4);
+                M::step(acc, sLi[fr * 16 + (lane & 15)][k], sS[r0 + k][fc * 16 + (lane & 15)]);
+            }
+            __syncthreads(); // all reads of rows r0.. before they are overwritten
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                sS[r0 + fr * 16 + M::row(lane, i)][fc * 16 + (lane & 15)] = M::get(acc, i);
+        }
+        __syncthreads();
+        // A(r0+32.., strip) -= L21_p U_pq: fragments (16 rows x 16 columns),
+        // two chains interleaved per wave
+        const int nt = nr - PW, nfr = (nt + 15) / 16, nf = 2 * nfr;
+        for (int f0 = 2 * wv; f0 < nf; f0 += 8) {
+            typename M::acc_t acc[2] = {M::zero(), M::zero()};
+#pragma unroll
+            for (int ks = 0; ks < PW; ks += M::KSTEP) {
+                const int k = ks + (lane >> 4);
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    const int f = min(f0 + u, nf - 1), fr = f >> 1, fc = f & 1;
+                    const int r = fr * 16 + (lane & 15);
+                    M::step(acc[u], keep_if(r < nt, sP[PW + min(r, nt - 1)][k]),
+                            sS[r0 + k][fc * 16 + (lane & 15)]);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int f = f0 + u, fr = f >> 1, fc = f & 1;
+                if (f < nf)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int r = fr * 16 + M::row(lane, i);
+                        if (r < nt) {
+                            T &d = sS[r0 + PW + r][fc * 16 + (lane & 15)];
+                            d = Sx::sub(d, M::get(acc[u], i));
+                        }
+                    }
+            }
+        }
+        __syncthreads();
+        DS_PROBE(2);
+    }
+
+    // ---- my panel: rows c0.. (nrow of them), thread t = row c0 + t
+    const int nrow = w - c0;
+    {
+        T x[PW];
+        const bool mine = tid < nrow;
+#pragma unroll
+        for (int c = 0; c < PW; ++c) x[c] = mine ? sS[c0 + tid][c] : Sx::zero();
+#pragma unroll
+        for (int j = 0; j < PW; ++j) {
+            if (j < pw) { // uniform
+                if (tid == j) { // the pivot row
+                    T piv = x[j];
+                    if (replace_tiny && Sx::abs1(piv) < thresh) {
+                        piv = Sx::thresh(piv, thresh);
+                        atomicAdd(tiny_count, 1);
+                    }
+                    const int z = Sx::iszero(piv);
+                    if (z) atomicMax(&zpiv[it.k], it.fcol + c0 + j + 1);
+                    x[j] = piv;
+                    s_rp[j] = z ? Sx::zero() : Sx::recip(piv);
+#pragma unroll
+                    for (int c = j; c < PW; ++c) s_prow[j & 1][c] = x[c];
+                }
+                __syncthreads();
+                if (tid > j && mine) {
+                    // the whole pivot row in flight at once (the LDS latency
+                    // once per step, not once per pair of columns)
+                    T u[PW];
+#pragma unroll
+                    for (int c = j; c < PW; ++c) u[c] = s_prow[j & 1][c];
+                    const T rp = s_rp[j];
+                    __builtin_amdgcn_sched_barrier(0);
+                    // a zero pivot leaves the column unscaled (SRC/pdgstrf2.c:246-252)
+                    const T l = Sx::iszero(u[j]) ? x[j] : Sx::mul(x[j], rp);
+                    x[j] = l;
+#pragma unroll
+                    for (int c = j + 1; c < PW; ++c) x[c] = Sx::fms(x[c], l, u[c]);
+                }
+            }
+        }
+        if (mine) {
+#pragma unroll
+            for (int c = 0; c < PW; ++c) sS[c0 + tid][c] = x[c];
+        }
+        if (tid >= pw && tid < PW) s_rp[tid] = Sx::zero();
+    }
+    __syncthreads();
+    DS_PROBE(3);
+
+    // ---- L_qq^{-1} (unit lower) and U_qq^{-1} (upper) by 8 x 8 blocks.
+    // Lq(i,k) = sS[c0+i][k] (i > k), Uq(i,k) = sS[c0+i][k] (i <= k); indices
+    // >= pw count as zero (the inverses' rows / columns there are zero).
+    auto Lq = [&](int i, int k) { return keep_if((i < pw) & (k < pw), sS[c0 + min(i, pw - 1)][min(k, pw - 1)]); };
+    for (int e = tid; e < PW * PW; e += DS_THREADS) {
+        sLi[e / PW][e % PW] = Sx::zero();
+        sUi[e / PW][e % PW] = Sx::zero();
+    }
+    __syncthreads();
+    // diagonal 8 x 8 blocks: threads 0..31 columns of L's, 32..63 of U's
+    if (tid < 64) {
+        const int bb = (tid & 31) >> 3, jj = tid & 7, o = bb * 8;
+        T v[8];
+        if (tid < 32) { // L_bb x = e_jj, unit lower
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                T s = i == jj ? one_of(Sx::zero()) : Sx::zero();
+#pragma unroll
+                for (int k = 0; k < i; ++k) s = Sx::fms(s, Lq(o + i, o + k), v[k]);
+                v[i] = i < jj ? Sx::zero() : s;
+            }
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+                if (o + i < pw && o + jj < pw) sLi[o + i][o + jj] = v[i];
+        } else { // U_bb y = e_jj, y(i) = rp(i) (e(i) - sum_{k>i} U(i,k) y(k))
+#pragma unroll
+            for (int i = 7; i >= 0; --i) {
+                T s = i == jj ? one_of(Sx::zero()) : Sx::zero();
+#pragma unroll
+                for (int k = i + 1; k < 8; ++k) s = Sx::fms(s, Lq(o + i, o + k), v[k]);
+                v[i] = i > jj ? Sx::zero() : Sx::mul(s, s_rp[o + i]);
+            }
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+                if (o + i < pw && o + jj < pw) sUi[o + i][o + jj] = v[i];
+        }
+    }
+    __syncthreads();
+    // off-diagonal blocks by distance d: L: X(a,b) = -X(a,a) sum_{c=b}^{a-1} L(a,c) X(c,b);
+    // U: Y(a,b) = -Y(a,a) sum_{c=a+1}^{b} U(a,c) Y(c,b)
+    for (int d = 1; d < 4; ++d) {
+        const int nblk = 4 - d; // pairs per factor
+        for (int e = tid; e < 2 * nblk * 64; e += DS_THREADS) {
+            const int u = e / (nblk * 64), pi = (e / 64) % nblk, i = (e & 63) >> 3, j = e & 7;
+            T s = Sx::zero();
+            if (u == 0) { // L block (a, b) = (pi + d, pi): T = sum_c L(a,c) X(c,b)
+                const int a = pi + d, bq = pi;
+                for (int c = bq; c < a; ++c)
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) s = Sx::fms(s, Lq(a * 8 + i, c * 8 + k), sLi[c * 8 + k][bq * 8 + j]);
+            } else { // U block (a, b) = (pi, pi + d): T = sum_c U(a,c) Y(c,b)
+                const int a = pi, bq = pi + d;
+                for (int c = a + 1; c <= bq; ++c)
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) s = Sx::fms(s, Lq(a * 8 + i, c * 8 + k), sUi[c * 8 + k][bq * 8 + j]);
+            }
+            sT[u][pi][e & 63] = s; // = -T
+        }
+        __syncthreads();
+        for (int e = tid; e < 2 * nblk * 64; e += DS_THREADS) {
+            const int u = e / (nblk * 64), pi = (e / 64) % nblk, i = (e & 63) >> 3, j = e & 7;
+            T s = Sx::zero();
+            if (u == 0) {
+                const int a = pi + d, bq = pi;
+#pragma unroll
+                for (int k = 0; k < 8; ++k) s = Sx::fms(s, sLi[a * 8 + i][a * 8 + k], sT[0][pi][k * 8 + j]);
+                if (a * 8 + i < pw && bq * 8 + j < pw) sLi[a * 8 + i][bq * 8 + j] = Sx::neg(s);
+            } else {
+                const int a = pi, bq = pi + d;
+#pragma unroll
+                for (int k = 0; k < 8; ++k) s = Sx::fms(s, sUi[a * 8 + i][a * 8 + k], sT[1][pi][k * 8 + j]);
+                if (a * 8 + i < pw && bq * 8 + j < pw) sUi[a * 8 + i][bq * 8 + j] = Sx::neg(s);
+            }
+        }
+        __syncthreads();
+    }
+
+    DS_PROBE(4);
+    // ---- publish: the strip, U_qq^{-1} (row-major), (L_qq^{-1})^T (row-major)
+    for (int e = tid; e < w * pw; e += DS_THREADS) {
+        const int r = e % w, c = e / w;
+        st_sc1(A + r + (int64_t)(c0 + c) * ld, sS[r][c]);
+    }
+    for (int e = tid; e < PW * PW; e += DS_THREADS) {
+        const int i = e / PW, jj = e % PW;
+        st_sc1(dinvU + (int64_t)q * PW * PW + e, sUi[i][jj]);
+        st_sc1(dinvLT + (int64_t)q * PW * PW + e, sLi[jj][i]);
+    }
+    ds_publish(fl + q, epoch);
+    DS_PROBE(5);
+}
+
+} // namespace slu

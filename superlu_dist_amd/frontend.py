@@ -308,3 +308,69 @@ class Amalgamation:
         if getattr(self, "h", None):
             lib().slu_amalg_free(self.h)
             self.h = None
+
+
+class GridAmalgamation:
+    """The engine's amalgamation of a Pr x Pc grid's LUStructs (csrc/amalg.h,
+    "grids"): every rank's coarse LUStruct (``merged[k]``, values zero until
+    ``expand``) and the host versions of the relayout -- pack, all-to-all,
+    unpack -- that the grid plan runs on the device with its transport.  All
+    ranks in one process, for tests."""
+
+    def __init__(self, lus, nprow, npcol, zero_frac=0.10, maxw=256):
+        self.lus = list(lus)
+        P = nprow * npcol
+        assert len(self.lus) == P
+        self.nprow, self.npcol = nprow, npcol
+        dt, n = self.lus[0].dtype, self.lus[0].n
+        ptrs = (C.c_void_p * P)(*[lu.ptr for lu in self.lus])
+        self.h = lib().slu_gamalg_create(dt, P, ptrs, n, nprow, npcol, zero_frac, maxw)
+        if not self.h:
+            raise RuntimeError(lib().slu_last_error().decode())
+        npt = DTYPES[dt]
+        self.merged = []
+        for k in range(P):
+            sz = np.zeros(8, np.int64)
+            lib().slu_gamalg_sizes(self.h, k, as_i64p(sz))
+            self.ns1, self.ns2, nli, nui, lval2, uval2, nlc2, nlr2 = map(int, sz)
+            xs, sn = np.zeros(self.ns2 + 1, np.int64), np.zeros(n, np.int64)
+            Li, Ui = np.zeros(max(nli, 1), np.int64), np.zeros(max(nui, 1), np.int64)
+            Lo, Lv = np.zeros(max(nlc2, 1), np.int64), np.zeros(max(nlc2, 1), np.int64)
+            Uo, Uv = np.zeros(max(nlr2, 1), np.int64), np.zeros(max(nlr2, 1), np.int64)
+            lib().slu_gamalg_arrays(self.h, k, as_i64p(xs), as_i64p(sn), as_i64p(Li), as_i64p(Lo),
+                                    as_i64p(Lv), as_i64p(Ui), as_i64p(Uo), as_i64p(Uv))
+            self.merged.append(LUStruct.from_arrays(
+                dt, n, xs, sn, nprow, npcol, k // npcol, k % npcol, Li[:nli], Lo[:nlc2],
+                np.zeros(lval2 + 1, npt), Lv[:nlc2], Ui[:nui], Uo[:nlr2], np.zeros(uval2 + 1, npt),
+                Uv[:nlr2]))
+
+    def flops(self):
+        """the ORIGINAL partition's algorithmic flops (summed over the ranks'
+        analysis ranges, as the grid plans report them)"""
+        out = (C.c_double * 2)()
+        lib().slu_gamalg_flops(self.h, self.lus[0].dtype, out)
+        return out[0] + out[1]
+
+    def _apply(self, o, m, direction):
+        P = len(self.lus)
+        arr = lambda xs: (C.c_void_p * P)(*[x.ctypes.data for x in xs])  # noqa: E731
+        rc = lib().slu_gamalg_apply(self.h, self.lus[0].dtype, arr([a for a, _ in o]), arr([b for _, b in o]),
+                                    arr([a for a, _ in m]), arr([b for _, b in m]), direction)
+        if rc:
+            raise RuntimeError("slu_gamalg_apply")
+
+    def expand(self):
+        """every rank's merged := the caller values routed to it (zeros elsewhere)"""
+        for m in self.merged:
+            m.Lval[:] = 0
+            m.Uval[:] = 0
+        self._apply([(lu.Lval, lu.Uval) for lu in self.lus], [(m.Lval, m.Uval) for m in self.merged], 0)
+
+    def compress(self, outs):
+        """outs[k] = (L, U) arrays in rank k's caller layout := the merged values"""
+        self._apply(outs, [(m.Lval, m.Uval) for m in self.merged], 1)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().slu_gamalg_free(self.h)
+            self.h = None

@@ -135,6 +135,13 @@ def lib():
         "slu_amalg_free": (None, [P]),
         "slu_symb_ref_info": (None, [P, C.POINTER(C.c_double)]),
         "slu_amalg_flops": (None, [P, C.c_int, C.POINTER(C.c_double)]),
+        "slu_gamalg_create": (P, [C.c_int, C.c_int, C.POINTER(P), C.c_int64, C.c_int, C.c_int,
+                                  C.c_double, C.c_int]),
+        "slu_gamalg_sizes": (None, [P, C.c_int, c_i64p]),
+        "slu_gamalg_arrays": (None, [P, C.c_int] + [c_i64p] * 8),
+        "slu_gamalg_flops": (None, [P, C.c_int, C.POINTER(C.c_double)]),
+        "slu_gamalg_apply": (C.c_int, [P, C.c_int] + [C.POINTER(P)] * 4 + [C.c_int]),
+        "slu_gamalg_free": (None, [P]),
         "slu_distribute_glu": (P, [C.c_int, C.c_int64, c_i64p, c_i64p, c_i64p, c_i64p, c_i64p,
                                    c_i64p, c_i64p, c_i64p, P, C.c_int, C.c_int, C.c_int, C.c_int]),
         "slu_lustruct_build": (P, [C.c_int, C.c_int64, C.c_int64, c_i64p, c_i64p, C.c_int,
