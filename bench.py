@@ -99,13 +99,13 @@ def build_lu(workload, nx, pr, pc, myrow, mycol, ordering="grid", symbolic="refe
     if symbolic == "reference":
         # what pdgssvx hands pdgstrf for this perm_c (ColPerm = MY_PERMC):
         # the reference's sp_colorder + symbfact, laid out by its pddistribute
-        # (bit-exact restatements, csrc/symbolic.cpp, csrc/distribute.cpp).
-        # 1x1: that LUstruct as is (the plan amalgamates it on the device,
-        # csrc/amalg.h).  Grids: the grid plan has no device relayout, so the
-        # same coarse partition is laid out by pddistribute's rules instead
-        # (SLU_SYMB_COARSE); the rate counts the reference partition's work.
-        S = Symbolic(A, perm, 60, 256, reference=True,
-                     coarse=pr * pc > 1 if coarse is None else coarse)
+        # (bit-exact restatements, csrc/symbolic.cpp, csrc/distribute.cpp), on
+        # every grid as is: the plan amalgamates it (1x1: csrc/amalg.h; 2D
+        # grids: the grid relayout of the same header).  3D grids factor the
+        # caller's partition, so --grid3d lays the coarse partition out with
+        # pddistribute's rules instead (coarse=True, SLU_SYMB_COARSE); the
+        # rate always counts the reference partition's work.
+        S = Symbolic(A, perm, 60, 256, reference=True, coarse=bool(coarse))
     else:
         # the library front-end's amalgamated partition (chains with <= 10 %
         # explicit zeros; graph ordering: chains through multi-child columns,
@@ -381,7 +381,7 @@ def main():
     gname = f"{pr}x{pc}" + (f"x{pz}" if pz > 1 else "")
     log(f"front-end {args.workload} nx={args.nx} grid {gname}")
     A, S, lu, perm = build_lu(args.workload, args.nx, pr, pc, myrow, mycol, args.ordering,
-                              args.symbolic, coarse=world > 1)
+                              args.symbolic, coarse=pz > 1)
     t_front = time.time() - t0
     log(f"front-end {t_front:.1f} s, {S.nsupers} supernodes")
     if world == 1:

@@ -289,35 +289,55 @@ inline uint64_t mix(uint64_t h, uint64_t v) {
     return h * 0xBF58476D1CE4E5B9ull;
 }
 
-// digest of the 1x1 structure: xsup and every L / U index array (host threads)
-template <typename LUS> uint64_t structure_digest(LUS *lu, int n) {
+// digest of this rank's structure: xsup and every local L / U index array
+// (host threads), the grid, and where the values live
+template <typename LUS> uint64_t structure_digest(LUS *lu, int n, const gridinfo_t *grid) {
     const int_t *xsup = lu->Glu_persist->xsup;
     const int ns = (int)(lu->Glu_persist->supno[n - 1] + 1);
-    std::vector<uint64_t> part(ns);
+    const int Pr = (int)grid->nprow, Pc = (int)grid->npcol;
+    const int nlc = (ns + Pc - 1) / Pc, nlr = (ns + Pr - 1) / Pr, nb = std::max(nlc, nlr);
+    std::vector<uint64_t> part(nb);
     auto idx = [](const int_t *ix, i64 len) {
         uint64_t h = 0x12345;
         for (i64 i = 0; i < len; ++i) h = mix(h, (uint64_t)ix[i]);
         return h;
     };
-    slu::parallel_for(ns, [&](int s) {
-        uint64_t h = mix((uint64_t)s, (uint64_t)xsup[s + 1]);
-        if (const int_t *ix = lu->Llu->Lrowind_bc_ptr[s]) {
-            i64 p = SLU_BC_HEADER;
-            for (i64 b = 0; b < ix[0]; ++b) p += SLU_LB_DESCRIPTOR + ix[p + 1];
-            h = mix(h, idx(ix, p));
-        }
-        if (const int_t *ux = lu->Llu->Ufstnz_br_ptr[s]) h = mix(h, idx(ux, ux[2]));
-        // and where the values live: a plan keeps host pointers (the D2H
-        // unpack targets), so another LUstruct of the same pattern is a miss
-        h = mix(h, (uint64_t)(uintptr_t)lu->Llu->Lnzval_bc_ptr[s]);
-        h = mix(h, (uint64_t)(uintptr_t)lu->Llu->Unzval_br_ptr[s]);
-        part[s] = h;
+    slu::parallel_for(nb, [&](int j) {
+        uint64_t h = mix((uint64_t)j, (uint64_t)xsup[std::min(j + 1, ns)]);
+        if (j < nlc)
+            if (const int_t *ix = lu->Llu->Lrowind_bc_ptr[j]) {
+                i64 p = SLU_BC_HEADER;
+                for (i64 b = 0; b < ix[0]; ++b) p += SLU_LB_DESCRIPTOR + ix[p + 1];
+                h = mix(h, idx(ix, p));
+                // and where the values live: a plan keeps host pointers (the
+                // D2H unpack targets), so another LUstruct of the same
+                // pattern is a miss
+                h = mix(h, (uint64_t)(uintptr_t)lu->Llu->Lnzval_bc_ptr[j]);
+            }
+        if (j < nlr)
+            if (const int_t *ux = lu->Llu->Ufstnz_br_ptr[j]) {
+                h = mix(h, idx(ux, ux[2]));
+                h = mix(h, (uint64_t)(uintptr_t)lu->Llu->Unzval_br_ptr[j]);
+            }
+        part[j] = h;
     });
     uint64_t h = mix((uint64_t)n, (uint64_t)ns);
     h = mix(h, (uint64_t)(uintptr_t)lu);
     h = mix(h, (uint64_t)(uintptr_t)lu->Llu);
+    h = mix(h, ((uint64_t)Pr << 32) | (uint64_t)Pc);
+    h = mix(h, (uint64_t)grid->iam);
+    h = mix(h, (uint64_t)(uintptr_t)grid->comm); // (the plan holds this grid's transport)
     for (uint64_t v : part) h = mix(h, v);
     return h;
+}
+
+// every rank of the grid reuses its cached plan, or none does (building a
+// plan is collective)
+bool all_ranks(bool mine, gridinfo_t *grid) {
+    if (grid->nprow * grid->npcol == 1) return mine;
+    int in = mine ? 1 : 0, out = 0;
+    mpi().allreduce(&in, &out, 1, MPI_INT, MPI_MIN, grid->comm);
+    return out == 1;
 }
 
 // process CPU time (all threads) and thread count, for SUPERLU_MI355X_TIMING
@@ -363,14 +383,20 @@ int_t pxgstrf(int dtype, const char *name, superlu_dist_options_t *options, int 
     try {
         const bool one = grid->nprow * grid->npcol == 1;
         const char *pc = getenv("SUPERLU_MI355X_PLAN_CACHE");
-        const bool cache = one && !(pc && !strcmp(pc, "0"));
+        const bool cache = !(pc && !strcmp(pc, "0"));
         const int rt = options->ReplaceTinyPivot == SLU_YES;
         uint64_t dg = 0;
         if (cache) {
-            dg = structure_digest(LUstruct, n);
+            dg = structure_digest(LUstruct, n, grid);
+            bool hit;
+            {
+                std::lock_guard<std::mutex> lk(g_cache_mu);
+                hit = g_cache.plan && g_cache.digest == dg && g_cache.dtype == dtype && g_cache.n == n &&
+                      g_cache.replace_tiny == rt;
+            }
+            hit = all_ranks(hit, grid);
             std::lock_guard<std::mutex> lk(g_cache_mu);
-            if (g_cache.plan && g_cache.digest == dg && g_cache.dtype == dtype && g_cache.n == n &&
-                g_cache.replace_tiny == rt) {
+            if (hit) {
                 plan = g_cache.plan; // same structure: reuse (values are uploaded again below)
                 g_cache.plan = nullptr;
             } else {
@@ -390,7 +416,7 @@ int_t pxgstrf(int dtype, const char *name, superlu_dist_options_t *options, int 
                 da = &g_deva;
         }
         const char *hf = getenv("SUPERLU_MI355X_HOST_FACTORS");
-        const bool keep_on_device = da && cache && !(hf && atoi(hf) == 1);
+        const bool keep_on_device = one && da && cache && !(hf && atoi(hf) == 1);
         bool pattern_ready = false;
         const bool reused = plan != nullptr;
         tp[1] = clk::now();
@@ -717,9 +743,17 @@ void pxgstrs(int dtype, const char *name, int_t n, LUS *LU, xScalePermstruct_t *
     bool cached = false;
     try {
         const bool one = grid->nprow * grid->npcol == 1;
-        if (one) {
-            std::lock_guard<std::mutex> lk(g_cache_mu);
-            if (g_cache.plan && g_cache.lu == LU && g_cache.dtype == dtype && g_cache.n == n) {
+        {
+            // the plan of the last pdgstrf on this LUstruct still holds its
+            // factors in HBM (grids too: its coarse storage); every rank of a
+            // grid must agree, the solve is collective
+            bool hit;
+            {
+                std::lock_guard<std::mutex> lk(g_cache_mu);
+                hit = g_cache.plan && g_cache.key == lu_key(LU) && g_cache.dtype == dtype && g_cache.n == n;
+            }
+            if (all_ranks(hit, grid)) {
+                std::lock_guard<std::mutex> lk(g_cache_mu);
                 plan = g_cache.plan;
                 cached = true;
             }

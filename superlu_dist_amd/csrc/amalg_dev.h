@@ -95,3 +95,56 @@ __global__ void __launch_bounds__(256) k_amalg_u(const UChunk *chunks, int nchun
 }
 
 } // namespace slu
+
+namespace slu {
+
+// Contiguous range copies (GaSpan), one wave per chunk of <= 64 ranges:
+// dir 0 b[dst + i] = a[src + i], dir 1 the reverse.  Short chunks (<= 256
+// values) go one value per lane (binary search over the prefix sums), long
+// ones range by range with the lanes over the values.  The grid plan's
+// pack of the caller's U blocks into the send buffer (and its reverse).
+template <typename T>
+__global__ void __launch_bounds__(256) k_ranges(const GaSpan *spans, int nspans, T *a, T *b, int dir) {
+    __shared__ int64_t s_incl[4][64], s_src[4][64], s_dst[4][64];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t c0 = ((int64_t)blockIdx.x * 4 + w) * 64;
+    if (c0 >= nspans) return; // (whole waves: no barrier below)
+    const int nc = (int)min((int64_t)64, (int64_t)nspans - c0);
+    GaSpan sp{0, 0, 0};
+    if (lane < nc) sp = spans[c0 + lane];
+    int64_t incl = sp.len;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int64_t v = __shfl_up(incl, d);
+        if (lane >= d) incl += v;
+    }
+    const int64_t total = __shfl(incl, 63);
+    if (total <= 256) {
+        s_incl[w][lane] = incl;
+        s_src[w][lane] = sp.src;
+        s_dst[w][lane] = sp.dst;
+        __builtin_amdgcn_wave_barrier();
+        for (int t = lane; t < total; t += 64) {
+            int lo = 0, hi = 63;
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (s_incl[w][mid] > t) hi = mid;
+                else lo = mid + 1;
+            }
+            const int64_t o = t - (lo ? s_incl[w][lo - 1] : 0);
+            const int64_t s = s_src[w][lo] + o, d = s_dst[w][lo] + o;
+            if (dir == 0) b[d] = a[s];
+            else a[s] = b[d];
+        }
+        return;
+    }
+    for (int j = 0; j < nc; ++j) {
+        const int64_t s = __shfl(sp.src, j), d = __shfl(sp.dst, j), len = __shfl(sp.len, j);
+        for (int64_t i = lane; i < len; i += 64) {
+            if (dir == 0) b[d + i] = a[s + i];
+            else a[s + i] = b[d + i];
+        }
+    }
+}
+
+} // namespace slu

@@ -288,6 +288,55 @@ struct Xport {
         }
         ops.clear();
     }
+    // plan-time all-to-all of variable-length int64 blobs in the world
+    // group: out[q] goes to rank q, the result's [p] came from rank p.  Sizes
+    // first (an all-gather), then one section per ordered pair, queued in
+    // the same order on every rank.
+    vector<vector<i64>> alltoallv(const vector<vector<i64>> &out) {
+        const int P = gsize(G_WORLD), me = grank(G_WORLD);
+        SLU_REQUIRE((int)out.size() == P && P <= 32, "alltoallv over %d ranks", P);
+        vector<vector<i64>> in(P);
+        in[me] = out[me];
+        if (P == 1) return in;
+        vector<i64> mine(P);
+        for (int q = 0; q < P; ++q) mine[q] = (i64)out[q].size();
+        const vector<vector<i64>> sz = allgatherv(G_WORLD, mine); // sz[p][q]
+        for (int p = 0; p < P; ++p)
+            if (p != me) in[p].resize(sz[p][me]);
+        if (host_mem) {
+            for (int p = 0; p < P; ++p)
+                for (int q = 0; q < P; ++q) {
+                    if (p == q || !sz[p][q]) continue;
+                    void *buf = me == p ? (void *)out[q].data() : me == q ? (void *)in[p].data() : nullptr;
+                    section(G_WORLD, p, 1u << q, buf, (size_t)sz[p][q] * sizeof(i64));
+                }
+            flush();
+            return in;
+        }
+        vector<i64> so(P + 1, 0), ro(P + 1, 0);
+        for (int q = 0; q < P; ++q) {
+            so[q + 1] = so[q] + (q == me ? 0 : sz[me][q]);
+            ro[q + 1] = ro[q] + (q == me ? 0 : sz[q][me]);
+        }
+        DevBuf<i64> ds, dr;
+        ds.alloc(std::max<i64>(so[P], 1));
+        dr.alloc(std::max<i64>(ro[P], 1));
+        for (int q = 0; q < P; ++q)
+            if (q != me && sz[me][q])
+                HIPCHK(hipMemcpy(ds.p + so[q], out[q].data(), sz[me][q] * sizeof(i64), hipMemcpyHostToDevice));
+        for (int p = 0; p < P; ++p)
+            for (int q = 0; q < P; ++q) {
+                if (p == q || !sz[p][q]) continue;
+                void *buf = me == p ? (void *)(ds.p + so[q]) : me == q ? (void *)(dr.p + ro[p]) : nullptr;
+                section(G_WORLD, p, 1u << q, buf, (size_t)sz[p][q] * sizeof(i64));
+            }
+        flush();
+        HIPCHK(hipStreamSynchronize(s));
+        for (int p = 0; p < P; ++p)
+            if (p != me && sz[p][me])
+                HIPCHK(hipMemcpy(in[p].data(), dr.p + ro[p], sz[p][me] * sizeof(i64), hipMemcpyDeviceToHost));
+        return in;
+    }
     // plan-time all-gather of variable-length int64 blobs within group g
     vector<vector<i64>> allgatherv(int g, const vector<i64> &mine) {
         const int P = gsize(g), me = grank(g);
@@ -3948,19 +3997,341 @@ struct AmalgPlan : PlanBase {
     }
 };
 
-// The plan for a caller's LUstruct: the amalgamated one on 1x1 grids when
-// chains merge (SLU_AMALG=0 turns it off; SLU_AMALG_ZERO sets the explicit
-// zero fraction, default 0.10), else the plain plan.
+// ------------------------------------------------------------ grid amalgamation
+// The coarse partition on a Pr x Pc grid (csrc/amalg.h, "grids"): the
+// analysis runs on the ranks' supernode ranges, every fine block goes to
+// the owner of its coarse block (structure once, values at every upload and
+// back at download), and the inner Plan -- the ordinary grid plan -- runs on
+// each rank's local coarse LUstruct with the caller's communicator.  The
+// value relayout on the device: pack (k_amalg_l over the caller's L with a
+// row map, k_ranges over its U blocks) into one send buffer ordered by
+// destination, one section per ordered rank pair over the transport (RCCL
+// send / receive on the world communicator, or the host transports), unpack
+// (k_amalg_l / k_amalg_u) into the zeroed coarse storage; download runs the
+// same programs backwards.
+template <typename T, typename HT, typename LocalLU, typename LUS>
+struct GridAmalgPlan : PlanBase {
+    using Inner = Plan<T, HT, LocalLU, LUS>;
+    LUS *LU = nullptr;
+    int n = 0, ns = 0, Pr = 1, Pc = 1, iam = 0, P = 1;
+    slu_comm *comm = nullptr;
+    slu_engine_opts opts{};
+    bool dry = false;
+    GaFine f;
+    vector<const int_t *> flidx, fuidx;
+    GaChains ch;
+    GaPartition g;
+    GaRelay r;
+    vector<vector<i64>> cnt; // cnt[p][q]: values rank p sends rank q
+    // the coarse LUstruct the inner plan reads (index arrays only)
+    LUS mlu{};
+    LocalLU mllu{};
+    Glu_persist_t mglu{};
+    vector<int_t *> mlidx, muidx;
+    std::unique_ptr<Inner> in;
+    Xport X;
+    hipStream_t xs = nullptr; // plan-time exchanges before the inner plan exists
+    // device: caller layout, send / receive buffers, programs
+    DevBuf<T> d_oL, d_oU, d_send, d_recv;
+    DevBuf<LColX> d_pl, d_ul;
+    DevBuf<int32_t> d_plrow, d_ulrow, d_uucol;
+    DevBuf<GaSpan> d_pu;
+    DevBuf<UChunk> d_uu;
+    DevBuf<i64> d_D;
+    double t_relay_plan = 0, t_expand = 0, t_compress = 0, t_h2d = 0, t_d2h = 0;
+    bool coarse_current = false;
+
+    static double ms_since(std::chrono::steady_clock::time_point t0) {
+        return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    }
+
+    // nullptr when nothing merges (every rank decides the same: the
+    // partition is all-gathered)
+    static GridAmalgPlan *make(LUS *lu, int n_, int pr, int pc, int iam_, slu_comm *c,
+                               const slu_engine_opts *o, double zero_frac, int maxw) {
+        const auto t0 = std::chrono::steady_clock::now();
+        std::unique_ptr<GridAmalgPlan> G(new GridAmalgPlan);
+        G->LU = lu;
+        G->n = n_;
+        G->Pr = pr;
+        G->Pc = pc;
+        G->P = pr * pc;
+        G->iam = iam_;
+        G->comm = c;
+        if (o) G->opts = *o;
+        G->dry = G->opts.schedule_only != 0;
+        SLU_REQUIRE(c && (c->world || c->host_fn || c->host_p2p), "a %dx%d grid needs a communicator", pr, pc);
+        SLU_REQUIRE(G->P <= 32, "grid amalgamation: at most 32 ranks");
+        if (!G->dry) {
+            HIPCHK(hipSetDevice(c->device));
+            HIPCHK(hipStreamCreateWithFlags(&G->xs, hipStreamNonBlocking));
+        }
+        G->X.c = c;
+        G->X.s = G->xs;
+        G->X.host_mem = G->dry;
+        LocalLU *L = lu->Llu;
+        GaFine &f = G->f;
+        f.n = n_;
+        f.ns = G->ns = (int)(lu->Glu_persist->supno[n_ - 1] + 1);
+        f.Pr = pr;
+        f.Pc = pc;
+        f.myrow = iam_ / pc;
+        f.mycol = iam_ % pc;
+        f.xsup = lu->Glu_persist->xsup;
+        G->flidx.assign(L->Lrowind_bc_ptr, L->Lrowind_bc_ptr + f.nlc());
+        G->fuidx.assign(L->Ufstnz_br_ptr, L->Ufstnz_br_ptr + f.nlr());
+        f.lidx = G->flidx.data();
+        f.uidx = G->fuidx.data();
+        // 1. structure to the analysis owners, chains of my range
+        G->ch = ga_analyse(f, G->X.alltoallv(ga_structure_out(f)), zero_frac, maxw);
+        // 2. the partition
+        G->g = ga_partition(f, G->X.allgatherv(G_WORLD, G->ch.gstart));
+        if (G->g.ns2 == G->ns) return nullptr;
+        // 3. relayout: my pieces' structure to the coarse owners, my coarse
+        // LUstruct and programs from what arrives; everybody's counts
+        ga_send_side(f, G->g, G->r);
+        ga_receive_side(f, G->g, G->X.alltoallv(G->r.sstruct), G->r);
+        G->cnt = G->X.allgatherv(G_WORLD, G->r.scount);
+        for (int p = 0; p < G->P; ++p)
+            SLU_REQUIRE(G->cnt[p][iam_] == G->r.rcount[p], "grid amalgamation: counts %d -> %d", p, iam_);
+        G->t_relay_plan = ms_since(t0);
+        G->build_inner();
+        if (!G->dry) G->build_programs();
+        G->sync_stats();
+        G->stats.t_plan_ms = ms_since(t0);
+        return G.release();
+    }
+
+    void build_inner() {
+        mlidx.assign(r.nlc2, nullptr);
+        muidx.assign(r.nlr2, nullptr);
+        for (int j = 0; j < r.nlc2; ++j)
+            if (!r.Lidx2[j].empty()) mlidx[j] = r.Lidx2[j].data();
+        for (int j = 0; j < r.nlr2; ++j)
+            if (!r.Uidx2[j].empty()) muidx[j] = r.Uidx2[j].data();
+        mglu.xsup = g.xsup2.data();
+        mglu.supno = g.supno2.data();
+        mllu.Lrowind_bc_ptr = mlidx.data();
+        mllu.Ufstnz_br_ptr = muidx.data();
+        mlu.Glu_persist = &mglu;
+        mlu.Llu = &mllu;
+        slu_engine_opts io = opts;
+        io.overlap_upload = io.overlap_download = 0;
+        in.reset(new Inner(&mlu, n, Pr, Pc, iam, comm, &io));
+        if (!dry) X.s = in->stream; // the relayout's sections go on the kernels' stream
+    }
+
+    template <typename V> static void up(DevBuf<V> &d, const vector<V> &h) {
+        if (h.empty()) d.upload(vector<V>(1));
+        else d.upload(h);
+    }
+    void build_programs() {
+        up(d_pl, r.pack_l);
+        up(d_plrow, r.pack_lrow);
+        up(d_pu, r.pack_u);
+        up(d_ul, r.unpack_l);
+        up(d_ulrow, r.unpack_lrow);
+        up(d_uu, r.unpack_u);
+        up(d_uucol, r.unpack_ucol);
+        up(d_D, r.D);
+        d_send.alloc(std::max<i64>(r.soff[P], 1));
+        d_recv.alloc(std::max<i64>(r.received, 1));
+    }
+    void ensure_o() {
+        if (d_oL.p) return;
+        d_oL.alloc(std::max<i64>(r.lval, 1));
+        d_oU.alloc(std::max<i64>(r.uval, 1));
+    }
+    // the caller's local values <-> d_oL / d_oU
+    vector<Xfer> xfers() {
+        ensure_o();
+        LocalLU *L = LU->Llu;
+        vector<Xfer> v;
+        for (int j = 0; j < f.nlc(); ++j)
+            if (L->Lrowind_bc_ptr[j] && r.lsrc[j + 1] > r.lsrc[j])
+                v.push_back({(char *)(d_oL.p + r.lsrc[j]), (char *)L->Lnzval_bc_ptr[j],
+                             (size_t)(r.lsrc[j + 1] - r.lsrc[j]) * sizeof(T)});
+        for (int j = 0; j < f.nlr(); ++j)
+            if (L->Ufstnz_br_ptr[j] && r.usrc[j + 1] > r.usrc[j])
+                v.push_back({(char *)(d_oU.p + r.usrc[j]), (char *)L->Unzval_br_ptr[j],
+                             (size_t)(r.usrc[j + 1] - r.usrc[j]) * sizeof(T)});
+        return merge_xfers(std::move(v));
+    }
+
+    void launch_l(const DevBuf<LColX> &items, size_t nitems, const DevBuf<int32_t> &lrow, T *o, T *m, int dir,
+                  hipStream_t st) {
+        if (nitems)
+            hipLaunchKernelGGL((k_amalg_l<T>), dim3((unsigned)nitems), dim3(256), 0, st, items.p, lrow.p, o, m, dir);
+    }
+    // the value all-to-all: forward p -> q from send to receive regions,
+    // backward q -> p the other way; my own pair is a device copy
+    void exchange(bool forward) {
+        hipStream_t st = in->stream;
+        const int me = iam;
+        if (r.scount[me])
+            HIPCHK(hipMemcpyAsync(forward ? d_recv.p + r.roff[me] : d_send.p + r.soff[me],
+                                  forward ? d_send.p + r.soff[me] : d_recv.p + r.roff[me],
+                                  (size_t)r.scount[me] * sizeof(T), hipMemcpyDeviceToDevice, st));
+        for (int p = 0; p < P; ++p)
+            for (int q = 0; q < P; ++q) {
+                if (p == q || !cnt[p][q]) continue;
+                const int root = forward ? p : q, dest = forward ? q : p;
+                T *buf = nullptr;
+                if (me == p) buf = d_send.p + r.soff[q];
+                else if (me == q) buf = d_recv.p + r.roff[p];
+                X.section(G_WORLD, root, 1u << dest, buf, (size_t)cnt[p][q] * sizeof(T));
+            }
+        X.flush();
+    }
+
+    void expand() { // caller layout (d_oL / d_oU) -> coarse
+        const auto t0 = std::chrono::steady_clock::now();
+        hipStream_t st = in->stream;
+        launch_l(d_pl, r.pack_l.size(), d_plrow, d_send.p, d_oL.p, 1, st);
+        if (!r.pack_u.empty())
+            hipLaunchKernelGGL((k_ranges<T>), dim3((unsigned)((r.pack_u.size() + 255) / 256)), dim3(256), 0, st,
+                               d_pu.p, (int)r.pack_u.size(), d_oU.p, d_send.p, 0);
+        HIPCHK(hipGetLastError());
+        exchange(true);
+        HIPCHK(hipMemsetAsync(in->d_L.p, 0, in->d_L.bytes(), st));
+        HIPCHK(hipMemsetAsync(in->d_U.p, 0, in->d_U.bytes(), st));
+        launch_l(d_ul, r.unpack_l.size(), d_ulrow, d_recv.p, in->d_L.p, 0, st);
+        if (!r.unpack_u.empty())
+            hipLaunchKernelGGL((k_amalg_u<T>), dim3((unsigned)((r.unpack_u.size() + 3) / 4)), dim3(256), 0, st,
+                               d_uu.p, (int)r.unpack_u.size(), d_uucol.p, d_D.p, (i64)r.DL0, d_recv.p, in->d_L.p,
+                               in->d_U.p, 0);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipStreamSynchronize(st));
+        t_expand = ms_since(t0);
+    }
+    void compress() { // coarse -> caller layout
+        const auto t0 = std::chrono::steady_clock::now();
+        hipStream_t st = in->stream;
+        launch_l(d_ul, r.unpack_l.size(), d_ulrow, d_recv.p, in->d_L.p, 1, st);
+        if (!r.unpack_u.empty())
+            hipLaunchKernelGGL((k_amalg_u<T>), dim3((unsigned)((r.unpack_u.size() + 3) / 4)), dim3(256), 0, st,
+                               d_uu.p, (int)r.unpack_u.size(), d_uucol.p, d_D.p, (i64)r.DL0, d_recv.p, in->d_L.p,
+                               in->d_U.p, 1);
+        HIPCHK(hipGetLastError());
+        exchange(false);
+        launch_l(d_pl, r.pack_l.size(), d_plrow, d_send.p, d_oL.p, 0, st);
+        if (!r.pack_u.empty())
+            hipLaunchKernelGGL((k_ranges<T>), dim3((unsigned)((r.pack_u.size() + 255) / 256)), dim3(256), 0, st,
+                               d_pu.p, (int)r.pack_u.size(), d_oU.p, d_send.p, 1);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipStreamSynchronize(st));
+        t_compress = ms_since(t0);
+    }
+
+    void sync_stats() {
+        stats = in->stats;
+        const bool cp = sizeof(T) == 16;
+        const AmalgFlops &F = ch.fl; // my analysis range's share of the caller partition's work
+        stats.schur_flops = F.schur * (cp ? 4.0 : 1.0);
+        stats.panel_flops = (cp ? 6 * F.s1 + 10 * F.w + 8 * F.s2 : F.s1 + 2 * F.s2) +
+                            (cp ? 4.0 : 1.0) * F.trsm + F.trsv;
+        stats.nsupers_in = ns;
+        i64 groups = 0;
+        for (size_t i = 0; i < ch.gstart.size(); ++i) {
+            const i64 e = i + 1 < ch.gstart.size() ? ch.gstart[i + 1]
+                                                   : (i64)ga_range(ns, P, iam + 1);
+            groups += e - ch.gstart[i] > 1;
+        }
+        stats.amalg_groups = groups;
+        stats.t_amalg_ms = t_relay_plan;
+        stats.t_expand_ms = t_expand;
+        stats.t_compress_ms = t_compress;
+        stats.t_upload_ms = t_h2d;
+        stats.t_d2h_ms = t_d2h;
+        stats.h2d_bytes = (double)(r.lval + r.uval) * sizeof(T);
+        stats.d2h_bytes = stats.h2d_bytes;
+    }
+
+    void upload() override {
+        const auto t0 = std::chrono::steady_clock::now();
+        staged_h2d(xfers(), comm->device);
+        t_h2d = ms_since(t0);
+        expand();
+        in->vstate = 1;
+        in->d_acur = nullptr;
+        in->host_current = false;
+        coarse_current = false;
+        sync_stats();
+    }
+    void adopt_factors() override {
+        upload();
+        in->sync();
+        in->vstate = 2;
+    }
+    void factor(double anorm, int *info, int *tiny) override {
+        in->factor(anorm, info, tiny);
+        coarse_current = true;
+        sync_stats();
+    }
+    void download() override {
+        in->sync();
+        if (coarse_current) {
+            ensure_o();
+            compress();
+            coarse_current = false;
+        }
+        const auto t0 = std::chrono::steady_clock::now();
+        for (const Xfer &x : xfers()) HIPCHK(hipMemcpy(x.host, x.dev, x.bytes, hipMemcpyDeviceToHost));
+        t_d2h = ms_since(t0);
+        sync_stats();
+    }
+    void snapshot() override { in->snapshot(); }
+    void restore() override {
+        in->restore();
+        coarse_current = true;
+    }
+    void sync() override { in->sync(); }
+    void set_timing(int timing, int serial) override { in->set_timing(timing, serial); }
+    void solve(void *b, int64_t ldb, int nrhs) override {
+        in->solve(b, ldb, nrhs);
+        sync_stats();
+    }
+    void set_a_pattern(int64_t ncol, const int64_t *xa, const int64_t *asub) override {
+        in->set_a_pattern(ncol, xa, asub);
+        sync_stats();
+    }
+    void fill_a(const void *a, int on_device) override {
+        in->fill_a(a, on_device);
+        coarse_current = true;
+        sync_stats();
+    }
+    void refine(const void *b, void *x, int64_t ld, int nrhs, double *berr, int *steps) override {
+        in->refine(b, x, ld, nrhs, berr, steps);
+        sync_stats();
+    }
+    void check_exchange(int64_t *nsec, int64_t *nbytes) override {
+        in->check_exchange(nsec, nbytes);
+        sync_stats();
+    }
+    ~GridAmalgPlan() override {
+        in.reset();
+        if (xs) (void)hipStreamDestroy(xs);
+    }
+};
+
+// The plan for a caller's LUstruct: the amalgamated one when chains merge
+// (1x1: AmalgPlan; 2D grids: GridAmalgPlan; SLU_AMALG=0 turns it off;
+// SLU_AMALG_ZERO sets the explicit zero fraction, default 0.10), else the
+// plain plan.  3D grids factor the caller's partition (its forests).
 template <typename P> PlanBase *make_plan_any(void *LU, int n, int pr, int pc, int iam, slu_comm *c,
                                               const slu_engine_opts *o) {
     using A = AmalgPlan<typename P::value_type, typename P::host_type, typename P::local_type,
                         typename P::lus_type>;
+    using GA = GridAmalgPlan<typename P::value_type, typename P::host_type, typename P::local_type,
+                             typename P::lus_type>;
     const char *e = getenv("SLU_AMALG");
     const bool on = !(e && !strcmp(e, "0"));
+    const char *z = getenv("SLU_AMALG_ZERO");
+    const double zf = z ? atof(z) : 0.10;
     if (on && pr * pc == 1 && !(o && o->schedule_only) && !(c && c->npdep > 1)) {
-        const char *z = getenv("SLU_AMALG_ZERO");
-        if (PlanBase *p = A::make((typename P::lus_type *)LU, n, o, z ? atof(z) : 0.10, FAST_MAXW))
-            return p;
+        if (PlanBase *p = A::make((typename P::lus_type *)LU, n, o, zf, FAST_MAXW)) return p;
+    } else if (on && pr * pc > 1 && !(c && c->npdep > 1)) {
+        if (PlanBase *p = GA::make((typename P::lus_type *)LU, n, pr, pc, iam, c, o, zf, FAST_MAXW)) return p;
     }
     return make_plan<P>(LU, n, pr, pc, iam, c, o);
 }

@@ -124,10 +124,12 @@ def factor_error(lus, ref):
     return worst
 
 
-def stencil_case(kind, dims, dtype, grid, relax, maxsup):
-    """cases.build()-style recipe for a seeded stencil (picklable via partial)."""
+def stencil_case(kind, dims, dtype, grid, relax, maxsup, reference=False):
+    """cases.build()-style recipe for a seeded stencil (picklable via partial);
+    reference: the LUstruct pdgssvx builds (reference symbfact + pddistribute)
+    instead of the front-end's."""
     kw = {}
     if dtype == SLU_Z:
         kw = dict(diag=6 - 0.25, diag_im=-0.0025)
     A, perm = _stencil(kind, *dims, dtype, **kw)
-    return A, perm, dtype, grid, relax, maxsup, False
+    return (A, perm, dtype, grid, relax, maxsup, False) + ((True,) if reference else ())

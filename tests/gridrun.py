@@ -90,10 +90,12 @@ def _worker(rank, world, port, recipe, out_dir, device, fill=False, solve=False,
             lu = fx.lu(rank % (pr * pc))
             A = S = None
         else:
-            A, perm, dtype, (pr, pc), relax, maxsup, tiny = recipe()
+            rc = recipe()
+            A, perm, dtype, (pr, pc), relax, maxsup, tiny = rc[:7]
+            reference = len(rc) > 7 and rc[7]  # the structure pdgssvx builds (symbfact + pddistribute)
             anorm = cases.anorm(A)
             gg = GlooGrid(rank, pr, pc, pz)
-            S = Symbolic(A, perm, relax, maxsup)
+            S = Symbolic(A, perm, relax, maxsup, reference=reference)
             lu = S.distribute(pr, pc, gg.myrow, gg.mycol)
         res = {}
         if pz > 1:  # 3D grid: every layer holds the LUstruct; p2p transport
@@ -120,6 +122,8 @@ def _worker(rank, world, port, recipe, out_dir, device, fill=False, solve=False,
             res["nsec"], res["nbytes"] = p.check_exchange()
             st = p.stats()
             res["nlevels"] = st["nlevels"]
+            res["nsupers"], res["nsupers_in"] = st["nsupers"], st["nsupers_in"]
+            res["flops"] = st["schur_flops"] + st["panel_flops"]
             del p
         elif device is not None:
             if transport == "p2p":
@@ -153,7 +157,7 @@ def _worker(rank, world, port, recipe, out_dir, device, fill=False, solve=False,
             p.download()
             st = p.stats()
             res.update(info=info, tiny=ntiny, flops=st["schur_flops"] + st["panel_flops"],
-                       comm_bytes=st["comm_bytes"])
+                       comm_bytes=st["comm_bytes"], nsupers=st["nsupers"], nsupers_in=st["nsupers_in"])
             del p
         else:  # group plumbing only
             buf = np.full(16, rank, dtype=np.uint8)

@@ -82,8 +82,30 @@ def test_grid_matches_reference_fixture(name, fill, tmp_path):
     assert worst < TOL[meta["dtype"]], worst
 
 
-def _stencil_recipe(kind, dims, dtype, grid, relax, maxsup):
-    return cases.stencil_case(kind, dims, dtype, grid, relax, maxsup)
+def _stencil_recipe(kind, dims, dtype, grid, relax, maxsup, reference=False):
+    return cases.stencil_case(kind, dims, dtype, grid, relax, maxsup, reference)
+
+
+@pytest.mark.parametrize("grid,nx", [((2, 2), 16), ((2, 4), 16), ((1, 2), 12), ((3, 2), 12)])
+def test_grid_amalgamation_schedule_through_p2p_transport_cpu(grid, nx, tmp_path):
+    """The structure pdgssvx builds (reference symbfact + pddistribute: many
+    width-1 supernodes) on a grid: every rank's schedule-only plan runs the
+    grid amalgamation over the point-to-point transport (structure to the
+    analysis owners, partition all-gather, pieces to the coarse owners) and
+    replays the coarse plan's exchanges with checked bytes.  The ranks agree
+    on a partition coarser than the caller's, and their shares of the
+    caller partition's flops add up to the 1x1 count."""
+    from superlu_dist_amd.frontend import Amalgamation, Csc, nd_order
+    pr, pc = grid
+    rec = functools.partial(_stencil_recipe, STENCIL_3D7, (nx,) * 3, 0, grid, 60, 256, True)
+    out = run_grid(rec, pr, pc, tmp_path, device=None, transport="schedule", timeout=180)
+    ns = {int(o["nsupers"]) for o in out}
+    nin = {int(o["nsupers_in"]) for o in out}
+    assert len(ns) == 1 and len(nin) == 1 and ns.pop() < nin.pop()
+    assert len({int(o["nlevels"]) for o in out}) == 1
+    A = Csc.stencil(STENCIL_3D7, nx, nx, nx)
+    one = Amalgamation(Symbolic(A, nd_order(nx, nx, nx), 60, 256, reference=True).distribute())
+    assert sum(float(o["flops"]) for o in out) == pytest.approx(one.flops(), rel=1e-12)
 
 
 @pytest.mark.gpu
@@ -114,3 +136,28 @@ def test_grid_matches_oracle_stencil(kind, dims, dtype, grid, relax, maxsup, tra
 class _Fac:
     def __init__(self, d):
         self.Lval, self.Uval = d["L"], d["U"]
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not pyoracle.have_reference_harness(), reason="oracle/_ref not built")
+@pytest.mark.parametrize("grid", [(2, 2), (2, 4)])
+def test_grid_amalgamation_fingerprints_match_reference_pdgstrf(grid, tmp_path):
+    """The north-star path at a test size: the LUstruct pdgssvx builds for a
+    24^3 Laplacian (reference symbfact + pddistribute: the fine partition)
+    on a 2x2 / 2x4 grid, every rank factoring on the GPU through the grid
+    amalgamation (coarse partition, relayout over the point-to-point
+    transport); the factors, back in every rank's caller layout, against
+    the REFERENCE pdgstrf on the same grid through per-block fingerprints."""
+    pr, pc = grid
+    rec = functools.partial(_stencil_recipe, STENCIL_3D7, (24, 24, 24), 0, grid, 60, 256, True)
+    out = run_grid(rec, pr, pc, tmp_path, device=0, transport="p2p", timeout=600)
+    assert all(int(o["info"]) == 0 for o in out)
+    assert all(int(o["nsupers"]) < int(o["nsupers_in"]) for o in out)
+    A, perm = rec()[:2]
+    S = Symbolic(A, perm, 60, 256, reference=True)
+    mine = np.concatenate([pyoracle.blocksums(S.distribute(pr, pc, k // pc, k % pc), o["L"], o["U"])
+                           for k, o in enumerate(out)])
+    st, _ = pyoracle.run_reference(A, perm, pr, pc, symb_flags=2, want_factors=False,
+                                   want_blocksums=True, timeout=600)
+    c = pyoracle.compare_blocksums(mine, st["blocksums"])
+    assert c["match"] and c["rel_err"] <= 1e-12, c
