@@ -145,7 +145,7 @@ k_diag_strips(const DiagItemF<T> *items, int nitems, unsigned *flags, unsigned e
     __shared__ T sLi[PW][LD]; // L_pp^{-1}; later my L_qq^{-1}
     __shared__ T sUi[PW][LD]; // my U_qq^{-1}
     __shared__ T sT[2][4][64]; // 8 x 8 block products of the inverse (L, U)
-    __shared__ T s_prow[2][PW];
+    __shared__ int s_zp[PW];
     __shared__ T s_rp[PW];
     __shared__ int s_ok;
     DS_PROBE_START();
@@ -158,6 +158,7 @@ k_diag_strips(const DiagItemF<T> *items, int nitems, unsigned *flags, unsigned e
             return keep_if(ok & (e / w < pw), gld(A + min(r, w - 1) + (int64_t)(c0 + c) * ld));
         },
         [&](int e, T v) { sS[e % w][e / w] = v; });
+    __syncthreads();
 
     // ---- apply the panels of the strips to my left, in order
     for (int p = 0; p < q; ++p) {
@@ -225,131 +226,150 @@ k_diag_strips(const DiagItemF<T> *items, int nitems, unsigned *flags, unsigned e
         DS_PROBE(2);
     }
 
-    // ---- my panel: rows c0.. (nrow of them), thread t = row c0 + t
+    // ---- my panel: rows c0.. (nrow of them).  Wave 0 factors the top 64
+    // (the 32 x 32 diagonal block and 32 rows below it; lane = row, the
+    // pivot row through v_readlane: no barrier per column), then waves 1-3
+    // eliminate rows 64.. one row per thread against the finished U_qq in
+    // LDS (the same per-column semantics, no barrier at all) while wave 0
+    // forms U_qq^{-1} / L_qq^{-1} (below).
     const int nrow = w - c0;
-    {
+    if (wv == 0) {
         T x[PW];
-        const bool mine = tid < nrow;
+        const bool mine = lane < nrow;
 #pragma unroll
-        for (int c = 0; c < PW; ++c) x[c] = mine ? sS[c0 + tid][c] : Sx::zero();
+        for (int c = 0; c < PW; ++c) x[c] = mine ? sS[c0 + lane][c] : Sx::zero();
 #pragma unroll
         for (int j = 0; j < PW; ++j) {
             if (j < pw) { // uniform
-                if (tid == j) { // the pivot row
-                    T piv = x[j];
-                    if (replace_tiny && Sx::abs1(piv) < thresh) {
-                        piv = Sx::thresh(piv, thresh);
-                        atomicAdd(tiny_count, 1);
-                    }
-                    const int z = Sx::iszero(piv);
-                    if (z) atomicMax(&zpiv[it.k], it.fcol + c0 + j + 1);
-                    x[j] = piv;
-                    s_rp[j] = z ? Sx::zero() : Sx::recip(piv);
-#pragma unroll
-                    for (int c = j; c < PW; ++c) s_prow[j & 1][c] = x[c];
+                T piv = rlane(x[j], j);
+                if (replace_tiny && Sx::abs1(piv) < thresh) {
+                    piv = Sx::thresh(piv, thresh);
+                    if (lane == 0) atomicAdd(tiny_count, 1);
                 }
-                __syncthreads();
-                if (tid > j && mine) {
-                    // the whole pivot row in flight at once (the LDS latency
-                    // once per step, not once per pair of columns)
-                    T u[PW];
+                const int z = Sx::iszero(piv);
+                if (z && lane == 0) atomicMax(&zpiv[it.k], it.fcol + c0 + j + 1);
+                const T rp = z ? Sx::zero() : Sx::recip(piv);
+                // a zero pivot leaves the column unscaled (SRC/pdgstrf2.c:246-252)
+                const T l = lane > j ? (z ? x[j] : Sx::mul(x[j], rp)) : Sx::zero();
+                x[j] = lane > j ? l : (lane == j ? piv : x[j]);
 #pragma unroll
-                    for (int c = j; c < PW; ++c) u[c] = s_prow[j & 1][c];
-                    const T rp = s_rp[j];
-                    __builtin_amdgcn_sched_barrier(0);
-                    // a zero pivot leaves the column unscaled (SRC/pdgstrf2.c:246-252)
-                    const T l = Sx::iszero(u[j]) ? x[j] : Sx::mul(x[j], rp);
-                    x[j] = l;
-#pragma unroll
-                    for (int c = j + 1; c < PW; ++c) x[c] = Sx::fms(x[c], l, u[c]);
+                for (int c = j + 1; c < PW; ++c) x[c] = Sx::fms(x[c], l, rlane(x[c], j));
+                if (lane == 0) {
+                    s_rp[j] = rp;
+                    s_zp[j] = z;
                 }
             }
         }
-        if (mine) {
+        if (mine)
 #pragma unroll
-            for (int c = 0; c < PW; ++c) sS[c0 + tid][c] = x[c];
+            for (int c = 0; c < PW; ++c) sS[c0 + lane][c] = x[c];
+        if (lane >= pw && lane < PW) {
+            s_rp[lane] = Sx::zero();
+            s_zp[lane] = 0;
         }
-        if (tid >= pw && tid < PW) s_rp[tid] = Sx::zero();
     }
     __syncthreads();
     DS_PROBE(3);
-
-    // ---- L_qq^{-1} (unit lower) and U_qq^{-1} (upper) by 8 x 8 blocks.
-    // Lq(i,k) = sS[c0+i][k] (i > k), Uq(i,k) = sS[c0+i][k] (i <= k); indices
-    // >= pw count as zero (the inverses' rows / columns there are zero).
-    auto Lq = [&](int i, int k) { return keep_if((i < pw) & (k < pw), sS[c0 + min(i, pw - 1)][min(k, pw - 1)]); };
-    for (int e = tid; e < PW * PW; e += DS_THREADS) {
-        sLi[e / PW][e % PW] = Sx::zero();
-        sUi[e / PW][e % PW] = Sx::zero();
-    }
-    __syncthreads();
-    // diagonal 8 x 8 blocks: threads 0..31 columns of L's, 32..63 of U's
-    if (tid < 64) {
-        const int bb = (tid & 31) >> 3, jj = tid & 7, o = bb * 8;
-        T v[8];
-        if (tid < 32) { // L_bb x = e_jj, unit lower
+    if (wv > 0) { // rows 64.. of the panel, thread per row
+        const int i = tid;
+        if (i < nrow) {
+            T x[PW];
 #pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                T s = i == jj ? one_of(Sx::zero()) : Sx::zero();
+            for (int c = 0; c < PW; ++c) x[c] = sS[c0 + i][c];
 #pragma unroll
-                for (int k = 0; k < i; ++k) s = Sx::fms(s, Lq(o + i, o + k), v[k]);
-                v[i] = i < jj ? Sx::zero() : s;
+            for (int j = 0; j < PW; ++j) {
+                if (j < pw) {
+                    const T l = s_zp[j] ? x[j] : Sx::mul(x[j], s_rp[j]);
+                    x[j] = l;
+#pragma unroll
+                    for (int c = j + 1; c < PW; ++c) x[c] = Sx::fms(x[c], l, sS[c0 + j][c]);
+                }
             }
 #pragma unroll
-            for (int i = 0; i < 8; ++i)
-                if (o + i < pw && o + jj < pw) sLi[o + i][o + jj] = v[i];
-        } else { // U_bb y = e_jj, y(i) = rp(i) (e(i) - sum_{k>i} U(i,k) y(k))
+            for (int c = 0; c < PW; ++c) sS[c0 + i][c] = x[c];
+        }
+    } else {
+        // ---- meanwhile wave 0: L_qq^{-1} (unit lower) and U_qq^{-1} (upper)
+        // by 8 x 8 blocks.  Lq(i,k) = sS[c0+i][k] (i > k: L, i <= k: U);
+        // indices >= pw count as zero (the inverses' rows / columns there
+        // are zero).  One wave: its LDS accesses complete in order, so no
+        // barrier separates the stages.
+        auto Lq = [&](int i, int k) { return keep_if((i < pw) & (k < pw), sS[c0 + min(i, pw - 1)][min(k, pw - 1)]); };
+        for (int e = lane; e < PW * PW; e += 64) {
+            sLi[e / PW][e % PW] = Sx::zero();
+            sUi[e / PW][e % PW] = Sx::zero();
+        }
+        __builtin_amdgcn_wave_barrier();
+        { // diagonal 8 x 8 blocks: lanes 0..31 columns of L's, 32..63 of U's
+            const int bb = (lane & 31) >> 3, jj = lane & 7, o = bb * 8;
+            T v[8];
+            if (lane < 32) { // L_bb x = e_jj, unit lower
 #pragma unroll
-            for (int i = 7; i >= 0; --i) {
-                T s = i == jj ? one_of(Sx::zero()) : Sx::zero();
+                for (int i = 0; i < 8; ++i) {
+                    T sacc = i == jj ? one_of(Sx::zero()) : Sx::zero();
 #pragma unroll
-                for (int k = i + 1; k < 8; ++k) s = Sx::fms(s, Lq(o + i, o + k), v[k]);
-                v[i] = i > jj ? Sx::zero() : Sx::mul(s, s_rp[o + i]);
+                    for (int k = 0; k < i; ++k) sacc = Sx::fms(sacc, Lq(o + i, o + k), v[k]);
+                    v[i] = i < jj ? Sx::zero() : sacc;
+                }
+#pragma unroll
+                for (int i = 0; i < 8; ++i)
+                    if (o + i < pw && o + jj < pw) sLi[o + i][o + jj] = v[i];
+            } else { // U_bb y = e_jj, y(i) = rp(i) (e(i) - sum_{k>i} U(i,k) y(k))
+#pragma unroll
+                for (int i = 7; i >= 0; --i) {
+                    T sacc = i == jj ? one_of(Sx::zero()) : Sx::zero();
+#pragma unroll
+                    for (int k = i + 1; k < 8; ++k) sacc = Sx::fms(sacc, Lq(o + i, o + k), v[k]);
+                    v[i] = i > jj ? Sx::zero() : Sx::mul(sacc, s_rp[o + i]);
+                }
+#pragma unroll
+                for (int i = 0; i < 8; ++i)
+                    if (o + i < pw && o + jj < pw) sUi[o + i][o + jj] = v[i];
             }
+        }
+        __builtin_amdgcn_wave_barrier();
+        // off-diagonal blocks by distance d: L: X(a,b) = -X(a,a) sum_{c=b}^{a-1} L(a,c) X(c,b);
+        // U: Y(a,b) = -Y(a,a) sum_{c=a+1}^{b} U(a,c) Y(c,b)
+        for (int d = 1; d < 4; ++d) {
+            const int nblk = 4 - d; // block pairs per factor
+            for (int e = lane; e < 2 * nblk * 64; e += 64) {
+                const int u = e / (nblk * 64), pi = (e / 64) % nblk, i = (e & 63) >> 3, j = e & 7;
+                T sacc = Sx::zero();
+                if (u == 0) { // L block (a, b) = (pi + d, pi): T = sum_c L(a,c) X(c,b)
+                    const int a = pi + d, bq = pi;
+                    for (int c = bq; c < a; ++c)
 #pragma unroll
-            for (int i = 0; i < 8; ++i)
-                if (o + i < pw && o + jj < pw) sUi[o + i][o + jj] = v[i];
+                        for (int k = 0; k < 8; ++k)
+                            sacc = Sx::fms(sacc, Lq(a * 8 + i, c * 8 + k), sLi[c * 8 + k][bq * 8 + j]);
+                } else { // U block (a, b) = (pi, pi + d): T = sum_c U(a,c) Y(c,b)
+                    const int a = pi, bq = pi + d;
+                    for (int c = a + 1; c <= bq; ++c)
+#pragma unroll
+                        for (int k = 0; k < 8; ++k)
+                            sacc = Sx::fms(sacc, Lq(a * 8 + i, c * 8 + k), sUi[c * 8 + k][bq * 8 + j]);
+                }
+                sT[u][pi][e & 63] = sacc; // = -T
+            }
+            __builtin_amdgcn_wave_barrier();
+            for (int e = lane; e < 2 * nblk * 64; e += 64) {
+                const int u = e / (nblk * 64), pi = (e / 64) % nblk, i = (e & 63) >> 3, j = e & 7;
+                T sacc = Sx::zero();
+                if (u == 0) {
+                    const int a = pi + d, bq = pi;
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) sacc = Sx::fms(sacc, sLi[a * 8 + i][a * 8 + k], sT[0][pi][k * 8 + j]);
+                    if (a * 8 + i < pw && bq * 8 + j < pw) sLi[a * 8 + i][bq * 8 + j] = Sx::neg(sacc);
+                } else {
+                    const int a = pi, bq = pi + d;
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) sacc = Sx::fms(sacc, sUi[a * 8 + i][a * 8 + k], sT[1][pi][k * 8 + j]);
+                    if (a * 8 + i < pw && bq * 8 + j < pw) sUi[a * 8 + i][bq * 8 + j] = Sx::neg(sacc);
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
         }
     }
     __syncthreads();
-    // off-diagonal blocks by distance d: L: X(a,b) = -X(a,a) sum_{c=b}^{a-1} L(a,c) X(c,b);
-    // U: Y(a,b) = -Y(a,a) sum_{c=a+1}^{b} U(a,c) Y(c,b)
-    for (int d = 1; d < 4; ++d) {
-        const int nblk = 4 - d; // pairs per factor
-        for (int e = tid; e < 2 * nblk * 64; e += DS_THREADS) {
-            const int u = e / (nblk * 64), pi = (e / 64) % nblk, i = (e & 63) >> 3, j = e & 7;
-            T s = Sx::zero();
-            if (u == 0) { // L block (a, b) = (pi + d, pi): T = sum_c L(a,c) X(c,b)
-                const int a = pi + d, bq = pi;
-                for (int c = bq; c < a; ++c)
-#pragma unroll
-                    for (int k = 0; k < 8; ++k) s = Sx::fms(s, Lq(a * 8 + i, c * 8 + k), sLi[c * 8 + k][bq * 8 + j]);
-            } else { // U block (a, b) = (pi, pi + d): T = sum_c U(a,c) Y(c,b)
-                const int a = pi, bq = pi + d;
-                for (int c = a + 1; c <= bq; ++c)
-#pragma unroll
-                    for (int k = 0; k < 8; ++k) s = Sx::fms(s, Lq(a * 8 + i, c * 8 + k), sUi[c * 8 + k][bq * 8 + j]);
-            }
-            sT[u][pi][e & 63] = s; // = -T
-        }
-        __syncthreads();
-        for (int e = tid; e < 2 * nblk * 64; e += DS_THREADS) {
-            const int u = e / (nblk * 64), pi = (e / 64) % nblk, i = (e & 63) >> 3, j = e & 7;
-            T s = Sx::zero();
-            if (u == 0) {
-                const int a = pi + d, bq = pi;
-#pragma unroll
-                for (int k = 0; k < 8; ++k) s = Sx::fms(s, sLi[a * 8 + i][a * 8 + k], sT[0][pi][k * 8 + j]);
-                if (a * 8 + i < pw && bq * 8 + j < pw) sLi[a * 8 + i][bq * 8 + j] = Sx::neg(s);
-            } else {
-                const int a = pi, bq = pi + d;
-#pragma unroll
-                for (int k = 0; k < 8; ++k) s = Sx::fms(s, sUi[a * 8 + i][a * 8 + k], sT[1][pi][k * 8 + j]);
-                if (a * 8 + i < pw && bq * 8 + j < pw) sUi[a * 8 + i][bq * 8 + j] = Sx::neg(s);
-            }
-        }
-        __syncthreads();
-    }
 
     DS_PROBE(4);
     // ---- publish: the strip, U_qq^{-1} (row-major), (L_qq^{-1})^T (row-major)

@@ -42,6 +42,7 @@
 
 #include "common.h"
 #include "kernels.h"
+#include "diag_strips.h"
 #include "fill.h"
 #include "solve.h"
 #include "hostio.h"
@@ -578,7 +579,9 @@ struct Plan : PlanBase {
     DevBuf<int> d_rg, d_ra, d_cg, d_cb, d_pair, d_ct0;
     DevBuf<DRec> d_prec;
     DevBuf<i64> d_cvoff;
-    DevBuf<int> d_counters; // [0] tiny pivots
+    DevBuf<int> d_counters; // [0] tiny pivots, [1] k_diag_strips hand-off timeout
+    DevBuf<unsigned> d_dsflags; // k_diag_strips: per fast diag item, DS_MAXS strip flags
+    unsigned ds_epoch = 0;      // ... set to the factorization's epoch when a strip is published
     DevBuf<int> d_zpiv;     // per supernode: max zero-pivot column + 1
     DevBuf<i64> d_info;     // 2D grids: all-gather of the per-rank info
 
@@ -2242,6 +2245,8 @@ struct Plan : PlanBase {
         d_ucol_fst.upload(ucol_fst);
         d_counters.alloc(4);
         d_zpiv.alloc(nsupers);
+        d_dsflags.alloc(std::max<size_t>(df_items.size(), 1) * DS_MAXS);
+        HIPCHK(hipMemset(d_dsflags.p, 0, d_dsflags.bytes()));
         ev_pan.resize(levels.size());
         ev_rest.resize(levels.size());
         for (size_t L = 0; L < levels.size(); ++L) {
@@ -2615,6 +2620,23 @@ struct Plan : PlanBase {
     // gain nothing further, tools/ab_env.sh).
     int rest_split = getenv("SLU_REST_SPLIT") ? atoi(getenv("SLU_REST_SPLIT")) : 30;
     int rest_chunks = getenv("SLU_REST_CHUNKS") ? atoi(getenv("SLU_REST_CHUNKS")) : 1;
+    // k_diag_strips (diag_strips.h) for the levels near the root: a few wide
+    // real blocks, each factored by one workgroup per 32-column strip
+    // (SLU_DIAG_STRIPS=0: k_diag_lu_f everywhere; SLU_DIAG_STRIPS_MAX: the
+    // most blocks a level may hold for it, default 32)
+    // (SLU_DIAG_STRIPS=2, test hook: every fast level, narrow blocks too)
+    int strips_mode = getenv("SLU_DIAG_STRIPS") ? atoi(getenv("SLU_DIAG_STRIPS")) : 1;
+    int strips_max = getenv("SLU_DIAG_STRIPS_MAX") ? atoi(getenv("SLU_DIAG_STRIPS_MAX")) : 32;
+    bool strips_ok(const LevelRange &R) const {
+        if (cplx || strips_mode == 0) return false;
+        return strips_mode == 2 || (R.df_maxw > DF_SMALLW && R.df_n <= strips_max);
+    }
+    void launch_strips(const LevelRange &R, double thresh, hipStream_t st) {
+        if constexpr (!cplx)
+            hipLaunchKernelGGL(k_diag_strips<T>, dim3(ds_grid(R.df_n)), dim3(DS_THREADS), 0, st, d_df.p + R.df_off,
+                               R.df_n, d_dsflags.p + (size_t)R.df_off * DS_MAXS, ds_epoch, d_counters.p + 1, thresh,
+                               opts.replace_tiny_pivot, d_counters.p, d_zpiv.p);
+    }
     void launch_big(const LevelRange &R, int off, int cnt, hipStream_t st) {
         hipLaunchKernelGGL(k_schur_big<T>, dim3(cnt), dim3(BigCfg<T>::THREADS), 0, st,
                            d_tiles_big.p + off, d_kinfo.p + R.k_off, d_L.p, d_U.p,
@@ -2648,6 +2670,10 @@ struct Plan : PlanBase {
         const float s_eps = 5.9604644775390625e-08f; // FLT_EPSILON * 0.5
         double thresh = sizeof(T) == 4 ? (double)(float)(s_eps * (float)anorm) : (double)s_eps * anorm;
         HIPCHK(hipMemsetAsync(d_counters.p, 0, d_counters.bytes(), stream));
+        if (++ds_epoch >= 0x7fffffffu) { // (strip flags: a new epoch per factorization)
+            HIPCHK(hipMemsetAsync(d_dsflags.p, 0, d_dsflags.bytes(), stream));
+            ds_epoch = 1;
+        }
         HIPCHK(hipMemsetAsync(d_zpiv.p, 0, d_zpiv.bytes(), stream));
 #ifdef SLU_SB_STAMP
         {
@@ -2718,7 +2744,9 @@ struct Plan : PlanBase {
                 });
             if (R.df_n)
                 span(0, P, [&] {
-                    if (R.df_maxw <= DF_SMALLW)
+                    if (strips_ok(R))
+                        launch_strips(R, thresh, P);
+                    else if (R.df_maxw <= DF_SMALLW)
                         hipLaunchKernelGGL((k_diag_lu_f<T, DF_SMALLW, DF_SMALL_THREADS>), dim3(R.df_n),
                                            dim3(DF_SMALL_THREADS), 0, P, d_df.p + R.df_off, thresh,
                                            opts.replace_tiny_pivot, d_counters.p, d_zpiv.p);
@@ -2849,6 +2877,8 @@ struct Plan : PlanBase {
         host_current = overlap_dl;
         int hc[4];
         HIPCHK(hipMemcpy(hc, d_counters.p, sizeof hc, hipMemcpyDeviceToHost));
+        SLU_REQUIRE(hc[1] == 0, "factor: a diagonal-block strip waited more than a second for its left "
+                                "neighbour (k_diag_strips hand-off timeout)");
         vector<int> zp(nsupers);
         HIPCHK(hipMemcpy(zp.data(), d_zpiv.p, nsupers * sizeof(int), hipMemcpyDeviceToHost));
         // per-rank info: the zero pivot of the last supernode (in elimination

@@ -19,10 +19,12 @@ check of that reconstruction.
 """
 import glob
 import os
+import subprocess
 
 import numpy as np
 import pytest
 
+from conftest import ROOT
 from lusolve import lu_coords_matrix_from_lus
 from refdump import Fixture
 from superlu_dist_amd import symbolic as sy
@@ -139,3 +141,32 @@ def test_distribute_matches_reference_pddistribute(name):
         assert lu.view.Lval_cnt == sum(int(lu.Lidx[o + 1]) * int(xs[j * fx.pc + mycol + 1] -
                                                                  xs[j * fx.pc + mycol])
                                        for j, o in enumerate(lu.Loff) if o >= 0) + 1
+
+
+ASAN_DRV = os.path.join(ROOT, "oracle", "_ref", "distribute_destroy_asan")
+
+
+@pytest.mark.skipif(not os.path.exists(ASAN_DRV) or not os.path.exists("/opt/conda/bin/mpiexec"),
+                    reason="ASAN driver not built (make -C oracle asan)")
+@pytest.mark.parametrize("nprocs,grid", [(1, (1, 1)), (4, (2, 2))])
+@pytest.mark.parametrize("refill", [False, True])
+@pytest.mark.parametrize("t,matrix", [("d", "g20.rua"), ("d", "big.rua"), ("s", "g20.rua"),
+                                      ("z", "cg20.cua")])
+def test_distribute_ownership_under_asan(t, matrix, refill, nprocs, grid):
+    """The LUstruct this library's p?distribute builds is freed by the
+    REFERENCE's p?Destroy_LU (SRC/pdutil.c:485, psutil.c:435, pzutil.c:483)
+    without a bad free, double free or overflow: the reference's p?gssvx
+    (nrhs = 0) around our p?distribute (and the SamePattern_SameRowPerm
+    refill), our p?gstrf skipped (SUPERLU_MI355X_FACTOR_SKIP=1, no GPU), in
+    a process built with AddressSanitizer (oracle/gen/distribute_destroy_main.c).
+    With the s / z per-block allocation of commit 1947008 reverted this run
+    aborts with 'attempting free on address which was not malloc()-ed'."""
+    env = dict(os.environ, SUPERLU_MI355X_FACTOR_SKIP="1", ASAN_OPTIONS="detect_leaks=0",
+               OMP_NUM_THREADS="1", MKL_NUM_THREADS="1")
+    args = ["-t", t, "-R", str(grid[0]), "-C", str(grid[1])] + (["-r"] if refill else [])
+    cmd = ["/opt/conda/bin/mpiexec", "-n", str(nprocs), ASAN_DRV] + args + \
+          [os.path.join(ROOT, "tests", "golden", "matrices", matrix)]
+    r = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=300)
+    out = r.stdout + r.stderr
+    assert "AddressSanitizer" not in out, out[-3000:]
+    assert r.returncode == 0 and out.count(": OK") == nprocs, out[-3000:]

@@ -275,3 +275,25 @@ def test_dropin_plan_cache_refactors_new_values(monkeypatch):
     assert rv == 0 and info == 0
     err = cases.factor_error([other], [(ref.Lval, ref.Uval)])
     assert err < TOL[0], err
+
+
+@pytest.mark.parametrize("mode", ["0", "1", "2"])
+@pytest.mark.parametrize("kind,dims,dtype", [
+    (STENCIL_3D7, (24, 24, 24), 0),
+    (STENCIL_3D27, (14, 14, 14), 1),
+])
+def test_gpu_diag_strips_match_oracle(kind, dims, dtype, mode, monkeypatch):
+    """The multi-workgroup diagonal LU (k_diag_strips, csrc/diag_strips.h) on
+    the reference structure: off (0), the default levels (1: wide blocks, few
+    per level) and every fast level (2, narrow blocks and the leaves' many
+    blocks too) -- factors against the oracle."""
+    monkeypatch.setenv("SLU_DIAG_STRIPS", mode)
+    A = Csc.stencil(kind, *dims, dtype=dtype)
+    S = Symbolic(A, nd_order(*dims), 60, 256, reference=True)
+    gpu, ref = S.distribute(), S.distribute()
+    an = cases.anorm(A)
+    info, tiny, st = factor_lustruct(gpu, anorm=an)
+    o = pyoracle.oracle_factor([ref], 1, 1, A.n, False, an)
+    assert info == o["info"] == 0
+    err = cases.factor_error([gpu], [(ref.Lval, ref.Uval)])
+    assert err < TOL[dtype], err

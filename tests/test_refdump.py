@@ -88,10 +88,14 @@ def test_oracle_matches_reference_on_reference_lustructs(name):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("strips", ["1", "2"])
 @pytest.mark.parametrize("name", ONE)
-def test_gpu_dropin_pdgstrf_on_reference_lustructs(name):
+def test_gpu_dropin_pdgstrf_on_reference_lustructs(name, strips, monkeypatch):
     """The exported pdgstrf / psgstrf / pzgstrf, called as pdgssvx calls them,
-    factor the reference-built LUstruct in place to the reference's factors."""
+    factor the reference-built LUstruct in place to the reference's factors.
+    strips 2: every real diagonal block through k_diag_strips (its zero- /
+    tiny-pivot semantics against the reference's)."""
+    monkeypatch.setenv("SLU_DIAG_STRIPS", strips)
     from superlu_dist_amd import capi
     fx = Fixture(name)
     lu = fx.lu(0)
