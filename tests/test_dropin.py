@@ -106,8 +106,9 @@ def test_reference_driver_with_our_factorization(drv, matrix, extra, nprocs, gri
 def test_reference_driver_default_ordering_through_our_metis(drv, matrix):
     """No -q: the drivers' default ColPerm = METIS_AT_PLUS_A, which calls
     METIS_NodeND (SRC/get_perm_c.c:524-541).  METIS is not in the image, so
-    only the library's nested dissection can serve it; the all-reference
-    driver runs MMD (-q 2) for the accuracy yardstick."""
+    only the library's nested dissection can serve it; the driver with the
+    reference's factorization and solve runs MMD (-q 2) for the accuracy
+    yardstick."""
     ref_err, _, _ = _run(f"{drv}_ref", 1, ["-r", "1", "-c", "1", "-q", "2"], matrix)
     my_err, _, out = _run(f"{drv}_mi355x_full", 1, ["-r", "1", "-c", "1"], matrix)
     print(f"{drv} {matrix} METIS_AT_PLUS_A via the library: {my_err:.3e} (reference, MMD: {ref_err:.3e})")
@@ -176,8 +177,10 @@ def test_reference_reentry_drivers_with_our_distribute_factor_solve(drv, matrix,
 # (pdgssvx3d: 3D matrix distribution, dinitTrf3Dpartition's forests, its
 # ancestor zeroing, pdgstrf3d, dgatherAllFactoredLU, pdgstrs / pdgsrfs on
 # layer 0) with pdgstrf3d from libslu_mi355x_3d.so (oracle/_ref/
-# pddrive3d_mi355x, `make -C oracle dropin3d`) against the all-reference
-# driver (pddrive3d_ref, `make -C oracle ref3d`).  Several ranks share the
+# pddrive3d_mi355x, `make -C oracle dropin3d`) against the driver with the
+# reference's pdgstrf3d (pddrive3d_ref, `make -C oracle ref3d`; the _nd
+# variants of both take METIS_NodeND from libslu_mi355x_metis.so, so for them
+# the yardstick is the reference everywhere except the ordering).  Several ranks share the
 # box's GPU: the library carries the layer exchanges and the ancestor
 # reductions over MPI point to point.
 
