@@ -4,9 +4,11 @@ Inputs:
   * the 1-GPU per-level log of `bench.py --level-log` (stderr lines
     "[slu rank 0] lvl nsup diag trsm big small atomic GFLOP diag_ms trsm_ms
     big_ms small_ms comm_ms TF/s wall_ms");
-  * the per-level panel volumes of the same LU structure (computed here from
-    the front-end: bytes of L(:,k) below the diagonal block and of U(k,:)
-    for the supernodes of each level).
+  * the per-level panel volumes of the same LU structure (computed here:
+    bytes of L(:,k) below the diagonal block and of U(k,:) for the
+    supernodes of each level) -- the coarse partition the plans factor
+    (the amalgamated reference structure, Symbolic(reference=True,
+    coarse=True); --frontend: the library front-end's, for round-2 logs).
 
 For a Pr x Pc grid (P = Pr Pc ranks, one per GPU) each level costs
   chain_L = diag_L + trsm_L / ((Pr + Pc) / 2) + comm_L
@@ -56,12 +58,13 @@ def parse_log(path):
     return sorted(out, key=lambda r: r["lvl"])
 
 
-def level_volumes(nx):
+def level_volumes(nx, frontend=False):
     """Per supernode: level, bytes of L(:,k) below the diagonal block, bytes
     of U(k,:), and the L block rows / U block columns (for the need masks)."""
     from superlu_dist_amd.frontend import STENCIL_3D7, Csc, Symbolic, nd_order
     A = Csc.stencil(STENCIL_3D7, nx, nx, nx)
-    S = Symbolic(A, nd_order(nx, nx, nx), 60, 256)
+    S = (Symbolic(A, nd_order(nx, nx, nx), 60, 256) if frontend else
+         Symbolic(A, nd_order(nx, nx, nx), 60, 256, reference=True, coarse=True))
     lu = S.distribute()
     ns, xs = S.nsupers, S.xsup
     lvl = np.zeros(ns, dtype=np.int64)
@@ -139,11 +142,13 @@ def main():
     ap.add_argument("--nx", type=int, default=100)
     ap.add_argument("--bw", type=float, default=50.0, help="GB/s per rank per broadcast")
     ap.add_argument("--lat", type=float, default=30.0, help="us per collective")
+    ap.add_argument("--frontend", action="store_true",
+                    help="volumes of the library front-end's partition (round-2 logs)")
     ap.add_argument("--t1", type=float, default=None,
                     help="measured 1-GPU factor time (ms); default: sum of the log's level walls")
     a = ap.parse_args()
     rows = parse_log(a.log)
-    lvl, sn = level_volumes(a.nx)
+    lvl, sn = level_volumes(a.nx, a.frontend)
     t1, _, _ = model(rows, None, 1, 1, a.bw, a.lat)
     if a.t1:
         t1 = a.t1
