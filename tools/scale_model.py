@@ -146,13 +146,18 @@ def main():
                     help="volumes of the library front-end's partition (round-2 logs)")
     ap.add_argument("--t1", type=float, default=None,
                     help="measured 1-GPU factor time (ms); default: sum of the log's level walls")
+    ap.add_argument("--diag-scale", type=float, default=1.0,
+                    help="what-if: multiply every level's diagonal-LU time (grid chains only)")
     a = ap.parse_args()
     rows = parse_log(a.log)
-    lvl, sn = level_volumes(a.nx, a.frontend)
     t1, _, _ = model(rows, None, 1, 1, a.bw, a.lat)
+    for r in rows:
+        r["diag"] *= a.diag_scale
+    lvl, sn = level_volumes(a.nx, a.frontend)
     if a.t1:
         t1 = a.t1
-    out = {"levels": len(rows), "bw_GBs": a.bw, "lat_us": a.lat, "t1_ms": round(t1, 1)}
+    out = {"levels": len(rows), "bw_GBs": a.bw, "lat_us": a.lat, "t1_ms": round(t1, 1),
+           "diag_scale": a.diag_scale}
     for pr, pc in ((1, 2), (2, 2), (2, 4), (4, 2)):
         vol = recv_volumes(lvl, sn, pr, pc)
         t, chain, schur = model(rows, vol, pr, pc, a.bw, a.lat)
