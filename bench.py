@@ -175,12 +175,18 @@ def abi_leg(lu, anorm, factor_ms, fingerprint=None):
     L0, U0 = lu.Lval.copy(), lu.Uval.copy()
     walls = []
     if os.environ.get("SLU_ABI_BREAKDOWN_ONLY"):
-        walls = [0.0, 0.0]
-    for _ in range(0 if walls else 2):  # first call of the process (HIP / pinned-pool set-up), then warm
+        walls = [0.0, 0.0, 0.0]
+    # first call of the process (Fact = DOFACT: plan build, HIP / pinned-pool
+    # set-up), then the refactorization as pdgssvx calls it (Fact =
+    # SamePattern_SameRowPerm: the cached plan, shallow structure digest),
+    # then a DOFACT call on the same arrays (cached plan, full digest)
+    opt = capi.default_options()
+    for fact in ([] if walls else [0, 2, 0]):
         lu.Lval[:] = L0
         lu.Uval[:] = U0
+        opt.Fact = fact
         t = time.perf_counter()
-        rv, info, st = capi.pxgstrf(lu, anorm)
+        rv, info, st = capi.pxgstrf(lu, anorm, options=opt)
         walls.append((time.perf_counter() - t) * 1e3)
         assert rv == 0 and info == 0, (rv, info)
     # the drop-in's factors, fingerprinted for the parity check of the
@@ -205,6 +211,7 @@ def abi_leg(lu, anorm, factor_ms, fingerprint=None):
     h2d = st["t_upload_ms"]
     pcie = 56.0  # GB/s, registered H2D / D2H on the box (profiles/r02_pcie_micro.json)
     return {"utime_fact_ms": round(walls[1], 1), "utime_fact_ms_first_call": round(walls[0], 1),
+            "utime_fact_ms_cached_dofact": round(walls[2], 1),
             "bar_ms": round(1.2 * (h2d + factor_ms), 1),
             "breakdown_ms": {"plan_build": round(st["t_plan_ms"], 1),
                              "h2d_values": round(h2d, 1),

@@ -218,16 +218,23 @@ void reap_later(slu_plan *p) {
     });
 }
 
-// ---- plan cache (1x1 grids).  pdgssvx refactors one pattern with Fact =
-// SamePattern / SamePattern_SameRowPerm (SRC/superlu_defs.h:577-598): the
-// LUstruct's index arrays are the same, only the values differ.  The last
-// plan is kept (with its HBM) and reused when the structure digest matches,
-// so such a call pays upload + factor + download only.  Grids always build
-// afresh (their communicator belongs to grid->comm).  SUPERLU_MI355X_PLAN_CACHE=0
-// frees the plan after every call, as the reference frees its buffers.
+// ---- plan cache.  pdgssvx refactors one pattern with Fact = SamePattern /
+// SamePattern_SameRowPerm (SRC/superlu_defs.h:577-598): the LUstruct's index
+// arrays are the same, only the values differ.  The last plan is kept (with
+// its HBM) and reused when the structure digest matches, so such a call pays
+// upload + factor + download only; on a grid every rank reuses or every rank
+// rebuilds (the digest covers grid->comm: the plan holds its transport).
+// The digest hashes every index array, except under Fact =
+// SamePattern_SameRowPerm: there the caller reuses "the L & U data structures
+// set up from the previous factorization" (SRC/superlu_defs.h:590-598,
+// pdgssvx skips symbfact and pddistribute only refills values,
+// SRC/pddistribute.c:545-672), and a shallow digest (the LUstruct's tables,
+// every block's pointers and header words) suffices.
+// SUPERLU_MI355X_PLAN_CACHE=0 frees the plan after every call, as the
+// reference frees its buffers.
 struct CachedPlan {
     slu_plan *plan = nullptr;
-    uint64_t digest = 0;
+    uint64_t digest = 0, shallow = 0;
     int dtype = -1, n = -1, replace_tiny = -1;
     const void *lu = nullptr; // the LUstruct the cached factors belong to (pdgstrs)
     struct Key {
@@ -331,6 +338,47 @@ template <typename LUS> uint64_t structure_digest(LUS *lu, int n, const gridinfo
     return h;
 }
 
+// the shallow digest: the tables, every local block's index / value pointers
+// and header words, the grid (O(blocks), no index array is read through)
+template <typename LUS> uint64_t shallow_digest(LUS *lu, int n, const gridinfo_t *grid) {
+    const int_t *xsup = lu->Glu_persist->xsup;
+    const int ns = (int)(lu->Glu_persist->supno[n - 1] + 1);
+    const int Pr = (int)grid->nprow, Pc = (int)grid->npcol;
+    const int nlc = (ns + Pc - 1) / Pc, nlr = (ns + Pr - 1) / Pr, nb = std::max(nlc, nlr);
+    constexpr int CH = 4096;
+    std::vector<uint64_t> part((nb + CH - 1) / CH);
+    auto *L = lu->Llu;
+    slu::parallel_for((int)part.size(), [&](int c) {
+        uint64_t h = (uint64_t)c;
+        for (int j = c * CH; j < std::min(nb, (c + 1) * CH); ++j) {
+            h = mix(h, (uint64_t)xsup[std::min(j + 1, ns)]);
+            if (j < nlc) {
+                const int_t *ix = L->Lrowind_bc_ptr[j];
+                h = mix(h, (uint64_t)(uintptr_t)ix);
+                h = mix(h, (uint64_t)(uintptr_t)L->Lnzval_bc_ptr[j]);
+                if (ix) h = mix(mix(h, (uint64_t)ix[0]), (uint64_t)ix[1]);
+            }
+            if (j < nlr) {
+                const int_t *ux = L->Ufstnz_br_ptr[j];
+                h = mix(h, (uint64_t)(uintptr_t)ux);
+                h = mix(h, (uint64_t)(uintptr_t)L->Unzval_br_ptr[j]);
+                if (ux) h = mix(mix(mix(h, (uint64_t)ux[0]), (uint64_t)ux[1]), (uint64_t)ux[2]);
+            }
+        }
+        part[c] = h;
+    }, 1);
+    uint64_t h = mix(mix((uint64_t)n, (uint64_t)ns), 0x5A11u);
+    h = mix(h, (uint64_t)(uintptr_t)lu);
+    h = mix(h, (uint64_t)(uintptr_t)L);
+    h = mix(h, (uint64_t)(uintptr_t)L->Lrowind_bc_ptr);
+    h = mix(h, (uint64_t)(uintptr_t)L->Ufstnz_br_ptr);
+    h = mix(h, ((uint64_t)Pr << 32) | (uint64_t)Pc);
+    h = mix(h, (uint64_t)grid->iam);
+    h = mix(h, (uint64_t)(uintptr_t)grid->comm);
+    for (uint64_t v : part) h = mix(h, v);
+    return h;
+}
+
 // every rank of the grid reuses its cached plan, or none does (building a
 // plan is collective)
 bool all_ranks(bool mine, gridinfo_t *grid) {
@@ -389,11 +437,19 @@ int_t pxgstrf(int dtype, const char *name, superlu_dist_options_t *options, int 
         const char *pc = getenv("SUPERLU_MI355X_PLAN_CACHE");
         const bool cache = !(pc && !strcmp(pc, "0"));
         const int rt = options->ReplaceTinyPivot == SLU_YES;
-        uint64_t dg = 0;
+        uint64_t dg = 0, sdg = 0;
         if (cache) {
-            dg = structure_digest(LUstruct, n, grid);
-            bool hit;
-            {
+            sdg = shallow_digest(LUstruct, n, grid);
+            bool hit = false;
+            if (options->Fact == SLU_SAMEPATTERN_SAMEROWPERM) {
+                // the previous factorization's L & U structures, by contract
+                std::lock_guard<std::mutex> lk(g_cache_mu);
+                hit = g_cache.plan && g_cache.shallow == sdg && g_cache.key == lu_key(LUstruct) &&
+                      g_cache.dtype == dtype && g_cache.n == n && g_cache.replace_tiny == rt;
+                if (hit) dg = g_cache.digest;
+            }
+            if (!hit) {
+                dg = structure_digest(LUstruct, n, grid);
                 std::lock_guard<std::mutex> lk(g_cache_mu);
                 hit = g_cache.plan && g_cache.digest == dg && g_cache.dtype == dtype && g_cache.n == n &&
                       g_cache.replace_tiny == rt;
@@ -493,6 +549,7 @@ int_t pxgstrf(int dtype, const char *name, superlu_dist_options_t *options, int 
             std::lock_guard<std::mutex> lk(g_cache_mu);
             g_cache.plan = plan;
             g_cache.digest = dg;
+            g_cache.shallow = sdg;
             g_cache.dtype = dtype;
             g_cache.n = n;
             g_cache.replace_tiny = rt;

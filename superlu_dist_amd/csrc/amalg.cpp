@@ -23,6 +23,7 @@ using i64 = int64_t;
 // One original supernode's structure as the plan needs it.
 struct SnInfo {
     i64 nsupr = 0, ulen = 0, ucols = 0; // L rows, U values, U column entries
+    i64 ucne = 0;                       // non-empty U column entries
     double schur = 0, trsv = 0;         // 2 m seglen, seglen (seglen + 1) over U columns
     int parent = -1;                    // first block row below the diagonal block
     int b = 0;                          // L rows below the diagonal block
@@ -57,7 +58,7 @@ template <typename F> inline void for_ucols(const int_t *ux, const int_t *xsup, 
 
 std::vector<int> amalg_chains(int64_t n, int ns, const int_t *xsup, const int_t *const *lidx,
                               const int_t *const *uidx, double zero_frac, int maxw, int a0, int a1,
-                              AmalgFlops *fl) {
+                              AmalgFlops *fl, std::vector<int64_t> *ucne) {
     const bool prof = getenv("SLU_AMALG_TIME") != nullptr;
     auto t0 = std::chrono::steady_clock::now();
     auto tick = [&](const char *what) {
@@ -71,59 +72,90 @@ std::vector<int> amalg_chains(int64_t n, int ns, const int_t *xsup, const int_t 
     SLU_REQUIRE(n < (1ll << 31), "amalgamation: n %lld does not fit int32", (long long)n);
     const int nr = a1 - a0;
 
-    // ---- pass 1: per supernode structure facts (parallel)
+    // ---- pass 1: per supernode structure facts (parallel).  Set tests by
+    // stamps in a per-thread row marker (no sorting: the reference's rows
+    // come in symbfact's order, not ascending)
     std::vector<SnInfo> inf(nr);
     parallel_for(nr, [&](int si) {
         const int s = a0 + si;
-        thread_local std::vector<int32_t> bl, uc, bl2;
+        thread_local std::vector<uint32_t> mark;
+        thread_local uint32_t stamp = 0;
+        if ((i64)mark.size() < n) { mark.assign(n, 0); stamp = 0; }
+        if (stamp > 0xFFFFFFF0u) { std::fill(mark.begin(), mark.end(), 0); stamp = 0; }
         SnInfo &I = inf[si];
         const int_t *ux = uidx[s];
-        if (ux) {
-            i64 p = SLU_BR_HEADER;
-            for (i64 b = 0; b < ux[0]; ++b) {
-                I.ucols += W(ux[p]);
-                p += SLU_UB_DESCRIPTOR + W(ux[p]);
-            }
-            I.ulen = ux[1];
-        }
         const int_t *ix = lidx[s];
-        if (!ix) return;
-        I.nsupr = ix[1];
-        {
+        // L: diagonal block first and full, then mark below(s)
+        const bool lok = ix && ix[0] >= 1 && ix[SLU_BC_HEADER] == s && ix[SLU_BC_HEADER + 1] == W(s);
+        const uint32_t sb = ++stamp;
+        if (ix) I.nsupr = ix[1];
+        if (lok) {
+            int b = 0;
             i64 p = SLU_BC_HEADER;
-            if (ix[0] < 1 || ix[p] != s || ix[p + 1] != W(s)) return; // diagonal block first, full
+            for (i64 k = 0; k < ix[0]; ++k) {
+                const i64 gb = ix[p], nrw = ix[p + 1];
+                if (gb != s) {
+                    for (i64 i = 0; i < nrw; ++i) mark[ix[p + 2 + i]] = sb;
+                    b += (int)nrw;
+                }
+                p += SLU_LB_DESCRIPTOR + nrw;
+            }
+            I.b = b;
+            SLU_REQUIRE(I.nsupr == W(s) + I.b, "amalgamation: L column %d rows %lld != %d + %d", s,
+                        (long long)I.nsupr, W(s), I.b);
+            if (ix[0] > 1) I.parent = (int)ix[SLU_BC_HEADER + SLU_LB_DESCRIPTOR + ix[SLU_BC_HEADER + 1]];
         }
-        below_rows(ix, s, bl);
-        I.b = (int)bl.size();
-        SLU_REQUIRE(I.nsupr == W(s) + I.b, "amalgamation: L column %d rows %lld != %d + %d", s,
-                    (long long)I.nsupr, W(s), I.b);
-        {
-            i64 p = SLU_BC_HEADER;
-            if (ix[0] > 1) I.parent = (int)ix[p + SLU_LB_DESCRIPTOR + ix[p + 1]];
-        }
+        // U, once: column counts, and against the mark the symmetric test
         const i64 end = xsup[s + 1];
-        uc.clear();
-        for_ucols(ux, xsup, [&](i64 g, i64 fst) {
-            if (fst >= end) return;
-            uc.push_back((int32_t)g);
-            const double seg = (double)(end - fst);
-            I.trsv += seg * (seg + 1);
-            I.schur += 2.0 * I.b * seg;
-        });
-        std::sort(bl.begin(), bl.end());
-        I.sym = bl == uc; // U columns come out ascending (blocks by jb)
+        int nuc = 0;
+        bool sym = true;
+        if (ux) {
+            I.ulen = ux[1];
+            i64 p = SLU_BR_HEADER;
+            for (i64 k = 0; k < ux[0]; ++k) {
+                const i64 jb = ux[p], w = xsup[jb + 1] - xsup[jb];
+                I.ucols += w;
+                for (i64 c = 0; c < w; ++c) {
+                    const i64 fst = ux[p + SLU_UB_DESCRIPTOR + c];
+                    if (fst >= end) continue;
+                    ++nuc;
+                    if (!lok) continue;
+                    sym = sym && mark[xsup[jb] + c] == sb;
+                    const double seg = (double)(end - fst);
+                    I.trsv += seg * (seg + 1);
+                    I.schur += 2.0 * I.b * seg;
+                }
+                p += SLU_UB_DESCRIPTOR + w;
+            }
+        }
+        I.ucne = nuc;
+        if (!lok) return;
+        I.sym = sym && nuc == I.b; // (rows and columns are distinct: equal sets)
         I.ok = true;
         // nested into s+1: below(s) within cols(s+1) u below(s+1)
         if (I.parent == s + 1 && s + 1 < a1) {
-            below_rows(lidx[s + 1], s + 1, bl2);
-            std::sort(bl2.begin(), bl2.end());
+            const uint32_t s2 = ++stamp;
+            const int_t *i2 = lidx[s + 1];
+            if (i2) {
+                i64 p = SLU_BC_HEADER;
+                for (i64 k = 0; k < i2[0]; ++k) {
+                    const i64 nrw = i2[p + 1];
+                    if (i2[p] != s + 1)
+                        for (i64 i = 0; i < nrw; ++i) mark[i2[p + 2 + i]] = s2;
+                    p += SLU_LB_DESCRIPTOR + nrw;
+                }
+            }
             const i64 f1 = xsup[s + 1], l1 = xsup[s + 2];
-            size_t q = 0;
             bool nest = true;
-            for (int32_t r : bl) {
-                if (r >= f1 && r < l1) continue;
-                while (q < bl2.size() && bl2[q] < r) ++q;
-                if (q == bl2.size() || bl2[q] != r) { nest = false; break; }
+            i64 p = SLU_BC_HEADER;
+            for (i64 k = 0; nest && k < ix[0]; ++k) {
+                const i64 nrw = ix[p + 1];
+                if (ix[p] != s)
+                    for (i64 i = 0; i < nrw; ++i) {
+                        const i64 r = ix[p + 2 + i];
+                        if ((r < f1 || r >= l1) && mark[r] != s2) { nest = false; break; }
+                    }
+                p += SLU_LB_DESCRIPTOR + nrw;
             }
             I.nested = nest;
         }
@@ -139,27 +171,48 @@ std::vector<int> amalg_chains(int64_t n, int ns, const int_t *xsup, const int_t 
             fl->trsv += inf[si].trsv;
             fl->schur += inf[si].schur;
         }
+    if (ucne) {
+        ucne->resize(nr);
+        for (int si = 0; si < nr; ++si) (*ucne)[si] = inf[si].ucne;
+    }
     tick("pass 1 (structure facts)");
-    // ---- pass 2: greedy chains (never across a1)
-    std::vector<int> gstart; // first original supernode of every group
-    {
-        std::vector<int32_t> ff((size_t)n, -1); // first-row of column g in the open chain
-        std::vector<int32_t> touched;
-        int s = a0;
-        while (s < a1) {
-            gstart.push_back(s);
+    // ---- pass 2: greedy chains (never across a1).  A chain only grows over
+    // links e -> e + 1 that pass 1 allows, so the maximal runs of allowed
+    // links are independent: runs in parallel, each greedy in order.
+    auto link = [&](int e) {
+        const SnInfo &A = inf[e - a0];
+        return e + 1 < a1 && A.ok && A.sym && A.nested && A.parent == e + 1 && inf[e + 1 - a0].ok &&
+               inf[e + 1 - a0].sym;
+    };
+    std::vector<int> runs; // first supernode of every run (end: a1)
+    for (int s = a0; s < a1;) {
+        runs.push_back(s);
+        int e = s;
+        while (link(e)) ++e;
+        s = e + 1;
+    }
+    const int nruns = (int)runs.size();
+    runs.push_back(a1);
+    std::vector<std::vector<int>> rstart(nruns);
+    parallel_for(nruns, [&](int ri) {
+        thread_local std::vector<int32_t> ff; // first row of column g in the open chain
+        if ((i64)ff.size() < n) ff.assign(n, -1);
+        thread_local std::vector<int32_t> touched;
+        const int r1 = runs[ri + 1];
+        std::vector<int> &out = rstart[ri];
+        int s = runs[ri];
+        while (s < r1) {
+            out.push_back(s);
             int e = s;
             const SnInfo &I0 = inf[s - a0];
             int wJ = W(s);
             i64 orig = (i64)W(s) * I0.nsupr + I0.ulen;
             touched.clear();
-            if (I0.ok && I0.sym)
+            if (e + 1 < r1)
                 for_ucols(uidx[s], xsup, [&](i64 g, i64 fst) {
                     if (fst < xsup[s + 1]) { ff[g] = (int32_t)fst; touched.push_back((int32_t)g); }
                 });
-            while (e + 1 < a1 && inf[e - a0].ok && inf[e - a0].sym && inf[e - a0].nested &&
-                   inf[e - a0].parent == e + 1 && inf[e + 1 - a0].ok && inf[e + 1 - a0].sym &&
-                   wJ + W(e + 1) <= maxw) {
+            while (e + 1 < r1 && wJ + W(e + 1) <= maxw) {
                 const int c = e + 1;
                 const i64 endc = xsup[c + 1];
                 double S = 0;
@@ -183,7 +236,9 @@ std::vector<int> amalg_chains(int64_t n, int ns, const int_t *xsup, const int_t 
             for (int32_t g : touched) ff[g] = -1;
             s = e + 1;
         }
-    }
+    }, 1);
+    std::vector<int> gstart;
+    for (auto &v : rstart) gstart.insert(gstart.end(), v.begin(), v.end());
     tick("pass 2 (chains)");
     return gstart;
 }
@@ -203,23 +258,14 @@ bool Amalg::build(int64_t n_, int ns, const int_t *xsup, const int_t *const *lid
     };
     auto W = [&](i64 k) { return (int)(xsup[k + 1] - xsup[k]); };
     AmalgFlops fl;
-    std::vector<int> gstart = amalg_chains(n, ns, xsup, lidx, uidx, zero_frac, maxw, 0, ns, &fl);
+    std::vector<i64> ucne; // non-empty U column entries per supernode
+    std::vector<int> gstart = amalg_chains(n, ns, xsup, lidx, uidx, zero_frac, maxw, 0, ns, &fl, &ucne);
     fl_w = fl.w;
     fl_s1 = fl.s1;
     fl_s2 = fl.s2;
     fl_trsm = fl.trsm;
     fl_trsv = fl.trsv;
     fl_schur = fl.schur;
-    std::vector<SnInfo> inf(ns); // (pass 3 reads the per-supernode U column counts only)
-    parallel_for(ns, [&](int s) {
-        if (const int_t *ux = uidx[s]) {
-            i64 p = SLU_BR_HEADER;
-            for (i64 b = 0; b < ux[0]; ++b) {
-                inf[s].ucols += W(ux[p]);
-                p += SLU_UB_DESCRIPTOR + W(ux[p]);
-            }
-        }
-    }, 64);
     ns2 = (int)gstart.size();
     tick("pass 2 (chains)");
     if (ns2 == ns1) return false;
@@ -238,13 +284,12 @@ bool Amalg::build(int64_t n_, int ns, const int_t *xsup, const int_t *const *lid
     auto W2 = [&](i64 J) { return (int)(xsup2[J + 1] - xsup2[J]); };
 
     // original value offsets (contiguous in supernode order) and program offsets
-    std::vector<i64> lsrc(ns + 1, 0), usrc(ns + 1, 0), lmap(ns + 1, 0), fcol(ns + 1, 0), nub(ns + 1, 0);
+    std::vector<i64> lsrc(ns + 1, 0), usrc(ns + 1, 0), lmap(ns + 1, 0), fcol(ns + 1, 0);
     for (int s = 0; s < ns; ++s) {
         lsrc[s + 1] = lsrc[s] + (lidx[s] ? (i64)lidx[s][1] * W(s) : 0);
         usrc[s + 1] = usrc[s] + (uidx[s] ? (i64)uidx[s][1] : 0);
         lmap[s + 1] = lmap[s] + (lidx[s] ? (i64)lidx[s][1] : 0);
-        fcol[s + 1] = fcol[s] + inf[s].ucols;
-        nub[s + 1] = nub[s] + (uidx[s] ? (i64)uidx[s][0] : 0);
+        fcol[s + 1] = fcol[s] + ucne[s];
     }
     lval1 = lsrc[ns];
     uval1 = usrc[ns];
@@ -330,11 +375,14 @@ bool Amalg::build(int64_t n_, int ns, const int_t *xsup, const int_t *const *lid
     DL0 = ucol_len[ns2];
     SLU_REQUIRE(DL0 + n < (1ll << 31), "amalgamation: destination table exceeds int32");
     if (programs) {
-        D.resize(DL0 + n);
+        // (uninitialised: every entry is written below, the first touch
+        // spread over the threads)
+        D.resize_uninit(DL0 + n);
         lcols.resize(ns);
-        lrow.resize(lmap[ns]);
+        lrow.resize_uninit(lmap[ns]);
         urows.resize(ns);
-        ucol.resize(2 * fcol[ns]);
+        ucd.resize_uninit(fcol[ns]);
+        ucl.resize_uninit(fcol[ns]);
     }
 
     // ---- pass 3b + 4: merged index arrays, D, expand programs (parallel)
@@ -468,12 +516,16 @@ bool Amalg::build(int64_t n_, int ns, const int_t *xsup, const int_t *const *lid
                                 "amalgamation: U block (%d,%lld) not in merged row %d", a, (long long)jb, J);
                     d0 = ucol_len[J] + U.colstart[it - U.blk.begin()] + (xsup[jb] - xsup2[Jp]);
                 }
-                for (i64 c = 0; c < w; ++c, ++f0) {
-                    ucol[2 * f0] = (int32_t)(d0 + c);
-                    ucol[2 * f0 + 1] = (int32_t)ux[p + SLU_UB_DESCRIPTOR + c];
+                for (i64 c = 0; c < w; ++c) {
+                    const i64 fst = ux[p + SLU_UB_DESCRIPTOR + c];
+                    if (fst >= R.end) continue;
+                    ucd[f0] = (int32_t)(d0 + c);
+                    ucl[f0] = (uint16_t)(R.end - fst - 1);
+                    ++f0;
                 }
                 p += SLU_UB_DESCRIPTOR + w;
             }
+            SLU_REQUIRE(f0 == fcol[a + 1], "amalgamation: U row %d non-empty columns", a);
         }
         for (int32_t r : below) rowpos[r] = -1;
     }, 1);
@@ -539,8 +591,8 @@ template <typename T> void Amalg::apply(T *oL, T *oU, T *mL, T *mU, int dir) con
         const URowX &R = urows[a];
         i64 src = R.src;
         for (int c = 0; c < R.nc; ++c) {
-            const i64 d = ucol[2 * (R.c0 + c)], f = ucol[2 * (R.c0 + c) + 1], len = R.end - f;
-            T *m = (d >= DL0 ? mL : mU) + D[d] + f;
+            const i64 d = ucd[R.c0 + c], len = ucl[R.c0 + c] + 1;
+            T *m = (d >= DL0 ? mL : mU) + D[d] + R.end - len;
             for (i64 i = 0; i < len; ++i) {
                 if (dir == 0) m[i] = oU[src + i];
                 else oU[src + i] = m[i];

@@ -36,6 +36,7 @@
 #include <cstdint>
 #include <vector>
 
+#include "common.h"
 #include "slu_abi.h"
 
 namespace slu {
@@ -54,10 +55,11 @@ struct AmalgFlops {
 // never cross a1.  lidx / uidx (1x1 reference format, every block of the
 // supernode) need to be valid for [a0, a1) only.  Returns the first
 // supernode of every group in the range; fl (if given) gets the range's
-// original-partition work added.
+// original-partition work added; ucne (if given) the non-empty U column
+// entries of every supernode of the range.
 std::vector<int> amalg_chains(int64_t n, int ns, const int_t *xsup, const int_t *const *lidx,
                               const int_t *const *uidx, double zero_frac, int maxw, int a0, int a1,
-                              AmalgFlops *fl);
+                              AmalgFlops *fl, std::vector<int64_t> *ucne = nullptr);
 
 // Relayout programs (device kernels in amalg_dev.h, host mirrors in the
 // apply functions).  A column range [c0, c1) of one L block column whose
@@ -67,13 +69,16 @@ struct LColX {
     int64_t src, dst, map;
     int32_t nsupr, c0, c1, ld2;
 };
-// <= 64 column segments of one U block row: segment of column entry c0 + j
-// is o[src + ...] (segments back to back), rows [fst, end) with (D index,
-// fst) = ucol[2 (c0 + j)], landing at D[index] + fst in the coarse L (index
-// >= DL0) or U values.
+// <= 64 non-empty column segments of one U block row: segment j is
+// o[src + ...] (segments back to back), rows [end - len, end) with len =
+// ucl[c0 + j] + 1, landing at D[ucd[c0 + j]] + end - len in the coarse L
+// (index >= DL0) or U values.  Empty segments (the reference stores a first
+// row = end for them) have no program entry: 6 bytes per non-empty column
+// (100^3: 129 M of the 310 M column entries are non-empty; lengths <= the
+// widest supernode, 512).
 struct UChunk {
     int64_t src; // value offset of the chunk's first segment (caller's layout)
-    int64_t c0;  // first column entry in ucol
+    int64_t c0;  // first column entry in ucd / ucl
     int32_t nc;  // <= 64
     int32_t end; // xsup[a + 1] of the row
 };
@@ -108,21 +113,22 @@ struct Amalg {
     };
     struct URowX {       // one original U block row a
         int64_t src;     // value offset of its first segment in the original U values
-        int64_t c0;      // first of its column entries in ucol
-        int32_t nc;      // column entries (all columns of all its blocks)
+        int64_t c0;      // first of its non-empty column entries in ucd / ucl
+        int32_t nc;      // non-empty column entries (over all its blocks)
         int32_t end;     // xsup[a + 1]
         int32_t w;       // width of a (segments are at most this long)
         int32_t pad;
     };
     std::vector<LCol> lcols;
-    std::vector<int32_t> lrow;  // merged row position of every stored original L row
+    RawVec<int32_t> lrow;       // merged row position of every stored original L row
     std::vector<URowX> urows;
-    // per original U column entry (block order, column order): the D index
-    // of its coarse destination (>= DL0: inside the coarse diagonal block, in
-    // the coarse L) and the first row of its segment
-    std::vector<int32_t> ucol;  // interleaved (didx, fst)
+    // per non-empty original U column entry (block order, column order): the
+    // D index of its coarse destination (>= DL0: inside the coarse diagonal
+    // block, in the coarse L) and its segment length - 1
+    RawVec<int32_t> ucd;
+    RawVec<uint16_t> ucl;
     int64_t DL0 = 0;
-    std::vector<int64_t> D;     // merged destination base per (merged row, column)
+    RawVec<int64_t> D;          // merged destination base per (merged row, column)
     int64_t n_merged_groups = 0, zeros = 0;
     bool programs = true; // false: the coarse structure only (no expand / compress programs)
     // algorithmic work of the ORIGINAL partition (the reference's accounting,
@@ -220,7 +226,8 @@ struct GaRelay {
     std::vector<LColX> unpack_l;      // o = receive buffer, m = coarse L (k_amalg_l, dir 0)
     std::vector<int32_t> unpack_lrow; // coarse local row of every received L row
     std::vector<UChunk> unpack_u;     // o = receive buffer (k_amalg_u, dir 0)
-    std::vector<int32_t> unpack_ucol; // (D index, fst) per received U column
+    std::vector<int32_t> unpack_ucd;  // D index per received non-empty U column
+    std::vector<uint16_t> unpack_ucl; // its segment length - 1
     std::vector<int64_t> D;
     int64_t DL0 = 0;
     int64_t received = 0; // values in the receive buffer

@@ -27,7 +27,7 @@ __global__ void __launch_bounds__(256) k_amalg_l(const LColX *items, const int32
     }
 }
 
-// One wave per chunk of <= 64 columns of an original U block row (the
+// One wave per chunk of <= 64 non-empty columns of an original U block row (the
 // engine splits the rows; the top separators' rows hold thousands of columns
 // of segments up to 256 long).  The lanes fetch the chunk's column
 // descriptors and coarse destinations at once and prefix-sum the segment
@@ -38,8 +38,8 @@ __global__ void __launch_bounds__(256) k_amalg_l(const LColX *items, const int32
 
 template <typename T>
 __global__ void __launch_bounds__(256) k_amalg_u(const UChunk *chunks, int nchunks,
-                                                 const int32_t *ucol, const int64_t *D, int64_t DL0,
-                                                 T *oU, T *mL, T *mU, int dir) {
+                                                 const int32_t *ucd, const uint16_t *ucl, const int64_t *D,
+                                                 int64_t DL0, T *oU, T *mL, T *mU, int dir) {
     __shared__ int s_incl[4][64];
     __shared__ int64_t s_dst[4][64]; // coarse offset of the column's first value, kind in bit 62
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -50,10 +50,10 @@ __global__ void __launch_bounds__(256) k_amalg_u(const UChunk *chunks, int nchun
     int len = 0;
     int64_t dst = 0;
     if (lane < C.nc) {
-        const int2 e = ((const int2 *)ucol)[C.c0 + lane];
-        len = C.end - e.y;
-        dst = D[e.x] + e.y;
-        if (e.x >= DL0) dst |= KIND;
+        const int32_t d = ucd[C.c0 + lane];
+        len = (int)ucl[C.c0 + lane] + 1;
+        dst = D[d] + C.end - len;
+        if (d >= DL0) dst |= KIND;
     }
     int incl = len;
 #pragma unroll

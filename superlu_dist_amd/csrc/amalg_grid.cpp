@@ -559,16 +559,18 @@ void ga_receive_side(const GaFine &f, const GaPartition &g, const GaStreams &in,
                 SLU_REQUIRE(it != bk.end() && it->first == Jp, "grid amalgamation: coarse U block (%d,%d) missing", I, Jp);
                 ce0 = ucols[li] + it->second + (xsup[jb] - x2[Jp]);
             }
-            for (int c0 = 0; c0 < w; c0 += 64) {
-                const int nc = std::min(64, w - c0);
-                r.unpack_u.push_back({off, (i64)r.unpack_ucol.size() / 2, nc, (int32_t)end});
-                for (int c = c0; c < c0 + nc; ++c) {
-                    const i64 fst = v[p + c];
-                    const i64 didx = Jp == I ? r.DL0 + xsup[jb] + c : ce0 + c;
-                    r.unpack_ucol.push_back((int32_t)didx);
-                    r.unpack_ucol.push_back((int32_t)fst);
-                    off += end - fst;
-                }
+            // chunks of <= 64 non-empty columns
+            int nc = 0;
+            for (int c = 0; c < w; ++c) {
+                const i64 fst = v[p + c];
+                if (fst >= end) continue;
+                if (nc == 0) r.unpack_u.push_back({off, (i64)r.unpack_ucd.size(), 0, (int32_t)end});
+                const i64 didx = Jp == I ? r.DL0 + xsup[jb] + c : ce0 + c;
+                r.unpack_ucd.push_back((int32_t)didx);
+                r.unpack_ucl.push_back((uint16_t)(end - fst - 1));
+                off += end - fst;
+                r.unpack_u.back().nc = ++nc;
+                if (nc == 64) nc = 0;
             }
             p += w;
         }
@@ -612,13 +614,13 @@ template <typename T> void ga_unpack(const GaRelay &r, T *recv, T *mL, T *mU, in
         const UChunk &x = r.unpack_u[k];
         i64 src = x.src;
         for (int c = 0; c < x.nc; ++c) {
-            const i64 d = r.unpack_ucol[2 * (x.c0 + c)], fst = r.unpack_ucol[2 * (x.c0 + c) + 1];
-            T *m = (d >= r.DL0 ? mL : mU) + r.D[d] + fst;
-            for (i64 i = 0; i < x.end - fst; ++i) {
+            const i64 d = r.unpack_ucd[x.c0 + c], len = r.unpack_ucl[x.c0 + c] + 1;
+            T *m = (d >= r.DL0 ? mL : mU) + r.D[d] + x.end - len;
+            for (i64 i = 0; i < len; ++i) {
                 if (dir == 0) m[i] = recv[src + i];
                 else recv[src + i] = m[i];
             }
-            src += x.end - fst;
+            src += len;
         }
     });
 }

@@ -8,6 +8,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <exception>
+#include <memory>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -31,12 +32,33 @@ inline std::string fmt(const char *f, ...) {
 
 void set_last_error(const std::string &s);
 
-// Host threads for the plan build (SLU_PLAN_THREADS, default min(8, cores)).
+// Host array without value-initialisation: large plan tables are filled by
+// parallel passes, so the first touch (page faults) is spread over threads.
+template <typename T> struct RawVec {
+    std::unique_ptr<T[]> a;
+    size_t n = 0;
+    void resize_uninit(size_t cnt) {
+        a.reset(cnt ? new T[cnt] : nullptr);
+        n = cnt;
+    }
+    T &operator[](size_t i) { return a[i]; }
+    const T &operator[](size_t i) const { return a[i]; }
+    size_t size() const { return n; }
+    const T *data() const { return a.get(); }
+    T *data() { return a.get(); }
+    bool empty() const { return n == 0; }
+    void clear() { a.reset(); n = 0; }
+};
+
+
+// Host threads for the plan build (SLU_PLAN_THREADS; default the
+// OMP_NUM_THREADS share when set, else the cores, at most 16).
 inline int plan_threads() {
     static const int t = [] {
-        const char *e = getenv("SLU_PLAN_THREADS");
-        int v = e ? atoi(e) : (int)std::thread::hardware_concurrency();
-        return std::max(1, std::min(e ? 64 : 8, v));
+        if (const char *e = getenv("SLU_PLAN_THREADS")) return std::max(1, std::min(64, atoi(e)));
+        int v = (int)std::thread::hardware_concurrency();
+        if (const char *o = getenv("OMP_NUM_THREADS"); o && atoi(o) > 0) v = std::min(v, atoi(o));
+        return std::max(1, std::min(16, v));
     }();
     return t;
 }

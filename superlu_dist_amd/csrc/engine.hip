@@ -57,21 +57,6 @@ namespace slu {
 static thread_local std::string g_last_error;
 void set_last_error(const std::string &s) { g_last_error = s; }
 
-// Host array without value-initialisation: large plan tables are filled by
-// parallel passes, so the first touch (page faults) is spread over threads.
-template <typename T> struct RawVec {
-    std::unique_ptr<T[]> a;
-    size_t n = 0;
-    void resize_uninit(size_t cnt) {
-        a.reset(cnt ? new T[cnt] : nullptr);
-        n = cnt;
-    }
-    T &operator[](size_t i) { return a[i]; }
-    const T &operator[](size_t i) const { return a[i]; }
-    size_t size() const { return n; }
-    const T *data() const { return a.get(); }
-};
-
 template <typename T> struct DevBuf {
     T *p = nullptr;
     size_t n = 0, guard = 0;
@@ -3626,7 +3611,8 @@ struct AmalgPlan : PlanBase {
     // caller layout on the device, and the relayout programs
     DevBuf<T> d_oL, d_oU;
     DevBuf<LColX> d_lx;
-    DevBuf<int32_t> d_lrow, d_ucol;
+    DevBuf<int32_t> d_lrow, d_ucd;
+    DevBuf<uint16_t> d_ucl;
     DevBuf<UChunk> d_ur;
     DevBuf<i64> d_D;
     vector<i64> usrc; // caller U value offset per block row
@@ -3660,12 +3646,21 @@ struct AmalgPlan : PlanBase {
             if (L->Ufstnz_br_ptr[s]) uv += L->Ufstnz_br_ptr[s][1];
             P->usrc[s + 1] = uv;
         }
+        const bool prof = getenv("SLU_PROFILE_PLAN") != nullptr;
+        auto tk = t0;
+        auto tick = [&](const char *what) { // SLU_PROFILE_PLAN: phase times on stderr
+            if (!prof) return;
+            fprintf(stderr, "[slu amalg plan] %-22s %7.1f ms\n", what, ms_since(tk));
+            tk = std::chrono::steady_clock::now();
+        };
         HIPCHK(hipSetDevice(0));
+        tick("caller layout");
         P->o_lv = lv;
         P->o_uv = uv;
         // the caller-layout copies only where values cross PCIe: a plan fed
         // by fill_a and read by solve never allocates them
         if (P->opts.overlap_upload || P->opts.overlap_download) P->ensure_o();
+        tick("caller-layout alloc");
         if (P->opts.overlap_upload) {
             AmalgPlan *raw = P.get();
             P->up_thread = std::thread([raw] {
@@ -3687,9 +3682,13 @@ struct AmalgPlan : PlanBase {
             }
             SLU_REQUIRE(P->A.lval1 == lv && P->A.uval1 == uv, "amalgamation: value counts");
             P->t_amalg = ms_since(ta);
+            tick("analysis");
             P->build_inner();
+            tick("coarse plan");
             P->build_programs();
+            tick("relayout programs");
             if (P->opts.overlap_download) P->build_d2h();
+            tick("d2h programs");
         } catch (...) {
             if (P->up_thread.joinable()) P->up_thread.join();
             throw;
@@ -3754,7 +3753,7 @@ struct AmalgPlan : PlanBase {
                     for (int c0 = 0; c0 < R.nc; c0 += 64) {
                         const int nc = std::min(64, R.nc - c0);
                         ur.push_back({src, R.c0 + c0, nc, R.end});
-                        for (int c = c0; c < c0 + nc; ++c) src += R.end - A.ucol[2 * (R.c0 + c) + 1];
+                        for (int c = c0; c < c0 + nc; ++c) src += A.ucl[R.c0 + c] + 1;
                     }
                 }
                 ub_lev[L + 1] = (int)ur.size();
@@ -3765,9 +3764,14 @@ struct AmalgPlan : PlanBase {
         if (ur.empty()) ur.resize(1);
         d_lx.upload(lx);
         d_ur.upload(ur);
-        d_lrow.upload(A.lrow.empty() ? vector<int32_t>(1) : A.lrow);
-        d_ucol.upload(A.ucol.empty() ? vector<int32_t>(2) : A.ucol);
-        d_D.upload(A.D.empty() ? vector<i64>(1) : A.D);
+        auto up = [](auto &d, const auto &h) { // (a 1-element buffer for an empty table)
+            if (h.empty()) d.alloc(1);
+            else d.upload(h.data(), h.size());
+        };
+        up(d_lrow, A.lrow);
+        up(d_ucd, A.ucd);
+        up(d_ucl, A.ucl);
+        up(d_D, A.D);
     }
     int nlx = 0;
 
@@ -3780,7 +3784,7 @@ struct AmalgPlan : PlanBase {
         const int u0 = ub_lev[L0], nr = ub_lev[L1] - u0;
         if (nr > 0)
             hipLaunchKernelGGL((k_amalg_u<T>), dim3((unsigned)((nr + 3) / 4)), dim3(256), 0, st,
-                               d_ur.p + u0, nr, d_ucol.p, d_D.p, (i64)A.DL0, d_oU.p, in->d_L.p,
+                               d_ur.p + u0, nr, d_ucd.p, d_ucl.p, d_D.p, (i64)A.DL0, d_oU.p, in->d_L.p,
                                in->d_U.p, dir);
         HIPCHK(hipGetLastError());
     }
@@ -4064,7 +4068,8 @@ struct GridAmalgPlan : PlanBase {
     // device: caller layout, send / receive buffers, programs
     DevBuf<T> d_oL, d_oU, d_send, d_recv;
     DevBuf<LColX> d_pl, d_ul;
-    DevBuf<int32_t> d_plrow, d_ulrow, d_uucol;
+    DevBuf<int32_t> d_plrow, d_ulrow, d_uucd;
+    DevBuf<uint16_t> d_uucl;
     DevBuf<GaSpan> d_pu;
     DevBuf<UChunk> d_uu;
     DevBuf<i64> d_D;
@@ -4162,7 +4167,8 @@ struct GridAmalgPlan : PlanBase {
         up(d_ul, r.unpack_l);
         up(d_ulrow, r.unpack_lrow);
         up(d_uu, r.unpack_u);
-        up(d_uucol, r.unpack_ucol);
+        up(d_uucd, r.unpack_ucd);
+        up(d_uucl, r.unpack_ucl);
         up(d_D, r.D);
         d_send.alloc(std::max<i64>(r.soff[P], 1));
         d_recv.alloc(std::max<i64>(r.received, 1));
@@ -4228,7 +4234,7 @@ struct GridAmalgPlan : PlanBase {
         launch_l(d_ul, r.unpack_l.size(), d_ulrow, d_recv.p, in->d_L.p, 0, st);
         if (!r.unpack_u.empty())
             hipLaunchKernelGGL((k_amalg_u<T>), dim3((unsigned)((r.unpack_u.size() + 3) / 4)), dim3(256), 0, st,
-                               d_uu.p, (int)r.unpack_u.size(), d_uucol.p, d_D.p, (i64)r.DL0, d_recv.p, in->d_L.p,
+                               d_uu.p, (int)r.unpack_u.size(), d_uucd.p, d_uucl.p, d_D.p, (i64)r.DL0, d_recv.p, in->d_L.p,
                                in->d_U.p, 0);
         HIPCHK(hipGetLastError());
         HIPCHK(hipStreamSynchronize(st));
@@ -4240,7 +4246,7 @@ struct GridAmalgPlan : PlanBase {
         launch_l(d_ul, r.unpack_l.size(), d_ulrow, d_recv.p, in->d_L.p, 1, st);
         if (!r.unpack_u.empty())
             hipLaunchKernelGGL((k_amalg_u<T>), dim3((unsigned)((r.unpack_u.size() + 3) / 4)), dim3(256), 0, st,
-                               d_uu.p, (int)r.unpack_u.size(), d_uucol.p, d_D.p, (i64)r.DL0, d_recv.p, in->d_L.p,
+                               d_uu.p, (int)r.unpack_u.size(), d_uucd.p, d_uucl.p, d_D.p, (i64)r.DL0, d_recv.p, in->d_L.p,
                                in->d_U.p, 1);
         HIPCHK(hipGetLastError());
         exchange(false);

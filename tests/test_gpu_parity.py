@@ -245,23 +245,32 @@ def test_gpu_reference_structure_fingerprints_match_reference_pdgstrf():
     assert c["match"] and c["rel_err"] <= 1e-12, c
 
 
-def test_dropin_plan_cache_refactors_new_values(monkeypatch):
+def test_dropin_plan_cache_refactors_new_values(monkeypatch, capfd):
     """The drop-in keeps its last 1x1 plan (pdgssvx's SamePattern_SameRowPerm
     refactorization, abi.cpp): a second pdgstrf on the same LUstruct with new
-    values must factor the NEW values; a second LUstruct of the same pattern
-    (its own arrays) must not be served by the first one's plan."""
+    values must factor the NEW values -- with Fact = DOFACT (full structure
+    digest) and with Fact = SamePattern_SameRowPerm (shallow digest: the
+    caller's contract is the previous L & U structures) -- and a second
+    LUstruct of the same pattern (its own arrays) must not be served by the
+    first one's plan."""
     from superlu_dist_amd import capi
+    monkeypatch.setenv("SUPERLU_MI355X_TIMING", "1")
     A = Csc.stencil(STENCIL_3D7, 16, 16, 16)
     S = Symbolic(A, nd_order(16, 16, 16), 60, 256, reference=True)
     lu, ref = S.distribute(), S.distribute()
     L0, U0 = lu.Lval.copy(), lu.Uval.copy()
-    for scale in (1.0, 2.0, 0.5):             # same structure, new values each call
+    opt = capi.default_options()
+    for fact, scale in ((0, 1.0), (0, 2.0), (2, 0.5), (2, 3.0)):   # same structure, new values
         lu.Lval[:] = L0 * scale
         lu.Uval[:] = U0 * scale
         ref.Lval[:] = L0 * scale
         ref.Uval[:] = U0 * scale
-        rv, info, _ = capi.pxgstrf(lu, 12.0 * scale)
+        opt.Fact = fact
+        capfd.readouterr()
+        rv, info, _ = capi.pxgstrf(lu, 12.0 * scale, options=opt)
         assert rv == 0 and info == 0
+        if scale != 1.0:
+            assert "plan reused" in capfd.readouterr().err, (fact, scale)
         pyoracle.oracle_factor([ref], 1, 1, A.n, False, 12.0 * scale)
         err = cases.factor_error([lu], [(ref.Lval, ref.Uval)])
         assert err < TOL[0], (scale, err)
