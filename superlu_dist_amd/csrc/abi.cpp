@@ -27,6 +27,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <future>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -438,21 +439,28 @@ int_t pxgstrf(int dtype, const char *name, superlu_dist_options_t *options, int 
         const bool cache = !(pc && !strcmp(pc, "0"));
         const int rt = options->ReplaceTinyPivot == SLU_YES;
         uint64_t dg = 0, sdg = 0;
+        // a miss on the shallow digest is a miss: the full digest is then
+        // only stored with the new plan, and is computed beside its build
+        std::future<uint64_t> dg_later;
         if (cache) {
             sdg = shallow_digest(LUstruct, n, grid);
-            bool hit = false;
-            if (options->Fact == SLU_SAMEPATTERN_SAMEROWPERM) {
-                // the previous factorization's L & U structures, by contract
+            bool hit;
+            {
                 std::lock_guard<std::mutex> lk(g_cache_mu);
                 hit = g_cache.plan && g_cache.shallow == sdg && g_cache.key == lu_key(LUstruct) &&
                       g_cache.dtype == dtype && g_cache.n == n && g_cache.replace_tiny == rt;
                 if (hit) dg = g_cache.digest;
             }
-            if (!hit) {
-                dg = structure_digest(LUstruct, n, grid);
-                std::lock_guard<std::mutex> lk(g_cache_mu);
-                hit = g_cache.plan && g_cache.digest == dg && g_cache.dtype == dtype && g_cache.n == n &&
-                      g_cache.replace_tiny == rt;
+            // Fact = SamePattern_SameRowPerm: the previous factorization's L & U
+            // structures, by contract; otherwise every index array is hashed
+            if (hit && options->Fact != SLU_SAMEPATTERN_SAMEROWPERM) {
+                const uint64_t full = structure_digest(LUstruct, n, grid);
+                hit = full == dg;
+                dg = full;
+            } else if (!hit) {
+                dg_later = std::async(std::launch::async, [LUstruct, n, grid] {
+                    return structure_digest(LUstruct, n, grid);
+                });
             }
             hit = all_ranks(hit, grid);
             std::lock_guard<std::mutex> lk(g_cache_mu);
@@ -545,6 +553,7 @@ int_t pxgstrf(int dtype, const char *name, superlu_dist_options_t *options, int 
         stat->ops[SLU_PHASE_FACT] = (float)(st.schur_flops + st.panel_flops);
         stat->TinyPivots += tiny;
         stat->gpu_buffer = (float)(st.lu_bytes + st.index_bytes);
+        if (dg_later.valid()) dg = dg_later.get();
         if (cache) {
             std::lock_guard<std::mutex> lk(g_cache_mu);
             g_cache.plan = plan;

@@ -30,19 +30,6 @@ struct SnInfo {
     bool sym = false, nested = false, ok = false;
 };
 
-// rows of L(:,s) below the diagonal block, in index order
-inline void below_rows(const int_t *ix, int s, std::vector<int32_t> &out) {
-    out.clear();
-    if (!ix) return;
-    i64 p = SLU_BC_HEADER;
-    for (i64 b = 0; b < ix[0]; ++b) {
-        const i64 gb = ix[p], nr = ix[p + 1];
-        if (gb != s)
-            for (i64 i = 0; i < nr; ++i) out.push_back((int32_t)ix[p + 2 + i]);
-        p += SLU_LB_DESCRIPTOR + nr;
-    }
-}
-
 // columns of U(s,:) with a non-empty segment, with their first rows
 template <typename F> inline void for_ucols(const int_t *ux, const int_t *xsup, F &&f) {
     if (!ux) return;
@@ -55,6 +42,23 @@ template <typename F> inline void for_ucols(const int_t *ux, const int_t *xsup, 
 }
 
 } // namespace
+
+// U row J of the coarse partition: merged block columns J' with the first
+// rows of every column
+struct Amalg::URow {
+    std::vector<int> blk;      // J' ascending
+    std::vector<int32_t> fst;  // all columns of all blocks, first row (end: empty)
+    std::vector<i64> colstart; // per block: first column entry
+};
+// what pass 4 (the programs) needs from passes 1-3
+struct Amalg::Work {
+    const int_t *xsup = nullptr;
+    const int_t *const *lidx = nullptr;
+    const int_t *const *uidx = nullptr;
+    std::vector<int> gstart;
+    std::vector<URow> urow;
+    std::vector<i64> lval_len, ucol_len, lsrc, usrc, lmap, fcol;
+};
 
 std::vector<int> amalg_chains(int64_t n, int ns, const int_t *xsup, const int_t *const *lidx,
                               const int_t *const *uidx, double zero_frac, int maxw, int a0, int a1,
@@ -295,15 +299,18 @@ bool Amalg::build(int64_t n_, int ns, const int_t *xsup, const int_t *const *lid
     uval1 = usrc[ns];
 
     // ---- pass 3a: merged structure sizes per J (parallel)
-    // U row J: merged block columns J' with the first rows of every column
-    struct URow {
-        std::vector<int> blk;           // J' ascending
-        std::vector<int32_t> fst;       // all columns of all blocks, first row (end: empty)
-        std::vector<i64> colstart;      // per block: first column entry
-    };
-    std::vector<URow> urow(ns2);
-    std::vector<i64> lidx_len(ns2 + 1, 0), lval_len(ns2 + 1, 0), uidx_len(ns2 + 1, 0),
-        uval_len(ns2 + 1, 0), ucol_len(ns2 + 1, 0);
+    work.reset(new Work);
+    Work &wk = *work;
+    wk.xsup = xsup;
+    wk.lidx = lidx;
+    wk.uidx = uidx;
+    wk.gstart = gstart;
+    std::vector<URow> &urow = wk.urow;
+    urow.resize(ns2);
+    std::vector<i64> &lval_len = wk.lval_len, &ucol_len = wk.ucol_len;
+    lval_len.assign(ns2 + 1, 0);
+    ucol_len.assign(ns2 + 1, 0);
+    std::vector<i64> lidx_len(ns2 + 1, 0), uidx_len(ns2 + 1, 0), uval_len(ns2 + 1, 0);
     std::vector<int> nblk2(ns2, 0);
     parallel_for(ns2, [&](int J) {
         thread_local std::vector<int32_t> ff;
@@ -365,8 +372,9 @@ bool Amalg::build(int64_t n_, int ns, const int_t *xsup, const int_t *const *lid
     tick("pass 3a (merged sizes)");
     lval2 = lval_len[ns2];
     uval2 = uval_len[ns2];
-    Lidx2.resize(lidx_len[ns2]);
-    Uidx2.resize(uidx_len[ns2]);
+    if (on_sizes) on_sizes(lval2, uval2);
+    Lidx2.resize_uninit(lidx_len[ns2]);
+    Uidx2.resize_uninit(uidx_len[ns2]);
     Loff2.assign(ns2, -1);
     Lvoff2.assign(ns2, -1);
     Uoff2.assign(ns2, -1);
@@ -374,22 +382,10 @@ bool Amalg::build(int64_t n_, int ns, const int_t *xsup, const int_t *const *lid
     // D: U-kind entries (one per merged U column entry), then L-kind (w_J per J)
     DL0 = ucol_len[ns2];
     SLU_REQUIRE(DL0 + n < (1ll << 31), "amalgamation: destination table exceeds int32");
-    if (programs) {
-        // (uninitialised: every entry is written below, the first touch
-        // spread over the threads)
-        D.resize_uninit(DL0 + n);
-        lcols.resize(ns);
-        lrow.resize_uninit(lmap[ns]);
-        urows.resize(ns);
-        ucd.resize_uninit(fcol[ns]);
-        ucl.resize_uninit(fcol[ns]);
-    }
 
-    // ---- pass 3b + 4: merged index arrays, D, expand programs (parallel)
+    // ---- pass 3b: merged index arrays (parallel)
     parallel_for(ns2, [&](int J) {
-        thread_local std::vector<int32_t> rowpos;
-        if ((i64)rowpos.size() < n) rowpos.assign(n, -1);
-        const int s0 = gstart[J], e = gstart[J + 1] - 1, wJ = W2(J);
+        const int e = gstart[J + 1] - 1, wJ = W2(J);
         const i64 x2J = xsup2[J], endJ = xsup2[J + 1];
         const i64 nsupr2 = (lval_len[J + 1] - lval_len[J]) / wJ;
         // L index
@@ -403,8 +399,6 @@ bool Amalg::build(int64_t n_, int ns, const int_t *xsup, const int_t *const *lid
         L[q + 1] = wJ;
         for (int c = 0; c < wJ; ++c) L[q + 2 + c] = x2J + c;
         q += SLU_LB_DESCRIPTOR + wJ;
-        std::vector<int32_t> below;
-        below_rows(lidx[e], e, below);
         {
             const int_t *ix = lidx[e];
             i64 p = SLU_BC_HEADER, desc = -1, last = -1;
@@ -431,15 +425,13 @@ bool Amalg::build(int64_t n_, int ns, const int_t *xsup, const int_t *const *lid
         // destination addresses in runs)
         {
             i64 p = SLU_BC_HEADER + SLU_LB_DESCRIPTOR + wJ;
-            int32_t r = wJ;
             for (i64 b = 1; b < L[0]; ++b) {
                 const i64 nr = L[p + 1];
                 std::sort(L + p + 2, L + p + 2 + nr);
-                for (i64 i = 0; i < nr; ++i) rowpos[L[p + 2 + i]] = r++;
                 p += SLU_LB_DESCRIPTOR + nr;
             }
         }
-        // U index + D (U kind)
+        // U index
         const URow &U = urow[J];
         if (!U.blk.empty()) {
             Uoff2[J] = uidx_len[J];
@@ -450,8 +442,7 @@ bool Amalg::build(int64_t n_, int ns, const int_t *xsup, const int_t *const *lid
             X[1] = uval_len[J + 1] - uval_len[J];
             X[2] = len1;
             X[len1] = -1;
-            i64 p = SLU_BR_HEADER, ce = 0, seg = 0;
-            const i64 d0 = ucol_len[J];
+            i64 p = SLU_BR_HEADER, ce = 0;
             for (size_t b = 0; b < U.blk.size(); ++b) {
                 const int Jp = U.blk[b];
                 X[p] = Jp;
@@ -459,18 +450,84 @@ bool Amalg::build(int64_t n_, int ns, const int_t *xsup, const int_t *const *lid
                 for (int c = 0; c < W2(Jp); ++c, ++ce) {
                     const int32_t f = U.fst[ce];
                     X[p + SLU_UB_DESCRIPTOR + c] = f;
-                    if (programs) D[d0 + ce] = Uvoff2[J] + seg - f;
-                    seg += endJ - f;
                     nnz += endJ - f;
                 }
                 X[p + 1] = nnz;
                 p += SLU_UB_DESCRIPTOR + W2(Jp);
             }
         }
+    }, 1);
+    tick("pass 3b (merged index arrays)");
+    // explicit zeros introduced
+    zeros = (lval2 + uval2) - (lval1 + uval1);
+    wk.lsrc = std::move(lsrc);
+    wk.usrc = std::move(usrc);
+    wk.lmap = std::move(lmap);
+    wk.fcol = std::move(fcol);
+    if (!programs) work.reset();
+    else if (!defer_programs) build_programs();
+    return true;
+}
+
+Amalg::Amalg() = default;
+Amalg::~Amalg() = default;
+
+// ---- pass 4: D, the expand programs (parallel over merged supernodes; the
+// index arrays of pass 3b give every group's row positions)
+void Amalg::build_programs() {
+    SLU_REQUIRE(work, "amalgamation: programs without an analysis");
+    const bool prof = getenv("SLU_AMALG_TIME") != nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
+    Work &wk = *work;
+    const int_t *xsup = wk.xsup;
+    const int_t *const *lidx = wk.lidx;
+    const int_t *const *uidx = wk.uidx;
+    const std::vector<int> &gstart = wk.gstart;
+    const std::vector<i64> &lsrc = wk.lsrc, &usrc = wk.usrc, &lmap = wk.lmap, &fcol = wk.fcol,
+                           &lval_len = wk.lval_len, &ucol_len = wk.ucol_len;
+    const int ns = ns1;
+    auto W = [&](i64 k) { return (int)(xsup[k + 1] - xsup[k]); };
+    auto W2 = [&](i64 J) { return (int)(xsup2[J + 1] - xsup2[J]); };
+    // (uninitialised: every entry is written below, the first touch spread
+    // over the threads)
+    D.resize_uninit(DL0 + n);
+    lcols.resize(ns);
+    lrow.resize_uninit(lmap[ns]);
+    urows.resize(ns);
+    ucd.resize_uninit(fcol[ns]);
+    ucl.resize_uninit(fcol[ns]);
+    parallel_for(ns2, [&](int J) {
+        thread_local std::vector<int32_t> rowpos;
+        if ((i64)rowpos.size() < n) rowpos.assign(n, -1);
+        const int s0 = gstart[J], e = gstart[J + 1] - 1, wJ = W2(J);
+        const i64 x2J = xsup2[J], endJ = xsup2[J + 1];
+        const i64 nsupr2 = (lval_len[J + 1] - lval_len[J]) / wJ;
+        const int_t *L = Lidx2.data() + Loff2[J];
+        {
+            i64 p = SLU_BC_HEADER + SLU_LB_DESCRIPTOR + wJ;
+            int32_t r = wJ;
+            for (i64 b = 1; b < L[0]; ++b) {
+                const i64 nr = L[p + 1];
+                for (i64 i = 0; i < nr; ++i) rowpos[L[p + 2 + i]] = r++;
+                p += SLU_LB_DESCRIPTOR + nr;
+            }
+        }
+        // D (U kind)
+        const URow &U = wk.urow[J];
+        if (!U.blk.empty()) {
+            i64 ce = 0, seg = 0;
+            const i64 d0 = ucol_len[J];
+            for (size_t b = 0; b < U.blk.size(); ++b)
+                for (int c = 0; c < W2(U.blk[b]); ++c, ++ce) {
+                    const int32_t f = U.fst[ce];
+                    D[d0 + ce] = Uvoff2[J] + seg - f;
+                    seg += endJ - f;
+                }
+        }
         // D (L kind): row fst of column g inside J -> Lvoff2 + (g - x2J) * ld2 + fst - x2J
-        for (int c = 0; programs && c < wJ; ++c) D[DL0 + x2J + c] = Lvoff2[J] + (i64)c * nsupr2 - x2J;
+        for (int c = 0; c < wJ; ++c) D[DL0 + x2J + c] = Lvoff2[J] + (i64)c * nsupr2 - x2J;
         // expand programs of the members
-        for (int a = s0; programs && a <= e; ++a) {
+        for (int a = s0; a <= e; ++a) {
             const int_t *ix = lidx[a];
             LCol &C = lcols[a];
             C.src = lsrc[a];
@@ -527,12 +584,19 @@ bool Amalg::build(int64_t n_, int ns, const int_t *xsup, const int_t *const *lid
             }
             SLU_REQUIRE(f0 == fcol[a + 1], "amalgamation: U row %d non-empty columns", a);
         }
-        for (int32_t r : below) rowpos[r] = -1;
+        {
+            i64 p = SLU_BC_HEADER + SLU_LB_DESCRIPTOR + wJ;
+            for (i64 b = 1; b < L[0]; ++b) {
+                const i64 nr = L[p + 1];
+                for (i64 q = 0; q < nr; ++q) rowpos[L[p + 2 + q]] = -1;
+                p += SLU_LB_DESCRIPTOR + nr;
+            }
+        }
     }, 1);
-    tick("pass 3b/4 (merged arrays, programs)");
-    // explicit zeros introduced
-    zeros = (lval2 + uval2) - (lval1 + uval1);
-    return true;
+    work.reset(); // (the analysis state is not needed again)
+    if (prof)
+        fprintf(stderr, "[slu amalg] pass 4 (programs) %.1f ms\n",
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
 }
 
 void Amalg::coarse_glu(std::vector<int_t> &xlsub, std::vector<int_t> &lsub,

@@ -34,6 +34,7 @@
 // column) base table D, so that a U segment (a, g) lands at D + fst.
 #pragma once
 #include <cstdint>
+#include <functional>
 #include <vector>
 
 #include "common.h"
@@ -95,7 +96,7 @@ struct Amalg {
     std::vector<int_t> supno2;       // n
     std::vector<int> grp;            // original supernode -> merged
     // merged LUstruct, 1x1, flat reference formats (slu_lustruct_build's inputs)
-    std::vector<int_t> Lidx2, Uidx2;
+    RawVec<int_t> Lidx2, Uidx2;      // (every entry written by the analysis)
     std::vector<int64_t> Loff2, Lvoff2, Uoff2, Uvoff2; // per merged supernode, -1 if empty
     int64_t lval2 = 0, uval2 = 0;                       // value counts (no spare element)
     // original value layout: contiguous per block column / row in supernode order
@@ -131,6 +132,10 @@ struct Amalg {
     RawVec<int64_t> D;          // merged destination base per (merged row, column)
     int64_t n_merged_groups = 0, zeros = 0;
     bool programs = true; // false: the coarse structure only (no expand / compress programs)
+    // called by build() once lval2 / uval2 are known (before the coarse
+    // index arrays and the programs are built): the plan allocates the coarse
+    // storage beside the rest of the analysis
+    std::function<void(int64_t, int64_t)> on_sizes;
     // algorithmic work of the ORIGINAL partition (the reference's accounting,
     // SURVEY 8d; the plan's own counts are the coarse partition's): real-flop
     // sums, weighted by value type in the plan
@@ -140,9 +145,21 @@ struct Amalg {
     double fl_s1 = 0, fl_s2 = 0, fl_w = 0; // diagonal LU: w(w-1)/2, (w-1)w(2w-1)/6, w
 
     // Builds everything from a 1x1 LUstruct's index arrays.  Returns false
-    // when no two supernodes merge (the plan then runs the original).
+    // when no two supernodes merge (the plan then runs the original).  With
+    // defer_programs, build() stops after the coarse index arrays and
+    // build_programs() (which needs the same index arrays alive) builds D and
+    // the expand / compress programs: the plan runs it beside the coarse plan.
     bool build(int64_t n, int nsupers, const int_t *xsup, const int_t *const *lidx,
                const int_t *const *uidx, double zero_frac, int maxw);
+    bool defer_programs = false;
+    void build_programs();
+    Amalg();
+    ~Amalg();
+    Amalg(const Amalg &) = delete;
+    Amalg &operator=(const Amalg &) = delete;
+    struct URow;
+    struct Work;
+    std::unique_ptr<Work> work;
 
     // The coarse partition as a symbolic factorization (symbfact's
     // Glu_freeable arrays, for the structural distribute on any grid):

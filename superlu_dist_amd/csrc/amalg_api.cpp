@@ -57,10 +57,10 @@ void slu_amalg_arrays(const void *h, int64_t *xsup2, int64_t *supno2, int64_t *L
     const Amalg *A = (const Amalg *)h;
     std::copy(A->xsup2.begin(), A->xsup2.end(), xsup2);
     std::copy(A->supno2.begin(), A->supno2.end(), supno2);
-    std::copy(A->Lidx2.begin(), A->Lidx2.end(), Lidx2);
+    std::copy(A->Lidx2.data(), A->Lidx2.data() + A->Lidx2.size(), Lidx2);
     std::copy(A->Loff2.begin(), A->Loff2.end(), Loff2);
     std::copy(A->Lvoff2.begin(), A->Lvoff2.end(), Lvoff2);
-    std::copy(A->Uidx2.begin(), A->Uidx2.end(), Uidx2);
+    std::copy(A->Uidx2.data(), A->Uidx2.data() + A->Uidx2.size(), Uidx2);
     std::copy(A->Uoff2.begin(), A->Uoff2.end(), Uoff2);
     std::copy(A->Uvoff2.begin(), A->Uvoff2.end(), Uvoff2);
 }

@@ -85,6 +85,11 @@ template <typename T> struct DevBuf {
         n = cnt;
         guard = g;
     }
+    void swap(DevBuf &o) {
+        std::swap(p, o.p);
+        std::swap(n, o.n);
+        std::swap(guard, o.guard);
+    }
     void upload(const vector<T> &v) { upload(v.data(), v.size()); }
     void upload(const RawVec<T> &v) { upload(v.data(), v.size()); }
     void upload(const T *h, size_t cnt) {
@@ -577,8 +582,11 @@ struct Plan : PlanBase {
     bool fast_w(int w) const { return w <= FAST_MAXW; }
     i64 dinv_len(int w) const { return fast_w(w) ? 2 * (i64)((w + PW - 1) / PW) * PW * PW : 0; }
 
+    // pre (optional): the L / U value storage allocated ahead by the caller
+    // (an amalgamated plan allocates it beside its analysis: fresh HBM costs
+    // ~28 ms per GB), adopted when its sizes are this layout's
     Plan(LUS *lu, int n_, int nprow, int npcol, int iam_, slu_comm *c,
-         const slu_engine_opts *o) {
+         const slu_engine_opts *o, DevBuf<T> *pre = nullptr) {
         LU = lu;
         n = n_;
         Pr = nprow;
@@ -651,8 +659,14 @@ struct Plan : PlanBase {
         prof = getenv("SLU_PROFILE_PLAN") != nullptr;
         tprev = t0;
         value_layout();
-        d_L.alloc_guarded(std::max<i64>(lval_total, 1), SB_UGUARD);
-        d_U.alloc_guarded(std::max<i64>(uval_total, 1), SB_UGUARD);
+        if (pre && pre[0].n == (size_t)std::max<i64>(lval_total, 1) && pre[0].guard == SB_UGUARD &&
+            pre[1].n == (size_t)std::max<i64>(uval_total, 1) && pre[1].guard == SB_UGUARD) {
+            d_L.swap(pre[0]);
+            d_U.swap(pre[1]);
+        } else {
+            d_L.alloc_guarded(std::max<i64>(lval_total, 1), SB_UGUARD);
+            d_U.alloc_guarded(std::max<i64>(uval_total, 1), SB_UGUARD);
+        }
         tick("layout + alloc");
         if (opts.overlap_upload) {
             // the H2D copy of the values runs beside the rest of the plan
@@ -2442,7 +2456,7 @@ struct Plan : PlanBase {
             HIPCHK(hipStreamCreateWithPriority(&cs, hipStreamNonBlocking,
                                                pe && !strcmp(pe, "hi") ? prio_hi : prio_lo));
             const char *ge = getenv("SLU_D2H_WG");
-            const int nwg = ge ? std::max(1, atoi(ge)) : 32;
+            const int nwg = ge ? std::max(1, atoi(ge)) : 128; // (32: +25 ms of tail at 100^3, tools/d2h_variants.py)
             const char *me = getenv("SLU_D2H_MODE"); // diagnostics: push (zero-copy) | sdma
             const bool use_sdma = !(me && !strcmp(me, "push"));
             if (use_sdma && d_stage.n < (size_t)NS * D2H_SLOT) d_stage.alloc((size_t)NS * D2H_SLOT);
@@ -3618,6 +3632,12 @@ struct AmalgPlan : PlanBase {
     vector<i64> usrc; // caller U value offset per block row
     std::thread up_thread;
     std::string up_err;
+    // the coarse L / U storage, allocated beside the analysis as soon as its
+    // sizes are known (after pass 3a), adopted by the inner plan
+    DevBuf<T> pre[2];
+    std::thread alloc_thread;
+    std::string alloc_err;
+    std::mutex o_mu; // ensure_o: the upload thread or the D2H program build
     double up_ms = 0, h2d_bytes = 0;
     double t_amalg = 0, t_plan = 0, t_expand = 0, t_compress = 0, t_d2h = 0;
     bool coarse_current = false; // d_oL / d_oU stale: the coarse storage holds newer values
@@ -3658,9 +3678,21 @@ struct AmalgPlan : PlanBase {
         P->o_lv = lv;
         P->o_uv = uv;
         // the caller-layout copies only where values cross PCIe: a plan fed
-        // by fill_a and read by solve never allocates them
-        if (P->opts.overlap_upload || P->opts.overlap_download) P->ensure_o();
+        // by fill_a and read by solve never allocates them (the upload thread
+        // allocates them itself, beside the analysis)
+        if (!P->opts.overlap_upload && P->opts.overlap_download) P->ensure_o();
         tick("caller-layout alloc");
+        P->A.on_sizes = [raw = P.get()](int64_t lv2, int64_t uv2) {
+            raw->alloc_thread = std::thread([raw, lv2, uv2] {
+                try {
+                    HIPCHK(hipSetDevice(0));
+                    raw->pre[0].alloc_guarded(std::max<i64>(lv2, 1), SB_UGUARD);
+                    raw->pre[1].alloc_guarded(std::max<i64>(uv2, 1), SB_UGUARD);
+                } catch (const std::exception &e) {
+                    raw->alloc_err = e.what();
+                }
+            });
+        };
         if (P->opts.overlap_upload) {
             AmalgPlan *raw = P.get();
             P->up_thread = std::thread([raw] {
@@ -3676,13 +3708,19 @@ struct AmalgPlan : PlanBase {
             vector<const int_t *> li(L->Lrowind_bc_ptr, L->Lrowind_bc_ptr + ns),
                 ui(L->Ufstnz_br_ptr, L->Ufstnz_br_ptr + ns);
             const auto ta = std::chrono::steady_clock::now();
+            P->A.defer_programs = true;
             if (!P->A.build(n_, ns, xsup, li.data(), ui.data(), zero_frac, maxw)) {
                 if (P->up_thread.joinable()) P->up_thread.join();
+                if (P->alloc_thread.joinable()) P->alloc_thread.join();
                 return nullptr;
             }
             SLU_REQUIRE(P->A.lval1 == lv && P->A.uval1 == uv, "amalgamation: value counts");
             P->t_amalg = ms_since(ta);
             tick("analysis");
+            // the relayout programs (host pass 4; beside the coarse plan's
+            // build it only slowed both down on the box's 16 cores)
+            P->A.build_programs();
+            tick("programs (host)");
             P->build_inner();
             tick("coarse plan");
             P->build_programs();
@@ -3691,6 +3729,8 @@ struct AmalgPlan : PlanBase {
             tick("d2h programs");
         } catch (...) {
             if (P->up_thread.joinable()) P->up_thread.join();
+            if (P->alloc_thread.joinable()) P->alloc_thread.join();
+            if (P->prog_thread.joinable()) P->prog_thread.join();
             throw;
         }
         P->t_plan = ms_since(t0);
@@ -3714,7 +3754,9 @@ struct AmalgPlan : PlanBase {
         mlu.Llu = &mllu;
         slu_engine_opts io = opts;
         io.overlap_upload = io.overlap_download = 0;
-        in.reset(new Inner(&mlu, n, 1, 1, 0, nullptr, &io));
+        if (alloc_thread.joinable()) alloc_thread.join();
+        SLU_REQUIRE(alloc_err.empty(), "%s", alloc_err.c_str());
+        in.reset(new Inner(&mlu, n, 1, 1, 0, nullptr, &io, pre));
     }
 
     // Programs in level order of the coarse plan (so the D2H can compress a
@@ -3739,44 +3781,76 @@ struct AmalgPlan : PlanBase {
             lx.insert(lx.end(), bl[L].begin(), bl[L].end());
             lx_lev[L + 1] = (int)lx.size();
         }
-        // U: the original block rows in level order, in chunks of <= 64 columns
-        vector<UChunk> ur;
+        // U: the original block rows in level order, in chunks of <= 64
+        // non-empty columns (chunk counts in order, then the rows in parallel)
+        ur_h.clear();
         {
             vector<vector<int>> rows(nl);
             for (int s = 0; s < ns; ++s)
                 if (A.urows[s].nc) rows[lev(s)].push_back(s);
+            vector<int> order;
+            order.reserve(ns);
+            vector<i64> first(ns + 1, 0);
             ub_lev.assign(nl + 1, 0);
+            i64 nch = 0;
             for (int L = 0; L < nl; ++L) {
                 for (int s : rows[L]) {
-                    const Amalg::URowX &R = A.urows[s];
-                    i64 src = R.src;
-                    for (int c0 = 0; c0 < R.nc; c0 += 64) {
-                        const int nc = std::min(64, R.nc - c0);
-                        ur.push_back({src, R.c0 + c0, nc, R.end});
-                        for (int c = c0; c < c0 + nc; ++c) src += A.ucl[R.c0 + c] + 1;
-                    }
+                    first[order.size()] = nch;
+                    order.push_back(s);
+                    nch += (A.urows[s].nc + 63) / 64;
                 }
-                ub_lev[L + 1] = (int)ur.size();
+                ub_lev[L + 1] = (int)nch;
             }
+            ur_h.resize(nch);
+            parallel_for((int)order.size(), [&](int i) {
+                const Amalg::URowX &R = A.urows[order[i]];
+                i64 src = R.src, k = first[i];
+                for (int c0 = 0; c0 < R.nc; c0 += 64) {
+                    const int nc = std::min(64, R.nc - c0);
+                    ur_h[k++] = {src, R.c0 + c0, nc, R.end};
+                    for (int c = c0; c < c0 + nc; ++c) src += A.ucl[R.c0 + c] + 1;
+                }
+            }, 256);
         }
         nlx = (int)lx.size();
         if (lx.empty()) lx.push_back({0, 0, 0, 0, 0, 0, 0});
-        if (ur.empty()) ur.resize(1);
-        d_lx.upload(lx);
-        d_ur.upload(ur);
-        auto up = [](auto &d, const auto &h) { // (a 1-element buffer for an empty table)
-            if (h.empty()) d.alloc(1);
-            else d.upload(h.data(), h.size());
-        };
-        up(d_lrow, A.lrow);
-        up(d_ucd, A.ucd);
-        up(d_ucl, A.ucl);
-        up(d_D, A.D);
+        if (ur_h.empty()) ur_h.resize(1);
+        lx_h = std::move(lx);
+        // the tables go up on a helper thread (1.5 GB at 100^3): the first
+        // relayout joins it (programs_ready)
+        prog_thread = std::thread([this] {
+            try {
+                HIPCHK(hipSetDevice(0));
+                auto up = [](auto &d, const auto &h) { // (a 1-element buffer for an empty table)
+                    if (h.empty()) d.alloc(1);
+                    else d.upload(h.data(), h.size());
+                };
+                up(d_lx, lx_h);
+                up(d_ur, ur_h);
+                up(d_lrow, A.lrow);
+                up(d_ucd, A.ucd);
+                up(d_ucl, A.ucl);
+                up(d_D, A.D);
+            } catch (const std::exception &e) {
+                prog_err = e.what();
+            }
+        });
+    }
+    vector<LColX> lx_h;
+    vector<UChunk> ur_h;
+    std::thread prog_thread;
+    std::string prog_err;
+    std::mutex prog_mu;
+    void programs_ready() {
+        std::lock_guard<std::mutex> lk(prog_mu);
+        if (prog_thread.joinable()) prog_thread.join();
+        SLU_REQUIRE(prog_err.empty(), "%s", prog_err.c_str());
     }
     int nlx = 0;
 
     // levels [L0, L1) of the relayout on stream st
     void relayout_levels(int dir, int L0, int L1, hipStream_t st) {
+        programs_ready();
         const int a = lx_lev[L0], b = lx_lev[L1];
         if (b > a)
             hipLaunchKernelGGL((k_amalg_l<T>), dim3(b - a), dim3(256), 0, st, d_lx.p + a, d_lrow.p,
@@ -3797,6 +3871,7 @@ struct AmalgPlan : PlanBase {
     // d_oU on the D2H stream.
     int compressed_to = 0;
     void build_d2h() {
+        ensure_o(); // (the push programs address d_oL / d_oU)
         Inner &P = *in;
         LocalLU *Llu = LU->Llu;
         const int_t *xsup = LU->Glu_persist->xsup;
@@ -3874,6 +3949,7 @@ struct AmalgPlan : PlanBase {
 
     i64 o_lv = 0, o_uv = 0;
     void ensure_o() {
+        std::lock_guard<std::mutex> lk(o_mu);
         if (d_oL.p) return;
         d_oL.alloc(std::max<i64>(o_lv, 1));
         d_oU.alloc(std::max<i64>(o_uv, 1));
@@ -4028,6 +4104,8 @@ struct AmalgPlan : PlanBase {
     void check_exchange(int64_t *nsec, int64_t *nbytes) override { in->check_exchange(nsec, nbytes); }
     ~AmalgPlan() override {
         if (up_thread.joinable()) up_thread.join();
+        if (alloc_thread.joinable()) alloc_thread.join();
+        if (prog_thread.joinable()) prog_thread.join();
     }
 };
 

@@ -1,0 +1,7 @@
+#!/bin/bash
+# Round 4: D2H pipeline knobs on the cached drop-in call at 100^3.
+set -o pipefail
+export TMPDIR=/tmp
+O=gpurun_out/r04k; mkdir -p $O
+SUPERLU_MI355X_TIMING=1 SLU_PROFILE_PLAN=1 timeout -k 10 600 python -u tools/d2h_variants.py 100 > $O/var.txt 2> $O/var.err || { tail -20 $O/var.err; exit 1; }
+cat $O/var.txt; grep -E "^rep|PDGSTRF|slu d2h" $O/var.err
