@@ -121,7 +121,7 @@ __device__ __forceinline__ void ds_publish(unsigned *f, unsigned epoch) {
 __host__ __device__ inline int ds_grid(int nitems) { return 64 * ((nitems + 7) / 8); }
 
 template <typename T>
-__global__ void __launch_bounds__(DS_THREADS, 1)
+__global__ void __launch_bounds__(DS_THREADS, 1) __attribute__((amdgpu_waves_per_eu(1, 1)))
 k_diag_strips(const DiagItemF<T> *items, int nitems, unsigned *flags, unsigned epoch, int *err,
               double thresh, int replace_tiny, int *tiny_count, int *zpiv) {
     static_assert(std::is_same<T, double>::value || std::is_same<T, float>::value, "real types");
@@ -143,8 +143,8 @@ k_diag_strips(const DiagItemF<T> *items, int nitems, unsigned *flags, unsigned e
     __shared__ T sS[MW][LD];  // my strip, all w rows
     __shared__ T sP[MW][LD];  // a received panel's L part (rows 32p..)
     __shared__ T sLi[PW][LD]; // L_pp^{-1}; later my L_qq^{-1}
+    __shared__ T sTmp[2][16][17]; // the inverses' 16 x 16 products
     __shared__ T sUi[PW][LD]; // my U_qq^{-1}
-    __shared__ T sT[2][4][64]; // 8 x 8 block products of the inverse (L, U)
     __shared__ int s_zp[PW];
     __shared__ T s_rp[PW];
     __shared__ int s_ok;
@@ -158,20 +158,59 @@ k_diag_strips(const DiagItemF<T> *items, int nitems, unsigned *flags, unsigned e
             return keep_if(ok & (e / w < pw), gld(A + min(r, w - 1) + (int64_t)(c0 + c) * ld));
         },
         [&](int e, T v) { sS[e % w][e / w] = v; });
+    // rows w .. c0 + 32 (the last strip's diagonal block past pw) read as
+    // zeros by the inverses below
+    for (int e = tid; e < (c0 + PW - w) * PW; e += DS_THREADS) sS[w + e / PW][e % PW] = Sx::zero();
     __syncthreads();
 
+    // A(r0 + 32 + [lo, hi), strip) -= L21 U_pq (sP rows 32 + .., U_pq in sS
+    // rows r0..): 16 x 16 fragments (lo a multiple of 16), two chains per
+    // wave, on waves w0, w0 + 1, .. (wn of them)
+    auto trail = [&](int r0, int lo, int hi, int w0, int wn) {
+        const int nfr = hi > lo ? (hi - lo + 15) / 16 : 0, nf = 2 * nfr;
+        for (int f0 = 2 * (wv - w0); f0 < nf; f0 += 2 * wn) {
+            typename M::acc_t acc[2] = {M::zero(), M::zero()};
+#pragma unroll
+            for (int ks = 0; ks < PW; ks += M::KSTEP) {
+                const int k = ks + (lane >> 4);
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    const int f = min(f0 + u, nf - 1), fr = f >> 1, fc = f & 1;
+                    const int r = lo + fr * 16 + (lane & 15);
+                    M::step(acc[u], keep_if(r < hi, sP[PW + min(r, hi - 1)][k]),
+                            sS[r0 + k][fc * 16 + (lane & 15)]);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int f = f0 + u, fr = f >> 1, fc = f & 1;
+                if (f < nf)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int r = lo + fr * 16 + M::row(lane, i);
+                        if (r < hi) {
+                            T &d = sS[r0 + PW + r][fc * 16 + (lane & 15)];
+                            d = Sx::sub(d, M::get(acc[u], i));
+                        }
+                    }
+            }
+        }
+    };
     // ---- apply the panels of the strips to my left, in order
     for (int p = 0; p < q; ++p) {
         if (!ds_wait(fl + p, epoch, err, &s_ok)) return;
         const int r0 = p * PW, nr = w - r0;
         DS_PROBE(0);
-        stage_loop<DS_THREADS, 8, T>(
-            tid, nr * PW,
-            [&](int e, bool ok) {
-                const int ee = min(e, nr * PW - 1);
-                return keep_if(ok, ld_sc1(A + r0 + ee % nr + (int64_t)(r0 + ee / nr) * ld));
-            },
-            [&](int e, T v) { sP[e % nr][e / nr] = v; });
+        // only L21_p (rows r0 + 32 ..): L_pp enters through its inverse
+        const int nb21 = nr - PW, rb = r0 + PW;
+        if (nb21 > 0)
+            stage_loop<DS_THREADS, 16, T>(
+                tid, nb21 * PW,
+                [&](int e, bool ok) {
+                    const int ee = min(e, nb21 * PW - 1);
+                    return keep_if(ok, ld_sc1(A + rb + ee % nb21 + (int64_t)(r0 + ee / nb21) * ld));
+                },
+                [&](int e, T v) { sP[PW + e % nb21][e / nb21] = v; });
         stage_loop<DS_THREADS, 4, T>( // dinvLT: [b][a] = Linv[a][b]
             tid, PW * PW, [&](int e, bool ok) { return keep_if(ok, ld_sc1(dinvLT + (int64_t)p * PW * PW + min(e, PW * PW - 1))); },
             [&](int e, T v) { sLi[e % PW][e / PW] = v; });
@@ -192,36 +231,10 @@ k_diag_strips(const DiagItemF<T> *items, int nitems, unsigned *flags, unsigned e
                 sS[r0 + fr * 16 + M::row(lane, i)][fc * 16 + (lane & 15)] = M::get(acc, i);
         }
         __syncthreads();
-        // A(r0+32.., strip) -= L21_p U_pq: fragments (16 rows x 16 columns),
-        // two chains interleaved per wave
-        const int nt = nr - PW, nfr = (nt + 15) / 16, nf = 2 * nfr;
-        for (int f0 = 2 * wv; f0 < nf; f0 += 8) {
-            typename M::acc_t acc[2] = {M::zero(), M::zero()};
-#pragma unroll
-            for (int ks = 0; ks < PW; ks += M::KSTEP) {
-                const int k = ks + (lane >> 4);
-#pragma unroll
-                for (int u = 0; u < 2; ++u) {
-                    const int f = min(f0 + u, nf - 1), fr = f >> 1, fc = f & 1;
-                    const int r = fr * 16 + (lane & 15);
-                    M::step(acc[u], keep_if(r < nt, sP[PW + min(r, nt - 1)][k]),
-                            sS[r0 + k][fc * 16 + (lane & 15)]);
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                const int f = f0 + u, fr = f >> 1, fc = f & 1;
-                if (f < nf)
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const int r = fr * 16 + M::row(lane, i);
-                        if (r < nt) {
-                            T &d = sS[r0 + PW + r][fc * 16 + (lane & 15)];
-                            d = Sx::sub(d, M::get(acc[u], i));
-                        }
-                    }
-            }
-        }
+        // A(r0+32.., strip) -= L21_p U_pq.  The last panel before my own LU
+        // updates only the 64 rows the LU reads now; the rest is updated by
+        // waves 1-3 beside the LU (below)
+        trail(r0, 0, p + 1 == q ? min(64, nr - PW) : nr - PW, 0, 4);
         __syncthreads();
         DS_PROBE(2);
     }
@@ -267,10 +280,121 @@ k_diag_strips(const DiagItemF<T> *items, int nitems, unsigned *flags, unsigned e
             s_rp[lane] = Sx::zero();
             s_zp[lane] = 0;
         }
+    } else if (q > 0) {
+        trail(c0 - PW, 64, nrow, 1, 3); // the last panel's update of rows c0 + 64 ..
     }
     __syncthreads();
     DS_PROBE(3);
-    if (wv > 0) { // rows 64.. of the panel, thread per row
+    // ---- the inverses, then the rows below the top 64.
+    // (I) wave 0: the four 16 x 16 diagonal blocks of L_qq^{-1} (unit lower,
+    // blocks A, C) and U_qq^{-1} (upper, blocks D, F), a quarter-wave each,
+    // lane = column: w = e_j; for k: w[k] *= scale_k, w[t] -= M(t, k) w[k] for
+    // t > k, with M = L and scale 1, or M(t, k) = U(15 - t, 15 - k) (the block
+    // walked from its last row) and scale rp.  Columns >= pw of the strip are
+    // zeros (loaded so, kept so by the LU), as are its rows past the block
+    // (above); rows / columns >= pw of the inverses are set to zero.
+    // (II) the off-diagonal blocks on MFMA: L21^{-1} = -C^{-1} (B A^{-1})
+    // (wave 0), U12^{-1} = -D^{-1} (E F^{-1}) (wave 1).
+    // (III) rows 64..: X = A U_qq^{-1} on MFMA (all waves).  A zero pivot
+    // leaves its column unscaled (SRC/pdgstrf2.c:246-252), which no inverse
+    // expresses: such a strip eliminates those rows one per thread instead.
+    bool anyz = false;
+#pragma unroll
+    for (int c = 0; c < PW; ++c) anyz |= s_zp[c] != 0; // (uniform)
+    const T *sflat = &sS[0][0];
+    if (wv == 0) {
+        const int qd = lane >> 4, jj = lane & 15, o = 16 * (qd & 1);
+        const bool up = qd >= 2;
+        // (an index into the __shared__ array, not a pointer: keeps ds_read)
+        const int mb = up ? (c0 + o + 15) * LD + o + 15 : (c0 + o) * LD + o, sg = up ? -1 : 1;
+        T v[16];
+#pragma unroll
+        for (int t = 0; t < 16; ++t) v[t] = (up ? 15 - t : t) == jj ? one_of(Sx::zero()) : Sx::zero();
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            if (up) v[k] = Sx::mul(v[k], s_rp[o + 15 - k]);
+#pragma unroll
+            for (int t = k + 1; t < 16; ++t) v[t] = Sx::fms(v[t], sflat[mb + sg * (t * LD + k)], v[k]);
+        }
+        const bool cok = o + jj < pw;
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+            const int r = o + (up ? 15 - t : t);
+            const T val = (cok & (r < pw)) ? v[t] : Sx::zero();
+            if (up) sUi[r][o + jj] = val;
+            else sLi[r][o + jj] = val;
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t) { // the structural zero blocks
+            const int e = lane + 64 * t, r = e >> 4, c = e & 15;
+            sLi[r][16 + c] = Sx::zero();
+            sUi[16 + r][c] = Sx::zero();
+        }
+    }
+    __syncthreads();
+    if (wv < 2) {
+        // wave 0: T = B A^{-1}, L21^{-1} = -C^{-1} T; wave 1: T = E F^{-1},
+        // U12^{-1} = -D^{-1} T (one 16 x 16 x 16 product each, through sTmp)
+        const bool ul = wv == 0;
+        typename M::acc_t acc = M::zero();
+#pragma unroll
+        for (int ks = 0; ks < 16; ks += M::KSTEP) {
+            const int k = ks + (lane >> 4), r = lane & 15;
+            const T a = ul ? sS[c0 + 16 + r][k] : sS[c0 + r][16 + k];
+            const T b = ul ? sLi[k][r] : sUi[16 + k][16 + r];
+            M::step(acc, a, b);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) sTmp[wv][M::row(lane, i)][lane & 15] = M::get(acc, i);
+        asm volatile("" ::: "memory"); // (one wave: its LDS accesses complete in order)
+        acc = M::zero();
+#pragma unroll
+        for (int ks = 0; ks < 16; ks += M::KSTEP) {
+            const int k = ks + (lane >> 4), r = lane & 15;
+            const T a = ul ? sLi[16 + r][16 + k] : sUi[r][k];
+            M::step(acc, a, sTmp[wv][k][r]);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int r = M::row(lane, i), c = lane & 15;
+            if (ul) sLi[16 + r][c] = Sx::neg(M::get(acc, i));
+            else sUi[r][16 + c] = Sx::neg(M::get(acc, i));
+        }
+    }
+    __syncthreads();
+    if (!anyz) {
+        // (III) rows 64 .. nrow - 1: 16 x 16 fragments, all reads before the
+        // barrier, the writes after it
+        const int nb = nrow - 64, nfr = nb > 0 ? (nb + 15) / 16 : 0, nf = 2 * nfr;
+        constexpr int FMAX = (MW - 64) / 16 * 2 / 4; // fragments per wave
+        typename M::acc_t acc[FMAX];
+#pragma unroll
+        for (int u = 0; u < FMAX; ++u) {
+            acc[u] = M::zero();
+            const int f = wv + 4 * u;
+            if (f < nf) {
+                const int fr = f >> 1, fc = f & 1, r = fr * 16 + (lane & 15);
+#pragma unroll
+                for (int ks = 0; ks < PW; ks += M::KSTEP) {
+                    const int k = ks + (lane >> 4);
+                    M::step(acc[u], keep_if(r < nb, sS[c0 + 64 + min(r, nb - 1)][k]), sUi[k][fc * 16 + (lane & 15)]);
+                }
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < FMAX; ++u) {
+            const int f = wv + 4 * u;
+            if (f < nf) {
+                const int fr = f >> 1, fc = f & 1;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int r = fr * 16 + M::row(lane, i);
+                    if (r < nb) sS[c0 + 64 + r][fc * 16 + (lane & 15)] = M::get(acc[u], i);
+                }
+            }
+        }
+    } else if (wv > 0) { // rows 64.., thread per row
         const int i = tid;
         if (i < nrow) {
             T x[PW];
@@ -288,102 +412,33 @@ k_diag_strips(const DiagItemF<T> *items, int nitems, unsigned *flags, unsigned e
 #pragma unroll
             for (int c = 0; c < PW; ++c) sS[c0 + i][c] = x[c];
         }
-    } else {
-        // ---- meanwhile wave 0: L_qq^{-1} (unit lower) and U_qq^{-1} (upper)
-        // by 8 x 8 blocks.  Lq(i,k) = sS[c0+i][k] (i > k: L, i <= k: U);
-        // indices >= pw count as zero (the inverses' rows / columns there
-        // are zero).  One wave: its LDS accesses complete in order, so no
-        // barrier separates the stages.
-        auto Lq = [&](int i, int k) { return keep_if((i < pw) & (k < pw), sS[c0 + min(i, pw - 1)][min(k, pw - 1)]); };
-        for (int e = lane; e < PW * PW; e += 64) {
-            sLi[e / PW][e % PW] = Sx::zero();
-            sUi[e / PW][e % PW] = Sx::zero();
-        }
-        __builtin_amdgcn_wave_barrier();
-        { // diagonal 8 x 8 blocks: lanes 0..31 columns of L's, 32..63 of U's
-            const int bb = (lane & 31) >> 3, jj = lane & 7, o = bb * 8;
-            T v[8];
-            if (lane < 32) { // L_bb x = e_jj, unit lower
-#pragma unroll
-                for (int i = 0; i < 8; ++i) {
-                    T sacc = i == jj ? one_of(Sx::zero()) : Sx::zero();
-#pragma unroll
-                    for (int k = 0; k < i; ++k) sacc = Sx::fms(sacc, Lq(o + i, o + k), v[k]);
-                    v[i] = i < jj ? Sx::zero() : sacc;
-                }
-#pragma unroll
-                for (int i = 0; i < 8; ++i)
-                    if (o + i < pw && o + jj < pw) sLi[o + i][o + jj] = v[i];
-            } else { // U_bb y = e_jj, y(i) = rp(i) (e(i) - sum_{k>i} U(i,k) y(k))
-#pragma unroll
-                for (int i = 7; i >= 0; --i) {
-                    T sacc = i == jj ? one_of(Sx::zero()) : Sx::zero();
-#pragma unroll
-                    for (int k = i + 1; k < 8; ++k) sacc = Sx::fms(sacc, Lq(o + i, o + k), v[k]);
-                    v[i] = i > jj ? Sx::zero() : Sx::mul(sacc, s_rp[o + i]);
-                }
-#pragma unroll
-                for (int i = 0; i < 8; ++i)
-                    if (o + i < pw && o + jj < pw) sUi[o + i][o + jj] = v[i];
-            }
-        }
-        __builtin_amdgcn_wave_barrier();
-        // off-diagonal blocks by distance d: L: X(a,b) = -X(a,a) sum_{c=b}^{a-1} L(a,c) X(c,b);
-        // U: Y(a,b) = -Y(a,a) sum_{c=a+1}^{b} U(a,c) Y(c,b)
-        for (int d = 1; d < 4; ++d) {
-            const int nblk = 4 - d; // block pairs per factor
-            for (int e = lane; e < 2 * nblk * 64; e += 64) {
-                const int u = e / (nblk * 64), pi = (e / 64) % nblk, i = (e & 63) >> 3, j = e & 7;
-                T sacc = Sx::zero();
-                if (u == 0) { // L block (a, b) = (pi + d, pi): T = sum_c L(a,c) X(c,b)
-                    const int a = pi + d, bq = pi;
-                    for (int c = bq; c < a; ++c)
-#pragma unroll
-                        for (int k = 0; k < 8; ++k)
-                            sacc = Sx::fms(sacc, Lq(a * 8 + i, c * 8 + k), sLi[c * 8 + k][bq * 8 + j]);
-                } else { // U block (a, b) = (pi, pi + d): T = sum_c U(a,c) Y(c,b)
-                    const int a = pi, bq = pi + d;
-                    for (int c = a + 1; c <= bq; ++c)
-#pragma unroll
-                        for (int k = 0; k < 8; ++k)
-                            sacc = Sx::fms(sacc, Lq(a * 8 + i, c * 8 + k), sUi[c * 8 + k][bq * 8 + j]);
-                }
-                sT[u][pi][e & 63] = sacc; // = -T
-            }
-            __builtin_amdgcn_wave_barrier();
-            for (int e = lane; e < 2 * nblk * 64; e += 64) {
-                const int u = e / (nblk * 64), pi = (e / 64) % nblk, i = (e & 63) >> 3, j = e & 7;
-                T sacc = Sx::zero();
-                if (u == 0) {
-                    const int a = pi + d, bq = pi;
-#pragma unroll
-                    for (int k = 0; k < 8; ++k) sacc = Sx::fms(sacc, sLi[a * 8 + i][a * 8 + k], sT[0][pi][k * 8 + j]);
-                    if (a * 8 + i < pw && bq * 8 + j < pw) sLi[a * 8 + i][bq * 8 + j] = Sx::neg(sacc);
-                } else {
-                    const int a = pi, bq = pi + d;
-#pragma unroll
-                    for (int k = 0; k < 8; ++k) sacc = Sx::fms(sacc, sUi[a * 8 + i][a * 8 + k], sT[1][pi][k * 8 + j]);
-                    if (a * 8 + i < pw && bq * 8 + j < pw) sUi[a * 8 + i][bq * 8 + j] = Sx::neg(sacc);
-                }
-            }
-            __builtin_amdgcn_wave_barrier();
-        }
     }
     __syncthreads();
 
     DS_PROBE(4);
-    // ---- publish: the strip, U_qq^{-1} (row-major), (L_qq^{-1})^T (row-major)
-    for (int e = tid; e < w * pw; e += DS_THREADS) {
-        const int r = e % w, c = e / w;
-        st_sc1(A + r + (int64_t)(c0 + c) * ld, sS[r][c]);
+    // ---- publish what the strips to the right read: L21_q (rows c0 + 32 ..)
+    // and (L_qq^{-1})^T (row-major), then the flag; then the rest of the
+    // strip (rows < c0 + 32) and U_qq^{-1} (row-major), which only the
+    // TRSMs after this kernel read
+    {
+        const int r1 = c0 + PW, n21 = w - r1;
+        for (int e = tid; e < n21 * pw; e += DS_THREADS) {
+            const int r = r1 + e % n21, c = e / n21;
+            st_sc1(A + r + (int64_t)(c0 + c) * ld, sS[r][c]);
+        }
+        for (int e = tid; e < PW * PW; e += DS_THREADS) {
+            const int i = e / PW, jj = e % PW;
+            st_sc1(dinvLT + (int64_t)q * PW * PW + e, sLi[jj][i]);
+        }
+        ds_publish(fl + q, epoch);
+        DS_PROBE(5);
+        const int r1c = min(r1, w);
+        for (int e = tid; e < r1c * pw; e += DS_THREADS) {
+            const int r = e % r1c, c = e / r1c;
+            A[r + (int64_t)(c0 + c) * ld] = sS[r][c];
+        }
+        for (int e = tid; e < PW * PW; e += DS_THREADS) dinvU[(int64_t)q * PW * PW + e] = sUi[e / PW][e % PW];
     }
-    for (int e = tid; e < PW * PW; e += DS_THREADS) {
-        const int i = e / PW, jj = e % PW;
-        st_sc1(dinvU + (int64_t)q * PW * PW + e, sUi[i][jj]);
-        st_sc1(dinvLT + (int64_t)q * PW * PW + e, sLi[jj][i]);
-    }
-    ds_publish(fl + q, epoch);
-    DS_PROBE(5);
 }
 
 } // namespace slu
