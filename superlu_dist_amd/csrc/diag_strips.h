@@ -87,6 +87,14 @@ template <typename T> __device__ __forceinline__ T ld_sc1(const T *p) {
     return v;
 }
 
+// f(integral_constant<int, i>) for i = 0 .. N - 1, unrolled at compile time
+template <int N, int I = 0, typename F> __device__ __forceinline__ void ds_unroll(F &&f) {
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        ds_unroll<N, I + 1>(f);
+    }
+}
+
 // lane 0 of wave 0 waits for *f >= epoch; false (and *err set) on timeout
 __device__ __forceinline__ bool ds_wait(const unsigned *f, unsigned epoch, int *err, int *s_ok) {
     if (threadIdx.x == 0) {
@@ -251,28 +259,51 @@ k_diag_strips(const DiagItemF<T> *items, int nitems, unsigned *flags, unsigned e
         const bool mine = lane < nrow;
 #pragma unroll
         for (int c = 0; c < PW; ++c) x[c] = mine ? sS[c0 + lane][c] : Sx::zero();
+        // (tiny-pivot count and the last zero pivot in registers, one atomic
+        // each after the loop: no control flow between the columns' steps)
+        int ntiny = 0, zlast = 0;
+        T rps[PW];
+        int zps[PW];
 #pragma unroll
         for (int j = 0; j < PW; ++j) {
-            if (j < pw) { // uniform
-                T piv = rlane(x[j], j);
-                if (replace_tiny && Sx::abs1(piv) < thresh) {
-                    piv = Sx::thresh(piv, thresh);
-                    if (lane == 0) atomicAdd(tiny_count, 1);
-                }
-                const int z = Sx::iszero(piv);
-                if (z && lane == 0) atomicMax(&zpiv[it.k], it.fcol + c0 + j + 1);
-                const T rp = z ? Sx::zero() : Sx::recip(piv);
-                // a zero pivot leaves the column unscaled (SRC/pdgstrf2.c:246-252)
-                const T l = lane > j ? (z ? x[j] : Sx::mul(x[j], rp)) : Sx::zero();
-                x[j] = lane > j ? l : (lane == j ? piv : x[j]);
+            rps[j] = Sx::zero();
+            zps[j] = 0;
+        }
+        // one column step (the same per-column semantics for every strip)
+        auto lu_step = [&](auto jc) {
+            constexpr int j = decltype(jc)::value;
+            T piv = rlane(x[j], j);
+            const bool tiny = replace_tiny && Sx::abs1(piv) < thresh;
+            piv = tiny ? Sx::thresh(piv, thresh) : piv;
+            ntiny += tiny;
+            const int z = Sx::iszero(piv);
+            zlast = z ? it.fcol + c0 + j + 1 : zlast;
+            const T rp = z ? Sx::zero() : Sx::recip(piv);
+            // a zero pivot leaves the column unscaled (SRC/pdgstrf2.c:246-252)
+            const T l = lane > j ? (z ? x[j] : Sx::mul(x[j], rp)) : Sx::zero();
+            x[j] = lane > j ? l : (lane == j ? piv : x[j]);
 #pragma unroll
-                for (int c = j + 1; c < PW; ++c) x[c] = Sx::fms(x[c], l, rlane(x[c], j));
-                if (lane == 0) {
-                    s_rp[j] = rp;
-                    s_zp[j] = z;
-                }
+            for (int c = j + 1; c < PW; ++c) x[c] = Sx::fms(x[c], l, rlane(x[c], j));
+            rps[j] = rp;
+            zps[j] = z;
+        };
+        // full strips (pw = 32): the steps with no branch between them, so the
+        // next column's pivot and reciprocal overlap this column's updates
+        if (pw == PW)
+            ds_unroll<PW>([&](auto jc) { lu_step(jc); });
+        else
+            ds_unroll<PW>([&](auto jc) {
+                if (decltype(jc)::value < pw) lu_step(jc);
+            });
+        if (lane == 0) {
+#pragma unroll
+            for (int j = 0; j < PW; ++j) {
+                s_rp[j] = rps[j];
+                s_zp[j] = zps[j];
             }
         }
+        if (lane == 0 && ntiny) atomicAdd(tiny_count, ntiny);
+        if (lane == 0 && zlast) atomicMax(&zpiv[it.k], zlast);
         if (mine)
 #pragma unroll
             for (int c = 0; c < PW; ++c) sS[c0 + lane][c] = x[c];
