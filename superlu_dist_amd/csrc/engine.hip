@@ -3638,6 +3638,16 @@ struct AmalgPlan : PlanBase {
     std::thread alloc_thread;
     std::string alloc_err;
     std::mutex o_mu; // ensure_o: the upload thread or the D2H program build
+    // the D2H's pinned slots and HBM staging slots, allocated and touched
+    // (one DMA through each) beside the plan build: lazily, the first
+    // factorization paid ~70 ms more D2H tail for them
+    std::thread warm_thread;
+    std::string warm_err;
+    DevBuf<char> warm_stage;
+    void warm_join() {
+        if (warm_thread.joinable()) warm_thread.join();
+        SLU_REQUIRE(warm_err.empty(), "%s", warm_err.c_str());
+    }
     double up_ms = 0, h2d_bytes = 0;
     double t_amalg = 0, t_plan = 0, t_expand = 0, t_compress = 0, t_d2h = 0;
     bool coarse_current = false; // d_oL / d_oU stale: the coarse storage holds newer values
@@ -3704,6 +3714,30 @@ struct AmalgPlan : PlanBase {
                 }
             });
         }
+        if (P->opts.overlap_download) {
+            AmalgPlan *raw = P.get();
+            raw->warm_thread = std::thread([raw] {
+                try {
+                    HIPCHK(hipSetDevice(0));
+                    i64 slot = 128ll << 20; // (Plan::D2H_SLOT, and its override as in build_d2h)
+                    if (const char *e = getenv("SLU_D2H_SLOT_KB")) slot = std::max<i64>(16, atoll(e)) << 10;
+                    constexpr int NS = Inner::D2H_NS;
+                    std::lock_guard<std::mutex> in_use(pinned_pool(1).use);
+                    std::vector<char *> slots = pinned_pool(1).get(NS, slot);
+                    raw->warm_stage.alloc((size_t)NS * slot);
+                    hipStream_t st = nullptr;
+                    HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+                    HIPCHK(hipMemsetAsync(raw->warm_stage.p, 0, raw->warm_stage.bytes(), st));
+                    for (int i = 0; i < NS; ++i)
+                        HIPCHK(hipMemcpyAsync(slots[i], raw->warm_stage.p + (i64)i * slot, (size_t)slot,
+                                              hipMemcpyDeviceToHost, st));
+                    HIPCHK(hipStreamSynchronize(st));
+                    HIPCHK(hipStreamDestroy(st));
+                } catch (const std::exception &e) {
+                    raw->warm_err = e.what();
+                }
+            });
+        }
         try {
             vector<const int_t *> li(L->Lrowind_bc_ptr, L->Lrowind_bc_ptr + ns),
                 ui(L->Ufstnz_br_ptr, L->Ufstnz_br_ptr + ns);
@@ -3712,6 +3746,7 @@ struct AmalgPlan : PlanBase {
             if (!P->A.build(n_, ns, xsup, li.data(), ui.data(), zero_frac, maxw)) {
                 if (P->up_thread.joinable()) P->up_thread.join();
                 if (P->alloc_thread.joinable()) P->alloc_thread.join();
+                if (P->warm_thread.joinable()) P->warm_thread.join();
                 return nullptr;
             }
             SLU_REQUIRE(P->A.lval1 == lv && P->A.uval1 == uv, "amalgamation: value counts");
@@ -3731,6 +3766,7 @@ struct AmalgPlan : PlanBase {
             if (P->up_thread.joinable()) P->up_thread.join();
             if (P->alloc_thread.joinable()) P->alloc_thread.join();
             if (P->prog_thread.joinable()) P->prog_thread.join();
+            if (P->warm_thread.joinable()) P->warm_thread.join();
             throw;
         }
         P->t_plan = ms_since(t0);
@@ -3873,6 +3909,8 @@ struct AmalgPlan : PlanBase {
     void build_d2h() {
         ensure_o(); // (the push programs address d_oL / d_oU)
         Inner &P = *in;
+        warm_join();
+        if (warm_stage.p) P.d_stage.swap(warm_stage);
         LocalLU *Llu = LU->Llu;
         const int_t *xsup = LU->Glu_persist->xsup;
         const int nl = (int)P.levels.size();
@@ -4106,6 +4144,7 @@ struct AmalgPlan : PlanBase {
         if (up_thread.joinable()) up_thread.join();
         if (alloc_thread.joinable()) alloc_thread.join();
         if (prog_thread.joinable()) prog_thread.join();
+        if (warm_thread.joinable()) warm_thread.join();
     }
 };
 
