@@ -829,6 +829,7 @@ void pxgstrs(int dtype, const char *name, int_t n, LUS *LU, xScalePermstruct_t *
             }
         }
         if (!plan) {
+            reap_join(); // (nothing of an evicted plan still in flight if this aborts)
             {
                 std::lock_guard<std::mutex> lk(g_cache_mu);
                 const LuKey k = lu_key(LU);
@@ -838,7 +839,6 @@ void pxgstrs(int dtype, const char *name, int_t n, LUS *LU, xScalePermstruct_t *
                             "hold A); factor it again, or set SUPERLU_MI355X_HOST_FACTORS=1 so that "
                             "pdgstrf writes the factors back");
             }
-            reap_join();
             slu_comm *c = comm_for_grid(grid);
             slu_engine_opts eo{};
             char err[512] = {0};

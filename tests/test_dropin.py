@@ -245,3 +245,44 @@ def test_reference_3d_driver_with_our_pdgstrf3d(drv, matrix, order, grid):
     print(f"{drv} {matrix} {r}x{c}x{d}: ||x-xtrue||/||x|| ref {ref_err:.3e} mi355x {my_err:.3e}; "
           f"FACTOR time ref {ref_t} s, mi355x {my_t} s")
     assert my_err <= max(10 * ref_err, 1e-12), (my_err, ref_err)
+
+
+# ---- two LUstructs in one process: on a 1x1 grid the
+# factors of the last pdgstrf live only in HBM, in the cached plan.  Factoring
+# a second LUstruct evicts that plan; a FACTORED solve of the first must then
+# fail loudly instead of solving with A's values (oracle/gen/evict_solve_main.c).
+def _evict(env_extra):
+    env = dict(os.environ)
+    env.update({"OMP_NUM_THREADS": "1", "MKL_NUM_THREADS": "1", "MKL_THREADING_LAYER": "SEQUENTIAL",
+                "HSA_ENABLE_IPC_MODE_LEGACY": "0"}, **env_extra)
+    cmd = [MPIEXEC, "-n", "1", os.path.join(REF, "evict_solve"),
+           os.path.join(MAT, "g20.rua"), os.path.join(MAT, "big.rua")]
+    r = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=240)
+    out = r.stdout + r.stderr
+    errs = {int(k): float(v) for k, v in re.findall(r"system (\d): err ([0-9.eE+-]+)", out)}
+    return r.returncode, errs, out
+
+
+@pytest.mark.skipif(not _have("evict_solve"), reason="eviction driver not built")
+def test_evict_driver_binds_our_solve():
+    dyn, und, _ = _binding("evict_solve")
+    assert "libslu_mi355x_solve.so" in dyn
+    for sym in ("pdgstrf", "pdgstrs", "pddistribute"):
+        assert sym in und, sym
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not _have("evict_solve"), reason="eviction driver not built")
+def test_factored_solve_after_eviction_fails_loudly():
+    rc, errs, out = _evict({})
+    assert errs.get(1, 1) < 1e-10 and errs.get(2, 1) < 1e-10, out[-3000:]
+    assert rc != 0 and 3 not in errs, out[-3000:]
+    assert "kept only in GPU memory" in out, out[-3000:]
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not _have("evict_solve"), reason="eviction driver not built")
+def test_factored_solve_after_eviction_with_host_factors():
+    rc, errs, out = _evict({"SUPERLU_MI355X_HOST_FACTORS": "1"})
+    assert rc == 0, out[-3000:]
+    assert sorted(errs) == [1, 2, 3] and max(errs.values()) < 1e-10, out[-3000:]
