@@ -4,16 +4,22 @@
 #pragma once
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <exception>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <stdexcept>
 #include <string>
 #include <thread>
 #include <vector>
+
+#include <sys/mman.h>
+#include <unistd.h>
+#include <type_traits>
 
 namespace slu {
 
@@ -32,13 +38,34 @@ inline std::string fmt(const char *f, ...) {
 
 void set_last_error(const std::string &s);
 
+// Host memory for large plan tables: 2 MB aligned and advised as
+// transparent huge pages, so the first touch costs one fault per 2 MB
+// instead of one per 4 KB (the faults were most of the plan build's
+// system time); small ones from malloc.
+inline void *big_alloc(size_t bytes) {
+    constexpr size_t HP = size_t(2) << 20;
+    if (bytes < 2 * HP) return malloc(bytes ? bytes : 1);
+    const size_t r = (bytes + HP - 1) / HP * HP;
+    void *p = aligned_alloc(HP, r);
+    if (p) madvise(p, r, MADV_HUGEPAGE);
+    return p;
+}
+struct BigFree {
+    void operator()(void *p) const { free(p); }
+};
+
 // Host array without value-initialisation: large plan tables are filled by
 // parallel passes, so the first touch (page faults) is spread over threads.
 template <typename T> struct RawVec {
-    std::unique_ptr<T[]> a;
+    static_assert(std::is_trivially_destructible<T>::value, "RawVec holds plain data");
+    std::unique_ptr<T[], BigFree> a;
     size_t n = 0;
     void resize_uninit(size_t cnt) {
-        a.reset(cnt ? new T[cnt] : nullptr);
+        a.reset(nullptr);
+        if (cnt) {
+            a.reset((T *)big_alloc(cnt * sizeof(T)));
+            if (!a) throw std::bad_alloc();
+        }
         n = cnt;
     }
     T &operator[](size_t i) { return a[i]; }
@@ -62,6 +89,62 @@ inline int plan_threads() {
     }();
     return t;
 }
+
+namespace detail {
+// Persistent workers for parallel_for: the plan build calls it a few hundred
+// times (twice per elimination level in build_schedule), and fresh threads
+// per call cost their creation plus a fresh first touch of every
+// thread_local scratch array (n-sized, 4 KB page faults that serialise in
+// the kernel).  One job at a time; a second submitter (another host thread,
+// or a parallel_for nested in a job) spawns its own threads as before.
+inline thread_local bool t_in_pool = false;
+struct Pool {
+    std::mutex m;
+    std::condition_variable cv, dcv;
+    int nthreads = 0, want = 0, left = 0;
+    uint64_t gen = 0;
+    const std::function<void()> *job = nullptr;
+    std::atomic<bool> busy{false};
+    void ensure(int nw) { // (called by the submitter holding busy)
+        for (; nthreads < nw; ++nthreads) {
+            const int id = nthreads;
+            std::thread([this, id] { run(id); }).detach();
+        }
+    }
+    void run(int id) {
+        t_in_pool = true;
+        uint64_t seen = 0;
+        for (;;) {
+            const std::function<void()> *j;
+            {
+                std::unique_lock<std::mutex> lk(m);
+                cv.wait(lk, [&] { return gen != seen; });
+                seen = gen;
+                if (id >= want) continue;
+                j = job;
+            }
+            (*j)();
+            std::lock_guard<std::mutex> lk(m);
+            if (--left == 0) dcv.notify_all();
+        }
+    }
+};
+inline Pool &pool() {
+    // never destroyed: its threads wait until exit.  A forked child has none
+    // of its parent's workers: it starts a pool of its own.
+    static std::atomic<Pool *> p{nullptr};
+    static std::atomic<pid_t> owner{0};
+    static std::mutex mk;
+    if (owner.load() != getpid()) {
+        std::lock_guard<std::mutex> lk(mk);
+        if (owner.load() != getpid()) {
+            p = new Pool;
+            owner = getpid();
+        }
+    }
+    return *p.load();
+}
+} // namespace detail
 
 // f(i) for i in [0, n): dynamic chunks over plan_threads() threads; the
 // first exception is rethrown after every thread has stopped.
@@ -88,10 +171,32 @@ template <typename F> void parallel_for(int n, F &&f, int chunk = 64) {
             next = n;
         }
     };
-    std::vector<std::thread> th;
-    for (int t = 1; t < std::min(T, (n + chunk - 1) / chunk); ++t) th.emplace_back(work);
-    work();
-    for (auto &x : th) x.join();
+    const int nw = std::min(T, (n + chunk - 1) / chunk) - 1;
+    detail::Pool &P = detail::pool();
+    bool idle = false;
+    if (!detail::t_in_pool && P.busy.compare_exchange_strong(idle, true)) {
+        const std::function<void()> fn = work;
+        {
+            std::lock_guard<std::mutex> lk(P.m);
+            P.ensure(T - 1);
+            P.job = &fn;
+            P.want = P.left = nw;
+            ++P.gen;
+        }
+        P.cv.notify_all();
+        work();
+        {
+            std::unique_lock<std::mutex> lk(P.m);
+            P.dcv.wait(lk, [&] { return P.left == 0; });
+            P.job = nullptr;
+        }
+        P.busy = false;
+    } else {
+        std::vector<std::thread> th;
+        for (int t = 0; t < nw; ++t) th.emplace_back(work);
+        work();
+        for (auto &x : th) x.join();
+    }
     if (err) std::rethrow_exception(err);
 }
 
