@@ -548,8 +548,8 @@ struct Plan : PlanBase {
     vector<CopyItem<T>> dcopy, pcopy;
     vector<Sec> dsecs, psecs;
     // per-k panel arrays (device copies referenced by KInfo / TrsmUItem)
-    vector<int> h_rg, h_ra, h_cg, h_cb, h_pair, h_ct0;
-    vector<i64> h_cvoff;
+    RawVec<int> h_rg, h_ra, h_cg, h_cb, h_pair, h_ct0;
+    RawVec<i64> h_cvoff;
 
     // ---- device
     DevBuf<T> d_L, d_U, d_dpk, d_pan, d_dinv;
@@ -712,8 +712,9 @@ struct Plan : PlanBase {
             if (zmode) build_zranges(true);
             build_schedule();
             if (prof)
-                fprintf(stderr, "[slu plan %d]   (add_supernode %.1f ms, merge + atomics %.1f ms)\n",
-                        iam, t_addsn, t_merge);
+                fprintf(stderr, "[slu plan %d]   (add_supernode %.1f ms, merge + atomics %.1f ms: "
+                                "resize %.1f, copy %.1f, tiles %.1f)\n",
+                        iam, t_addsn, t_merge, t_resize, t_put, t_tiles);
             tick("build_schedule");
             build_device();
             tick("build_device");
@@ -1742,128 +1743,140 @@ struct Plan : PlanBase {
     }
     template <typename P> static P *shift(P *p, i64 d) { return (P *)((intptr_t)p + d); }
 
-    double t_addsn = 0, t_merge = 0;
-    // Supernodes of a level are independent: chunks of them are scheduled in
-    // parallel (parallel_for) into SchedOut's and merged in supernode order,
-    // which reproduces the sequential layout exactly.
+    double t_addsn = 0, t_merge = 0, t_resize = 0, t_put = 0, t_tiles = 0;
+    // Supernodes are scheduled in chunks (a level's supernodes in order, the
+    // levels in order) into SchedOut's, all chunks of all levels at once
+    // (add_supernode reads only the plan's structure); the tables are then
+    // sized once and every chunk copies (and relocates) its slices in
+    // parallel, which reproduces the sequential layout exactly.  Sizing per
+    // level instead regrew and value-initialised every table once per level,
+    // serially (66 of the 131 ms at 100^3).
     void build_schedule() {
         // value buffers first: work items point straight into them
         d_dpk.alloc(std::max<i64>(dpk_total, 1));
         d_pan.alloc_guarded(std::max<i64>(pan_total, 1), SB_UGUARD);
         d_dinv.alloc(std::max<i64>(dscr_max, 1));
+        const int NL = (int)levels.size();
+        vector<int> first(NL + 1, 0); // chunks of level L: [first[L], first[L+1])
+        for (int L = 0; L < NL; ++L) {
+            const int nk = (int)bylev[L].size();
+            first[L + 1] = first[L] + (nk >= 128 ? std::min(4 * plan_threads(), nk / 32) : 1);
+        }
+        const int NC = first[NL];
+        vector<SchedOut> outs(NC);
+        const auto ta = std::chrono::steady_clock::now();
+        parallel_for(NC, [&](int t) {
+            const int L = (int)(std::upper_bound(first.begin(), first.end(), t) - first.begin()) - 1;
+            const vector<int> &ks = bylev[L];
+            const i64 nk = (i64)ks.size(), nch = first[L + 1] - first[L], c = t - first[L];
+            for (i64 i = nk * c / nch; i < nk * (c + 1) / nch; ++i) add_supernode(ks[i], outs[t]);
+        }, 1);
+        t_addsn += ms_since(ta);
+        const auto tm0 = std::chrono::steady_clock::now();
+        enum { V_DIAG, V_DF, V_TL, V_TU, V_LF, V_UF, V_K, V_DC, V_RG, V_CG, V_PAIR, V_N };
+        vector<std::array<i64, V_N>> base(NC + 1);
+        {
+            SLU_REQUIRE(kinfos.empty() && h_rg.empty() && h_cg.empty() && h_pair.empty(),
+                        "build_schedule runs once per plan");
+            std::array<i64, V_N> b = {(i64)diag_items.size(), (i64)df_items.size(), (i64)tl_items.size(),
+                                      (i64)tu_items.size(), (i64)lf_items.size(), (i64)uf_items.size(),
+                                      0, (i64)dcopy.size(), 0, 0, 0};
+            for (int t = 0; t < NC; ++t) {
+                const SchedOut &O = outs[t];
+                base[t] = b;
+                b[V_DIAG] += O.diag_items.size();
+                b[V_DF] += O.df_items.size();
+                b[V_TL] += O.tl_items.size();
+                b[V_TU] += O.tu_items.size();
+                b[V_LF] += O.lf_items.size();
+                b[V_UF] += O.uf_items.size();
+                b[V_K] += O.kinfos.size();
+                b[V_DC] += O.dcopy.size();
+                b[V_RG] += O.h_rg.size();
+                b[V_CG] += O.h_cg.size();
+                b[V_PAIR] += O.h_pair.size();
+            }
+            base[NC] = b;
+            diag_items.resize(b[V_DIAG]);
+            df_items.resize(b[V_DF]);
+            tl_items.resize(b[V_TL]);
+            tu_items.resize(b[V_TU]);
+            lf_items.resize(b[V_LF]);
+            uf_items.resize(b[V_UF]);
+            kinfos.resize(b[V_K]);
+            khost.resize(b[V_K]);
+            dcopy.resize(b[V_DC]);
+            dcopy_src.resize(b[V_DC]);
+            h_rg.resize_uninit(b[V_RG]);
+            h_ra.resize_uninit(b[V_RG]);
+            h_cg.resize_uninit(b[V_CG]);
+            h_cb.resize_uninit(b[V_CG]);
+            h_ct0.resize_uninit(b[V_CG]);
+            h_cvoff.resize_uninit(b[V_CG]);
+            h_pair.resize_uninit(b[V_PAIR]);
+        }
+        t_resize += ms_since(tm0);
+        const auto tp0 = std::chrono::steady_clock::now();
+        parallel_for(NC, [&](int c) {
+            SchedOut &O = outs[c];
+            const std::array<i64, V_N> &B = base[c];
+            const i64 bc = B[V_CG], br = B[V_RG], bp = B[V_PAIR];
+            for (auto &k : O.kinfos) {
+                k.cvoff = shift(k.cvoff, bc);
+                k.ct0 = shift(k.ct0, bc);
+                k.cg = shift(k.cg, bc);
+                k.cb = shift(k.cb, bc);
+                k.rg = shift(k.rg, br);
+                k.ra = shift(k.ra, br);
+                k.pair = shift(k.pair, bp);
+            }
+            for (auto &t : O.uf_items) {
+                t.voff = shift(t.voff, bc);
+                t.t0 = shift(t.t0, bc);
+            }
+            for (auto &t : O.tu_items) {
+                t.voff = shift(t.voff, bc);
+                t.t0 = shift(t.t0, bc);
+            }
+            auto put = [](auto &dst, const auto &src, i64 at) {
+                std::copy(src.begin(), src.end(), dst.data() + at);
+            };
+            put(diag_items, O.diag_items, B[V_DIAG]);
+            put(df_items, O.df_items, B[V_DF]);
+            put(tl_items, O.tl_items, B[V_TL]);
+            put(tu_items, O.tu_items, B[V_TU]);
+            put(lf_items, O.lf_items, B[V_LF]);
+            put(uf_items, O.uf_items, B[V_UF]);
+            put(kinfos, O.kinfos, B[V_K]);
+            for (size_t i = 0; i < O.khost.size(); ++i) khost[B[V_K] + i] = std::move(O.khost[i]);
+            put(dcopy, O.dcopy, B[V_DC]);
+            put(dcopy_src, O.dcopy_src, B[V_DC]);
+            put(h_rg, O.h_rg, br);
+            put(h_ra, O.h_ra, br);
+            put(h_cg, O.h_cg, bc);
+            put(h_cb, O.h_cb, bc);
+            put(h_ct0, O.h_ct0, bc);
+            put(h_cvoff, O.h_cvoff, bc);
+            put(h_pair, O.h_pair, bp);
+        }, 1);
+        t_put += ms_since(tp0);
         vector<int> owner(lblk.size() + ublk.size(), -1), touched;
-        for (size_t L = 0; L < levels.size(); ++L) {
+        for (int L = 0; L < NL; ++L) {
+            const auto tt0 = std::chrono::steady_clock::now();
             LevelRange &R = levels[L];
-            R.diag_off = (int)diag_items.size();
-            R.tl_off = (int)tl_items.size();
-            R.tu_off = (int)tu_items.size();
-            R.k_off = (int)kinfos.size();
+            const std::array<i64, V_N> &B0 = base[first[L]], &B1 = base[first[L + 1]];
+            R.diag_off = (int)B0[V_DIAG];
+            R.tl_off = (int)B0[V_TL];
+            R.tu_off = (int)B0[V_TU];
+            R.k_off = (int)B0[V_K];
             R.tile_off = (int)tiles.size();
             R.big_off = (int)tiles_big.size();
-            R.df_off = (int)df_items.size();
-            R.lf_off = (int)lf_items.size();
-            R.uf_off = (int)uf_items.size();
-            R.dc_off = (int)dcopy.size();
-            const vector<int> &ks = bylev[L];
-            const int nk = (int)ks.size();
-            const int nch = nk >= 128 ? std::min(4 * plan_threads(), nk / 32) : 1;
-            vector<SchedOut> outs(nch);
-            const auto ta = std::chrono::steady_clock::now();
-            parallel_for(nch, [&](int c) {
-                const int a = (int)((i64)nk * c / nch), b = (int)((i64)nk * (c + 1) / nch);
-                for (int i = a; i < b; ++i) add_supernode(ks[i], outs[c]);
-            }, 1);
-            t_addsn += ms_since(ta);
-            const auto tm0 = std::chrono::steady_clock::now();
-            // merge in supernode order: bases by prefix sums, then every chunk
-            // copies (and relocates) its slices in parallel
-            enum { V_DIAG, V_DF, V_TL, V_TU, V_LF, V_UF, V_K, V_DC, V_RG, V_CG, V_PAIR, V_N };
-            vector<std::array<i64, V_N>> base(nch);
-            {
-                std::array<i64, V_N> b = {(i64)diag_items.size(), (i64)df_items.size(),
-                                          (i64)tl_items.size(), (i64)tu_items.size(),
-                                          (i64)lf_items.size(), (i64)uf_items.size(),
-                                          (i64)kinfos.size(), (i64)dcopy.size(), (i64)h_rg.size(),
-                                          (i64)h_cg.size(), (i64)h_pair.size()};
-                for (int c = 0; c < nch; ++c) {
-                    const SchedOut &O = outs[c];
-                    base[c] = b;
-                    b[V_DIAG] += O.diag_items.size();
-                    b[V_DF] += O.df_items.size();
-                    b[V_TL] += O.tl_items.size();
-                    b[V_TU] += O.tu_items.size();
-                    b[V_LF] += O.lf_items.size();
-                    b[V_UF] += O.uf_items.size();
-                    b[V_K] += O.kinfos.size();
-                    b[V_DC] += O.dcopy.size();
-                    b[V_RG] += O.h_rg.size();
-                    b[V_CG] += O.h_cg.size();
-                    b[V_PAIR] += O.h_pair.size();
-                }
-                diag_items.resize(b[V_DIAG]);
-                df_items.resize(b[V_DF]);
-                tl_items.resize(b[V_TL]);
-                tu_items.resize(b[V_TU]);
-                lf_items.resize(b[V_LF]);
-                uf_items.resize(b[V_UF]);
-                kinfos.resize(b[V_K]);
-                khost.resize(b[V_K]);
-                dcopy.resize(b[V_DC]);
-                dcopy_src.resize(b[V_DC]);
-                h_rg.resize(b[V_RG]);
-                h_ra.resize(b[V_RG]);
-                h_cg.resize(b[V_CG]);
-                h_cb.resize(b[V_CG]);
-                h_ct0.resize(b[V_CG]);
-                h_cvoff.resize(b[V_CG]);
-                h_pair.resize(b[V_PAIR]);
-            }
-            parallel_for(nch, [&](int c) {
-                SchedOut &O = outs[c];
-                const std::array<i64, V_N> &B = base[c];
-                const i64 bc = B[V_CG], br = B[V_RG], bp = B[V_PAIR];
-                for (auto &k : O.kinfos) {
-                    k.cvoff = shift(k.cvoff, bc);
-                    k.ct0 = shift(k.ct0, bc);
-                    k.cg = shift(k.cg, bc);
-                    k.cb = shift(k.cb, bc);
-                    k.rg = shift(k.rg, br);
-                    k.ra = shift(k.ra, br);
-                    k.pair = shift(k.pair, bp);
-                }
-                for (auto &t : O.uf_items) {
-                    t.voff = shift(t.voff, bc);
-                    t.t0 = shift(t.t0, bc);
-                }
-                for (auto &t : O.tu_items) {
-                    t.voff = shift(t.voff, bc);
-                    t.t0 = shift(t.t0, bc);
-                }
-                auto put = [](auto &dst, const auto &src, i64 at) {
-                    std::copy(src.begin(), src.end(), dst.begin() + at);
-                };
-                put(diag_items, O.diag_items, B[V_DIAG]);
-                put(df_items, O.df_items, B[V_DF]);
-                put(tl_items, O.tl_items, B[V_TL]);
-                put(tu_items, O.tu_items, B[V_TU]);
-                put(lf_items, O.lf_items, B[V_LF]);
-                put(uf_items, O.uf_items, B[V_UF]);
-                put(kinfos, O.kinfos, B[V_K]);
-                for (size_t i = 0; i < O.khost.size(); ++i) khost[B[V_K] + i] = std::move(O.khost[i]);
-                put(dcopy, O.dcopy, B[V_DC]);
-                put(dcopy_src, O.dcopy_src, B[V_DC]);
-                put(h_rg, O.h_rg, br);
-                put(h_ra, O.h_ra, br);
-                put(h_cg, O.h_cg, bc);
-                put(h_cb, O.h_cb, bc);
-                put(h_ct0, O.h_ct0, bc);
-                put(h_cvoff, O.h_cvoff, bc);
-                put(h_pair, O.h_pair, bp);
-            }, 1);
-            vector<int> kbase(nch);
-            for (int c = 0; c < nch; ++c) {
-                const SchedOut &O = outs[c];
-                kbase[c] = (int)(base[c][V_K] - R.k_off);
+            R.df_off = (int)B0[V_DF];
+            R.lf_off = (int)B0[V_LF];
+            R.uf_off = (int)B0[V_UF];
+            R.dc_off = (int)B0[V_DC];
+            for (int t = first[L]; t < first[L + 1]; ++t) {
+                const SchedOut &O = outs[t];
                 stats.panel_flops += O.panel_flops;
                 stats.schur_flops += O.schur_flops;
                 stats.schur_flops_padded += O.schur_flops_padded;
@@ -1878,31 +1891,33 @@ struct Plan : PlanBase {
             // critical tiles first: they are launched ahead of the rest so the
             // next level's panels can be factored while the rest runs
             for (int cls = 0; cls < 2; ++cls)
-                for (int c = 0; c < nch; ++c) {
-                    for (TileItem t : outs[c].big[cls]) {
-                        t.kslot += kbase[c];
-                        tiles_big.push_back(t);
+                for (int t = first[L]; t < first[L + 1]; ++t) {
+                    const int kb = (int)(base[t][V_K] - R.k_off);
+                    for (TileItem x : outs[t].big[cls]) {
+                        x.kslot += kb;
+                        tiles_big.push_back(x);
                     }
-                    for (TileItem t : outs[c].small[cls]) {
-                        t.kslot += kbase[c];
-                        tiles.push_back(t);
+                    for (TileItem x : outs[t].small[cls]) {
+                        x.kslot += kb;
+                        tiles.push_back(x);
                     }
                     if (cls == 0) {
-                        R.bigc_n += (int)outs[c].big[0].size();
-                        R.tilec_n += (int)outs[c].small[0].size();
+                        R.bigc_n += (int)outs[t].big[0].size();
+                        R.tilec_n += (int)outs[t].small[0].size();
                     }
                 }
             R.big_n = (int)tiles_big.size() - R.big_off;
-            R.df_n = (int)df_items.size() - R.df_off;
+            R.df_n = (int)(B1[V_DF] - B0[V_DF]);
             for (int i = R.df_off; i < R.df_off + R.df_n; ++i) R.df_maxw = std::max(R.df_maxw, df_items[i].w);
-            R.lf_n = (int)lf_items.size() - R.lf_off;
-            R.uf_n = (int)uf_items.size() - R.uf_off;
-            R.diag_n = (int)diag_items.size() - R.diag_off;
-            R.tl_n = (int)tl_items.size() - R.tl_off;
-            R.tu_n = (int)tu_items.size() - R.tu_off;
-            R.k_n = (int)kinfos.size() - R.k_off;
+            R.lf_n = (int)(B1[V_LF] - B0[V_LF]);
+            R.uf_n = (int)(B1[V_UF] - B0[V_UF]);
+            R.diag_n = (int)(B1[V_DIAG] - B0[V_DIAG]);
+            R.tl_n = (int)(B1[V_TL] - B0[V_TL]);
+            R.tu_n = (int)(B1[V_TU] - B0[V_TU]);
+            R.k_n = (int)(B1[V_K] - B0[V_K]);
             R.tile_n = (int)tiles.size() - R.tile_off;
-            R.dc_n = (int)dcopy.size() - R.dc_off;
+            R.dc_n = (int)(B1[V_DC] - B0[V_DC]);
+            t_tiles += ms_since(tt0);
             // conflicting destinations inside the level -> atomics
             touched.clear();
             for (int s = R.k_off; s < R.k_off + R.k_n; ++s) {
@@ -1919,12 +1934,12 @@ struct Plan : PlanBase {
                 }
             }
             for (int key : touched) owner[key] = -1;
-            t_merge += ms_since(tm0);
             for (int i = R.big_off; i < R.big_off + R.big_n; ++i)
                 R.atomic_tiles += kinfos[R.k_off + tiles_big[i].kslot].atomic;
             for (int i = R.tile_off; i < R.tile_off + R.tile_n; ++i)
                 R.atomic_tiles += kinfos[R.k_off + tiles[i].kslot].atomic;
         }
+        t_merge += ms_since(tm0);
         khost.clear();
     }
 

@@ -1296,9 +1296,6 @@ k_schur_big(const TileItem *tiles, const KInfo<T> *kinfo, T *Lval, T *Uval,
     gload(0);
     lstore(0, 0);
     __syncthreads();
-#ifdef SLU_SB_PRIO
-    __builtin_amdgcn_s_setprio(1);
-#endif
     SB_STAMP(c1_);
     auto mfma_stage = [&](int st) {
         const T *sA = smem + (st & 1) * STAGE, *sB = sA + SB_BK * LDS_A;
@@ -1317,14 +1314,6 @@ k_schur_big(const TileItem *tiles, const KInfo<T> *kinfo, T *Lval, T *Uval,
 #pragma unroll
                 for (int fn = 0; fn < FN; ++fn) M::step(acc[fm][fn], av[fm], bv[fn]);
         }
-#ifdef SLU_SB_SGB
-        // interleave: per k step its 6 LDS reads ahead of the previous step's MFMAs
-#pragma unroll
-        for (int ks = 0; ks < SB_BK / M::KSTEP; ++ks) {
-            __builtin_amdgcn_sched_group_barrier(0x100, FM + FN, 0);
-            __builtin_amdgcn_sched_group_barrier(0x008, FM * FN, 0);
-        }
-#endif
     };
     for (int st = 0; st + 1 < nst; ++st) {
         gload((st + 1) * SB_BK);
@@ -1365,9 +1354,6 @@ k_schur_big(const TileItem *tiles, const KInfo<T> *kinfo, T *Lval, T *Uval,
         }
     }
     mfma_stage(nst - 1);
-#ifdef SLU_SB_PRIO
-    __builtin_amdgcn_s_setprio(0);
-#endif
     __syncthreads();
     if (tbl) {
         if (tid < CPN) s_cp[tid] = t_code ? t_code : (t_uv - t_fst) * 8;
