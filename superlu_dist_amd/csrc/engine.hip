@@ -2180,6 +2180,10 @@ struct Plan : PlanBase {
 
     // ------------------------------------------------------- device
     void build_device() {
+        const auto tb0 = std::chrono::steady_clock::now();
+        auto sub = [&](const char *what, double mb) {
+            if (prof) fprintf(stderr, "[slu plan %d]   build_device %-10s %6.1f ms %8.1f MB\n", iam, what, ms_since(tb0), mb);
+        };
         d_rg.upload(h_rg);
         d_ra.upload(h_ra);
         d_cg.upload(h_cg);
@@ -2211,6 +2215,8 @@ struct Plan : PlanBase {
         }
         d_ct0.upload(h_ct0);
         d_cvoff.upload(h_cvoff);
+        sub("panels", (d_rg.bytes() + d_ra.bytes() + d_cg.bytes() + d_cb.bytes() + d_pair.bytes() + d_prec.bytes() +
+                       d_ct0.bytes() + d_cvoff.bytes()) / 1e6);
         for (auto &t : tu_items) {
             intptr_t co = (intptr_t)t.voff;
             t.voff = d_cvoff.p + co;
@@ -2252,11 +2258,14 @@ struct Plan : PlanBase {
         d_tiles_big.upload(tiles_big);
         d_dcopy.upload(dcopy);
         d_pcopy.upload(pcopy);
+        sub("items", (d_df.bytes() + d_lf.bytes() + d_uf.bytes() + d_kinfo.bytes() + d_tiles.bytes() +
+                      d_tiles_big.bytes()) / 1e6);
         d_lblk.upload(lblk);
         d_lmap.upload(lmap);
         d_ublk.upload(ublk);
         d_ucol_voff.upload(ucol_voff);
         d_ucol_fst.upload(ucol_fst);
+        sub("blocks", (d_lblk.bytes() + d_lmap.bytes() + d_ublk.bytes() + d_ucol_voff.bytes() + d_ucol_fst.bytes()) / 1e6);
         d_counters.alloc(4);
         d_zpiv.alloc(nsupers);
         d_dsflags.alloc(std::max<size_t>(df_items.size(), 1) * DS_MAXS);
@@ -3805,7 +3814,10 @@ struct AmalgPlan : PlanBase {
         mlu.Llu = &mllu;
         slu_engine_opts io = opts;
         io.overlap_upload = io.overlap_download = 0;
+        const auto tj = std::chrono::steady_clock::now();
         if (alloc_thread.joinable()) alloc_thread.join();
+        if (getenv("SLU_PROFILE_PLAN"))
+            fprintf(stderr, "[slu amalg plan]   (coarse storage: waited %.1f ms)\n", ms_since(tj));
         SLU_REQUIRE(alloc_err.empty(), "%s", alloc_err.c_str());
         in.reset(new Inner(&mlu, n, 1, 1, 0, nullptr, &io, pre));
     }
