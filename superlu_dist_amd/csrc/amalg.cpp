@@ -243,6 +243,17 @@ std::vector<int> amalg_chains(int64_t n, int ns, const int_t *xsup, const int_t 
     }, 1);
     std::vector<int> gstart;
     for (auto &v : rstart) gstart.insert(gstart.end(), v.begin(), v.end());
+    if (prof) { // the longest run bounds the pass (its chains are sequential)
+        i64 tot = 0, mx = 0, mxlen = 0;
+        for (int ri = 0; ri < nruns; ++ri) {
+            i64 c = 0;
+            for (int s = runs[ri]; s < runs[ri + 1]; ++s) c += inf[s - a0].ucols;
+            tot += c;
+            if (c > mx) { mx = c; mxlen = runs[ri + 1] - runs[ri]; }
+        }
+        fprintf(stderr, "[slu amalg] pass 2: %d runs, U column entries %lld, longest run %lld supernodes %lld entries\n",
+                nruns, (long long)tot, (long long)mxlen, (long long)mx);
+    }
     tick("pass 2 (chains)");
     return gstart;
 }

@@ -3662,6 +3662,19 @@ struct AmalgPlan : PlanBase {
     std::thread alloc_thread;
     std::string alloc_err;
     std::mutex o_mu; // ensure_o: the upload thread or the D2H program build
+    // fresh HBM is mapped at its first touch (~18 ms per GB); the caller-layout
+    // buffers are touched first thing on the upload thread (o_mapped), and
+    // with SLU_MAP_ORDER=1 the coarse storage's touch waits for that
+    std::mutex map_mu;
+    std::condition_variable map_cv;
+    bool o_mapped = false;
+    double t_omap = 0;
+    std::chrono::steady_clock::time_point t_born = std::chrono::steady_clock::now();
+    void set_mapped() {
+        std::lock_guard<std::mutex> lk(map_mu);
+        o_mapped = true;
+        map_cv.notify_all();
+    }
     // the D2H's pinned slots and HBM staging slots, allocated and touched
     // (one DMA through each) beside the plan build: lazily, the first
     // factorization paid ~70 ms more D2H tail for them
@@ -3720,8 +3733,18 @@ struct AmalgPlan : PlanBase {
             raw->alloc_thread = std::thread([raw, lv2, uv2] {
                 try {
                     HIPCHK(hipSetDevice(0));
+                    const char *mo = getenv("SLU_MAP_ORDER");
+                    if (mo && atoi(mo) == 1 && raw->opts.overlap_upload) {
+                        std::unique_lock<std::mutex> lk(raw->map_mu);
+                        raw->map_cv.wait(lk, [raw] { return raw->o_mapped; });
+                    }
+                    const auto ta = std::chrono::steady_clock::now();
+                    const double at = ms_since(raw->t_born);
                     raw->pre[0].alloc_guarded(std::max<i64>(lv2, 1), SB_UGUARD);
                     raw->pre[1].alloc_guarded(std::max<i64>(uv2, 1), SB_UGUARD);
+                    if (getenv("SLU_PROFILE_PLAN"))
+                        fprintf(stderr, "[slu amalg plan]   (coarse storage %.1f GB mapped in %.1f ms, from %.1f ms)\n",
+                                (lv2 + uv2) * sizeof(T) / 1e9, ms_since(ta), at);
                 } catch (const std::exception &e) {
                     raw->alloc_err = e.what();
                 }
@@ -3736,6 +3759,7 @@ struct AmalgPlan : PlanBase {
                 } catch (const std::exception &e) {
                     raw->up_err = e.what();
                 }
+                raw->set_mapped(); // (also on failure: the coarse storage's touch may wait for it)
             });
         }
         if (P->opts.overlap_download) {
@@ -4041,6 +4065,19 @@ struct AmalgPlan : PlanBase {
     void h2d() {
         const auto t0 = std::chrono::steady_clock::now();
         vector<Xfer> xs = xfers();
+        if (!o_mapped) {
+            hipStream_t st = nullptr;
+            HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+            HIPCHK(hipMemsetAsync(d_oL.p, 0, sizeof(T), st));
+            HIPCHK(hipMemsetAsync(d_oU.p, 0, sizeof(T), st));
+            HIPCHK(hipStreamSynchronize(st));
+            HIPCHK(hipStreamDestroy(st));
+            t_omap = ms_since(t0);
+            if (getenv("SLU_PROFILE_PLAN"))
+                fprintf(stderr, "[slu amalg plan]   (caller-layout storage %.1f GB mapped in %.1f ms, at %.1f ms)\n",
+                        (d_oL.bytes() + d_oU.bytes()) / 1e9, t_omap, ms_since(t_born));
+            set_mapped();
+        }
         staged_h2d(xs, 0);
         h2d_bytes = 0;
         for (auto &x : xs) h2d_bytes += (double)x.bytes;
