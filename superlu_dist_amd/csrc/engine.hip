@@ -3662,9 +3662,9 @@ struct AmalgPlan : PlanBase {
     std::thread alloc_thread;
     std::string alloc_err;
     std::mutex o_mu; // ensure_o: the upload thread or the D2H program build
-    // fresh HBM is mapped at its first touch (~18 ms per GB); the caller-layout
-    // buffers are touched first thing on the upload thread (o_mapped), and
-    // with SLU_MAP_ORDER=1 the coarse storage's touch waits for that
+    // fresh HBM is mapped at its first touch; the caller-layout buffers are
+    // touched first thing on the upload thread (o_mapped), and the D2H warm-up
+    // (pinned slots) waits for that
     std::mutex map_mu;
     std::condition_variable map_cv;
     bool o_mapped = false;
@@ -3733,11 +3733,6 @@ struct AmalgPlan : PlanBase {
             raw->alloc_thread = std::thread([raw, lv2, uv2] {
                 try {
                     HIPCHK(hipSetDevice(0));
-                    const char *mo = getenv("SLU_MAP_ORDER");
-                    if (mo && atoi(mo) == 1 && raw->opts.overlap_upload) {
-                        std::unique_lock<std::mutex> lk(raw->map_mu);
-                        raw->map_cv.wait(lk, [raw] { return raw->o_mapped; });
-                    }
                     const auto ta = std::chrono::steady_clock::now();
                     const double at = ms_since(raw->t_born);
                     raw->pre[0].alloc_guarded(std::max<i64>(lv2, 1), SB_UGUARD);
@@ -3759,7 +3754,7 @@ struct AmalgPlan : PlanBase {
                 } catch (const std::exception &e) {
                     raw->up_err = e.what();
                 }
-                raw->set_mapped(); // (also on failure: the coarse storage's touch may wait for it)
+                raw->set_mapped(); // (also on failure: the warm-up waits for it)
             });
         }
         if (P->opts.overlap_download) {
@@ -3767,6 +3762,13 @@ struct AmalgPlan : PlanBase {
             raw->warm_thread = std::thread([raw] {
                 try {
                     HIPCHK(hipSetDevice(0));
+                    // after the caller-layout buffers' mapping: beside it the
+                    // pinned allocation made that mapping 102-274 instead of
+                    // 34-37 ms (profiles/r04y)
+                    if (raw->opts.overlap_upload) {
+                        std::unique_lock<std::mutex> lk(raw->map_mu);
+                        raw->map_cv.wait(lk, [raw] { return raw->o_mapped; });
+                    }
                     i64 slot = 128ll << 20; // (Plan::D2H_SLOT, and its override as in build_d2h)
                     if (const char *e = getenv("SLU_D2H_SLOT_KB")) slot = std::max<i64>(16, atoll(e)) << 10;
                     constexpr int NS = Inner::D2H_NS;
