@@ -440,8 +440,11 @@ int_t pxgstrf(int dtype, const char *name, superlu_dist_options_t *options, int 
         const int rt = options->ReplaceTinyPivot == SLU_YES;
         uint64_t dg = 0, sdg = 0;
         // a miss on the shallow digest is a miss: the full digest is then
-        // only stored with the new plan, and is computed beside its build
+        // only stored with the new plan, and is computed beside the upload and
+        // the factorization (beside the plan build it took memory bandwidth
+        // and cores from the analysis passes)
         std::future<uint64_t> dg_later;
+        bool dg_needed = false;
         if (cache) {
             sdg = shallow_digest(LUstruct, n, grid);
             bool hit;
@@ -458,9 +461,7 @@ int_t pxgstrf(int dtype, const char *name, superlu_dist_options_t *options, int 
                 hit = full == dg;
                 dg = full;
             } else if (!hit) {
-                dg_later = std::async(std::launch::async, [LUstruct, n, grid] {
-                    return structure_digest(LUstruct, n, grid);
-                });
+                dg_needed = true;
             }
             hit = all_ranks(hit, grid);
             std::lock_guard<std::mutex> lk(g_cache_mu);
@@ -516,6 +517,10 @@ int_t pxgstrf(int dtype, const char *name, superlu_dist_options_t *options, int 
                                    grid->iam, c, &eo, err, sizeof err);
             if (!plan) throw slu::Error(err);
         }
+        if (dg_needed)
+            dg_later = std::async(std::launch::async, [LUstruct, n, grid] {
+                return structure_digest(LUstruct, n, grid);
+            });
         int myinfo = 0, tiny = 0;
         tp[2] = clk::now();
         const double cpu2 = timing ? process_cpu_ms() : 0;

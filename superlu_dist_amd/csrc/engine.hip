@@ -641,9 +641,12 @@ struct Plan : PlanBase {
         // next level's diag LU / TRSM / exchanges): higher priority, so its
         // workgroups are dispatched ahead of the bulk Schur update's
         int prio_lo = 0, prio_hi = 0;
+        const auto ts0 = std::chrono::steady_clock::now();
         HIPCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
         HIPCHK(hipStreamCreateWithPriority(&stream, hipStreamNonBlocking, prio_lo));
         HIPCHK(hipStreamCreateWithPriority(&pstream, hipStreamNonBlocking, prio_hi));
+        if (getenv("SLU_PROFILE_PLAN"))
+            fprintf(stderr, "[slu plan %d] streams               %6.1f ms\n", iam, ms_since(ts0));
         X.s = pstream;
         int_t *hx = LU->Glu_persist->xsup;
         nsupers = (int)(LU->Glu_persist->supno[n - 1] + 1);
