@@ -995,8 +995,9 @@ float pxdistribute(int dtype, const char *name, superlu_dist_options_t *options,
             g_deva.lrow = LU->Llu->Lrowind_bc_ptr;
             g_deva.dtype = dtype;
             g_deva.n = n;
-            g_deva.xa = xa;
-            g_deva.asub = asub;
+            // (the last use of xa / asub: moved, not copied)
+            g_deva.xa = std::move(xa);
+            g_deva.asub = std::move(asub);
             g_deva.a.assign((const char *)aval.data(), (const char *)(aval.data() + aval.size()));
             g_deva.gen = ++g_deva_gen;
         };
