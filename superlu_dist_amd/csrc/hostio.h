@@ -101,8 +101,12 @@ __global__ void __launch_bounds__(256) k_push(const PushSeg *segs, int n, char *
 }
 
 // Host -> device through a pinned ring: nthr threads, 2 buffers each.
-inline void staged_h2d(const std::vector<Xfer> &xs, int device, int nthr = 4,
+inline void staged_h2d(const std::vector<Xfer> &xs, int device, int nthr = 0,
                        size_t chunk = 32u << 20) {
+    if (nthr <= 0) { // SLU_H2D_THREADS (default 4)
+        const char *e = getenv("SLU_H2D_THREADS");
+        nthr = e && atoi(e) > 0 ? std::min(32, atoi(e)) : 4;
+    }
     struct Piece {
         const Xfer *x;
         size_t off, len;
