@@ -290,6 +290,58 @@ def cpu_baseline(A, perm, nx, nranks, timeout, flops, symbolic="reference", gpu_
                        f"thread, MKL sequential; factor time {t:.2f} s"}, parity)
 
 
+def preflight_parity(args, comm, pr, pc, myrow, mycol, rank, dist):
+    """Multi-rank runs, the checker (the reference checks
+    every grid run, TEST/pdtest.c:372-393): before the timed run, factor the
+    same workload at a small size (--preflight-nx, default 40) through the
+    same transport and grid, gather every rank's per-block fingerprints of
+    its factors (oracle/blocksum.h) to rank 0 and compare them with the
+    reference pdgstrf's on the same grid (oracle/_ref/ref_pdgstrf, CPU).
+    Returns the parity record on rank 0 (None elsewhere)."""
+    from superlu_dist_amd.engine import Plan
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+    nx = args.preflight_nx
+    t0 = time.time()
+    A, S, lu, perm = build_lu(args.workload, nx, pr, pc, myrow, mycol, args.ordering, args.symbolic)
+    p = Plan(lu, comm=comm)
+    p.upload()
+    info, _ = p.factor(one_norm(A))
+    p.download()
+    nsup = int(p.stats()["nsupers"])
+    del p
+    mine = pyoracle.blocksums(lu)
+    allsums = [None] * (pr * pc)
+    dist.all_gather_object(allsums, mine)
+    infos = [None] * (pr * pc)
+    dist.all_gather_object(infos, int(info))
+    t_gpu = time.time() - t0
+    if rank != 0:
+        return None
+    rec = {"preflight": f"{args.workload} nx={nx} (n={A.n}), {pr}x{pc} grid, factored on the "
+                        f"GPUs through the same transport before the timed run",
+           "against": f"reference pdgstrf on a {pr}x{pc} grid (oracle/_ref/ref_pdgstrf)",
+           "tolerance": 1e-12 if lu.Lval.dtype.itemsize >= 8 else 1e-5,
+           "info": infos, "nsupers_factored_rank0": nsup, "gpu_s": round(t_gpu, 2),
+           "method": "per-block fingerprints keyed by global (ib, jb), all ranks "
+                     "(oracle/blocksum.h; pyoracle.compare_blocksums)"}
+    if not pyoracle.have_reference_harness():
+        rec.update(ok=None, note="oracle/_ref not built: parity unchecked")
+        return rec
+    try:
+        st, _ = pyoracle.run_reference(A, perm, pr, pc, relax=60, maxsup=256, lookahead=10,
+                                       want_factors=False, timeout=600,
+                                       symb_flags=2 if args.symbolic == "reference" else 0,
+                                       want_blocksums=True)
+    except Exception as e:  # noqa: BLE001
+        rec.update(ok=False, error=f"reference run failed: {e}")
+        return rec
+    c = pyoracle.compare_blocksums(np.concatenate(allsums), st["blocksums"])
+    rec.update({k: (float(v) if isinstance(v, (float, np.floating)) else v) for k, v in c.items()})
+    rec["ok"] = bool(c["match"] and c["rel_err"] <= rec["tolerance"] and max(infos) == 0)
+    return rec
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -319,6 +371,11 @@ def main():
                     help="3D process grid (pdgstrf3d): PZ layers of a PR x PC grid, PR*PC*PZ = "
                          "--gpus; the layers factor the etree's forests and reduce the "
                          "ancestors between them (default: the 2D grid of --gpus ranks)")
+    ap.add_argument("--preflight-nx", type=int, default=40,
+                    help="multi-rank runs: grid points per dimension of the parity preflight "
+                         "(0 skips it)")
+    ap.add_argument("--rank-timeout", type=float, default=float(os.environ.get("SLU_BENCH_TIMEOUT_S", 1500)),
+                    help="--gpus N without a launcher: seconds before the spawned ranks are killed")
     ap.add_argument("--host-transport", action="store_true",
                     help="REHEARSAL ONLY: several ranks on one GPU through the host-staged "
                          "point-to-point test transport (the RCCL send / receive pairs over "
@@ -333,7 +390,7 @@ def main():
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # `bench.py --gpus N` without a launcher: start the N ranks here,
         # before anything touches the GPU (torch.distributed.run does the same)
-        sys.exit(spawn_ranks(args.gpus))
+        sys.exit(spawn_ranks(args.gpus, args.rank_timeout))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -408,6 +465,12 @@ def main():
             sys.exit(3)
         log(f"communicators: layer {sizes[0]}, row {sizes[1]}, column {sizes[2]}, "
             f"{sizes[3]} layers")
+    parity_pre = None
+    if world > 1 and pz == 1 and args.preflight_nx > 0 and not args.roofline_only:
+        log(f"parity preflight nx={args.preflight_nx} on the {gname} grid")
+        parity_pre = preflight_parity(args, comm, pr, pc, myrow, mycol, rank, dist)
+        if rank == 0:
+            log(f"parity preflight: ok={parity_pre.get('ok')} rel_err={parity_pre.get('rel_err')}")
     t0 = time.time()
     plan = Plan(lu, comm=comm, timing=2 if args.level_log else 1)
     t_plan = time.time() - t0
@@ -569,7 +632,7 @@ def main():
                        "comm_volume_gb_rank0": round(st0["comm_bytes"] / 1e9, 3)},
             "roofline": roof,
             "cpu_baseline": cpu,
-            "parity": parity,
+            "parity": parity if parity is not None else parity_pre,
             "next_rows": nxt,
             "abi_pdgstrf": abi,
             "phases_ms_per_step_rank0": {k[2:-3]: round(v / K, 3) for k, v in acc.items()},
@@ -584,11 +647,15 @@ def main():
         dist.destroy_process_group()
 
 
-def spawn_ranks(n):
+def spawn_ranks(n, timeout_s=1500.0):
     """One child process per rank with the torch.distributed.run environment
     (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT); rank 0's
-    stdout is ours (the one JSON line), the others' goes to stderr.  Returns
-    the first non-zero exit status (0 if all ranks succeeded)."""
+    stdout is ours (the one JSON line), the others' goes to stderr.  When a
+    rank fails, or the ranks are still running after timeout_s seconds, the
+    others are terminated (killed 15 s later) instead of waiting for a peer
+    that is gone: a rank whose exchange never completes ends through the
+    engine's watchdog (exit 86, csrc/watchdog.h), its peers through this.
+    Returns the first non-zero exit status (0 if all ranks succeeded)."""
     import socket
     with socket.socket() as so:
         so.bind(("127.0.0.1", 0))
@@ -599,9 +666,36 @@ def spawn_ranks(n):
                    LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable] + sys.argv, env=env,
                                       stdout=None if r == 0 else sys.stderr))
-    codes = [p.wait() for p in procs]
+    deadline = time.time() + timeout_s
+    codes = [None] * n
+    why = None
+    while any(c is None for c in codes):
+        for i, p in enumerate(procs):
+            if codes[i] is None:
+                codes[i] = p.poll()
+        failed = [(i, c) for i, c in enumerate(codes) if c not in (None, 0)]
+        if failed and any(c is None for c in codes):
+            why = f"rank {failed[0][0]} exited with {failed[0][1]}"
+        elif time.time() > deadline and any(c is None for c in codes):
+            why = f"ranks still running after {timeout_s:.0f} s"
+        if why:
+            log(f"{why}: terminating the other ranks")
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            t_kill = time.time() + 15
+            for i, p in enumerate(procs):
+                try:
+                    codes[i] = p.wait(max(0.1, t_kill - time.time()))
+                except subprocess.TimeoutExpired:
+                    p.kill()
+                    codes[i] = p.wait()
+            break
+        time.sleep(0.2)
     log(f"ranks exited with {codes}")
-    return next((c for c in codes if c != 0), 0)
+    if why and all(c == 0 or c < 0 for c in codes):
+        return 124
+    return next((c for c in codes if c not in (0, None) and c > 0), next((c for c in codes if c), 0))
 
 
 def pmc_traffic(workload, nx, pr, pc, kernel):

@@ -129,8 +129,11 @@ int mpi_host_bcast(void *ctx, int group, int root, void *buf, int64_t bytes) {
     return 0;
 }
 
+void evict_for_comm(slu_comm *c); // (plan cache, below)
+
 int grid_attr_delete(MPI_Comm, int, void *val, void *) {
     GridComm *g = (GridComm *)val;
+    evict_for_comm(g->c); // a cached plan must never outlive its transport
     slu_comm_destroy(g->c);
     delete g;
     return MPI_SUCCESS;
@@ -245,6 +248,7 @@ struct CachedPlan {
     bool a_pattern = false;   // the plan holds DevA's pattern (fill_a ready)
     uint64_t a_pattern_gen = 0; // ... of this DevA pattern generation
     bool host_factors = true; // the host L / U arrays hold these factors
+    slu_comm *comm = nullptr; // the transport the plan was built with (grid->comm's)
 };
 CachedPlan g_cache;
 std::mutex g_cache_mu;
@@ -270,6 +274,25 @@ void evict_cached() {
     if (!g_cache.host_factors) g_evicted.push_back(g_cache.key);
     reap_later(g_cache.plan);
     g_cache.plan = nullptr;
+}
+
+// superlu_gridexit frees grid->comm, whose attribute delete callback destroys
+// the engine communicators: a cached plan built on them goes first, and
+// synchronously (a reaper thread could still be in the plan while the
+// communicators are torn down).  Without this a later grid whose comm handle
+// and LUstruct land on the same addresses would hit the cache and call into
+// the freed transport.
+void evict_for_comm(slu_comm *c) {
+    slu_plan *p = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(g_cache_mu);
+        if (!g_cache.plan || g_cache.comm != c) return;
+        if (!g_cache.host_factors) g_evicted.push_back(g_cache.key);
+        p = g_cache.plan;
+        g_cache.plan = nullptr;
+    }
+    reap_join();
+    slu_plan_destroy(p);
 }
 
 // A in the LUstruct's coordinates (CSC), kept by this library's pddistribute
@@ -311,7 +334,7 @@ template <typename LUS> uint64_t structure_digest(LUS *lu, int n, const gridinfo
         return h;
     };
     slu::parallel_for(nb, [&](int j) {
-        uint64_t h = mix((uint64_t)j, (uint64_t)xsup[std::min(j + 1, ns)]);
+        uint64_t h = (uint64_t)j;
         if (j < nlc)
             if (const int_t *ix = lu->Llu->Lrowind_bc_ptr[j]) {
                 i64 p = SLU_BC_HEADER;
@@ -330,6 +353,7 @@ template <typename LUS> uint64_t structure_digest(LUS *lu, int n, const gridinfo
         part[j] = h;
     });
     uint64_t h = mix((uint64_t)n, (uint64_t)ns);
+    for (int j = 0; j <= ns; ++j) h = mix(h, (uint64_t)xsup[j]); // every global xsup entry
     h = mix(h, (uint64_t)(uintptr_t)lu);
     h = mix(h, (uint64_t)(uintptr_t)lu->Llu);
     h = mix(h, ((uint64_t)Pr << 32) | (uint64_t)Pc);
@@ -352,7 +376,6 @@ template <typename LUS> uint64_t shallow_digest(LUS *lu, int n, const gridinfo_t
     slu::parallel_for((int)part.size(), [&](int c) {
         uint64_t h = (uint64_t)c;
         for (int j = c * CH; j < std::min(nb, (c + 1) * CH); ++j) {
-            h = mix(h, (uint64_t)xsup[std::min(j + 1, ns)]);
             if (j < nlc) {
                 const int_t *ix = L->Lrowind_bc_ptr[j];
                 h = mix(h, (uint64_t)(uintptr_t)ix);
@@ -369,6 +392,7 @@ template <typename LUS> uint64_t shallow_digest(LUS *lu, int n, const gridinfo_t
         part[c] = h;
     }, 1);
     uint64_t h = mix(mix((uint64_t)n, (uint64_t)ns), 0x5A11u);
+    for (int j = 0; j <= ns; ++j) h = mix(h, (uint64_t)xsup[j]); // every global xsup entry
     h = mix(h, (uint64_t)(uintptr_t)lu);
     h = mix(h, (uint64_t)(uintptr_t)L);
     h = mix(h, (uint64_t)(uintptr_t)L->Lrowind_bc_ptr);
@@ -425,7 +449,11 @@ int_t pxgstrf(int dtype, const char *name, superlu_dist_options_t *options, int 
     // SUPERLU_MI355X_FACTOR_SKIP=1 (test hook, no GPU needed): return at once,
     // the LUstruct untouched -- the distribute / destroy ownership test runs
     // the reference's p?gssvx around this library's p?distribute on the CPU
-    if (const char *sk = getenv("SUPERLU_MI355X_FACTOR_SKIP"); sk && atoi(sk) == 1) return 0;
+    if (const char *sk = getenv("SUPERLU_MI355X_FACTOR_SKIP"); sk && atoi(sk) == 1) {
+        fprintf(stderr, "%s (MI355X library): SUPERLU_MI355X_FACTOR_SKIP=1 is set: test hook, the "
+                        "LUstruct is NOT factored\n", name);
+        return 0;
+    }
     slu_plan *plan = nullptr;
     // SUPERLU_MI355X_TIMING=1: wall-clock breakdown of the call on stderr
     const char *tm = getenv("SUPERLU_MI355X_TIMING");
@@ -445,13 +473,17 @@ int_t pxgstrf(int dtype, const char *name, superlu_dist_options_t *options, int 
         // and cores from the analysis passes)
         std::future<uint64_t> dg_later;
         bool dg_needed = false;
+        // this grid's transport (collective only when it is created): a cached
+        // plan is reused only on the communicators it was built with
+        slu_comm *const gcomm = comm_for_grid(grid);
         if (cache) {
             sdg = shallow_digest(LUstruct, n, grid);
             bool hit;
             {
                 std::lock_guard<std::mutex> lk(g_cache_mu);
                 hit = g_cache.plan && g_cache.shallow == sdg && g_cache.key == lu_key(LUstruct) &&
-                      g_cache.dtype == dtype && g_cache.n == n && g_cache.replace_tiny == rt;
+                      g_cache.dtype == dtype && g_cache.n == n && g_cache.replace_tiny == rt &&
+                      g_cache.comm == gcomm;
                 if (hit) dg = g_cache.digest;
             }
             // Fact = SamePattern_SameRowPerm: the previous factorization's L & U
@@ -499,7 +531,7 @@ int_t pxgstrf(int dtype, const char *name, superlu_dist_options_t *options, int 
         }
         if (!plan) {
             reap_join(); // the previous call's device memory is free again
-            slu_comm *c = comm_for_grid(grid);
+            slu_comm *c = gcomm;
             slu_engine_opts eo{};
             eo.replace_tiny_pivot = rt;
             // utime[FACT] (SRC/pdgssvx.c:1174-1180) covers the copies too: the
@@ -572,6 +604,7 @@ int_t pxgstrf(int dtype, const char *name, superlu_dist_options_t *options, int 
             g_cache.a_pattern_gen = da ? da->pattern_gen : 0;
             g_cache.host_factors = !keep_on_device;
             g_cache.key = lu_key(LUstruct);
+            g_cache.comm = gcomm;
         } else {
             reap_later(plan);
         }
@@ -822,10 +855,12 @@ void pxgstrs(int dtype, const char *name, int_t n, LUS *LU, xScalePermstruct_t *
             // the plan of the last pdgstrf on this LUstruct still holds its
             // factors in HBM (grids too: its coarse storage); every rank of a
             // grid must agree, the solve is collective
+            slu_comm *const gcomm = comm_for_grid(grid);
             bool hit;
             {
                 std::lock_guard<std::mutex> lk(g_cache_mu);
-                hit = g_cache.plan && g_cache.key == lu_key(LU) && g_cache.dtype == dtype && g_cache.n == n;
+                hit = g_cache.plan && g_cache.key == lu_key(LU) && g_cache.dtype == dtype && g_cache.n == n &&
+                      g_cache.comm == gcomm;
             }
             if (all_ranks(hit, grid)) {
                 std::lock_guard<std::mutex> lk(g_cache_mu);

@@ -587,6 +587,8 @@ void Amalg::build_programs() {
                 for (i64 c = 0; c < w; ++c) {
                     const i64 fst = ux[p + SLU_UB_DESCRIPTOR + c];
                     if (fst >= R.end) continue;
+                    SLU_REQUIRE(R.end - fst <= 65536, "amalgamation: U segment of %lld rows (> 65536)",
+                                (long long)(R.end - fst));
                     ucd[f0] = (int32_t)(d0 + c);
                     ucl[f0] = (uint16_t)(R.end - fst - 1);
                     ++f0;

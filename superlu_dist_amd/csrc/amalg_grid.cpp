@@ -567,6 +567,8 @@ void ga_receive_side(const GaFine &f, const GaPartition &g, const GaStreams &in,
                 if (nc == 0) r.unpack_u.push_back({off, (i64)r.unpack_ucd.size(), 0, (int32_t)end});
                 const i64 didx = Jp == I ? r.DL0 + xsup[jb] + c : ce0 + c;
                 r.unpack_ucd.push_back((int32_t)didx);
+                SLU_REQUIRE(end - fst <= 65536, "grid amalgamation: U segment of %lld rows (> 65536)",
+                            (long long)(end - fst));
                 r.unpack_ucl.push_back((uint16_t)(end - fst - 1));
                 off += end - fst;
                 r.unpack_u.back().nc = ++nc;

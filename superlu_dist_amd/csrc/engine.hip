@@ -48,6 +48,7 @@
 #include "hostio.h"
 #include "amalg.h"
 #include "amalg_dev.h"
+#include "watchdog.h"
 #include "slu_mi355x.h"
 
 using std::vector;
@@ -118,6 +119,42 @@ struct slu_comm {
     slu_host_bcast_fn host_fn = nullptr;
     slu_host_p2p_fn host_p2p = nullptr; // point-to-point test transport
     void *host_ctx = nullptr;
+    // exchange watchdog (watchdog.h), created with the first exchange
+    std::unique_ptr<slu::Watchdog> wd;
+    bool wd_init = false;
+    slu::Watchdog *watchdog() {
+        if (wd_init) return wd.get();
+        wd_init = true;
+        const double b = slu::Watchdog::bound_from_env();
+        if (b <= 0) return nullptr;
+        wd.reset(new slu::Watchdog);
+        wd->bound_s = b;
+        wd->device = device;
+        char w[160];
+        snprintf(w, sizeof w, "rank %d of a %dx%d%s grid (row %d, column %d%s), %s transport", iam, nprow, npcol,
+                 npdep > 1 ? ("x" + std::to_string(npdep)).c_str() : "", myrow, mycol,
+                 npdep > 1 ? (", layer " + std::to_string(zlayer)).c_str() : "",
+                 world || zcomm ? "RCCL" : host_p2p ? "host point-to-point" : "host broadcast");
+        wd->who = w;
+        if (world || zcomm) {
+            ncclComm_t cs[5] = {row, col, world, zcomm, all};
+            wd->abort_comms = [cs] {
+                for (ncclComm_t cm : cs)
+                    if (cm) ncclCommAbort(cm);
+            };
+            wd->async_error = [cs]() -> std::string {
+                static const char *names[5] = {"row", "column", "layer", "z", "world"};
+                for (int i = 0; i < 5; ++i) {
+                    ncclResult_t r = ncclSuccess;
+                    if (!cs[i] || ncclCommGetAsyncError(cs[i], &r) != ncclSuccess) continue;
+                    if (r != ncclSuccess && r != ncclInProgress)
+                        return std::string(names[i]) + " communicator: " + ncclGetErrorString(r);
+                }
+                return "";
+            };
+        }
+        return wd.get();
+    }
 };
 
 namespace slu {
@@ -142,6 +179,9 @@ struct Xport {
     vector<Op> ops;
     vector<char> hbuf;
     double sent = 0, recvd = 0; // bytes this rank moved (RCCL sections)
+    // what the next flush() is, for the watchdog's diagnostics
+    const char *phase = "plan-time exchange";
+    int level = -1;
     int gsize(int g) const {
         return g == G_WORLD ? c->nprow * c->npcol : g == G_ROW ? c->npcol : g == G_COL ? c->nprow : c->npdep;
     }
@@ -228,11 +268,71 @@ struct Xport {
                                   hipMemcpyHostToDevice, s));
         HIPCHK(hipStreamSynchronize(s));
     }
+    // this rank's part of the queued group, for the watchdog
+    std::string describe() const {
+        static const char *gn[4] = {"layer", "row", "column", "z"};
+        auto world_of = [&](int g, int m) {
+            return g == G_WORLD ? m : g == G_ROW ? c->myrow * c->npcol + m
+                                   : g == G_COL ? m * c->npcol + c->mycol : c->iam;
+        };
+        std::string s = phase;
+        if (level >= 0) s += " of level " + std::to_string(level);
+        int shown = 0, more = 0;
+        double sb = 0, rb = 0;
+        std::string lst;
+        auto add = [&](bool send, int g, int m, size_t bytes) {
+            (send ? sb : rb) += (double)bytes;
+            if (shown == 12) {
+                ++more;
+                return;
+            }
+            char b[160];
+            if (g == G_Z)
+                snprintf(b, sizeof b, "%s layer %d: %zu bytes", send ? "send to" : "receive from", m, bytes);
+            else
+                snprintf(b, sizeof b, "%s %s peer %d (rank %d): %zu bytes", send ? "send to" : "receive from",
+                         gn[g], m, world_of(g, m), bytes);
+            lst += (shown++ ? "; " : "") + std::string(b);
+        };
+        for (const Op &o : ops) {
+            const int me = grank(o.g), P = gsize(o.g);
+            if (me == o.root) {
+                for (int m = 0; m < P; ++m)
+                    if (m != me && (o.mask >> m & 1)) add(true, o.g, m, o.bytes);
+            } else if (o.mask >> me & 1) {
+                add(false, o.g, o.root, o.bytes);
+            }
+        }
+        char b[160];
+        snprintf(b, sizeof b, " (%zu ops; this rank sends %.0f and receives %.0f bytes): ", ops.size(), sb, rb);
+        s += b + lst;
+        if (more) s += "; ... " + std::to_string(more) + " more";
+        return s;
+    }
     void flush() {
         if (ops.empty()) return;
-        if (c->host_p2p) {
-            flush_p2p();
-        } else if (c->host_fn) {
+        Watchdog *wd = c->watchdog();
+        if (c->host_p2p || c->host_fn) {
+            // host transports block in the callback: the record is open for its duration
+            const uint64_t id = wd ? wd->open(describe(), nullptr) : 0;
+            if (c->host_p2p) flush_host_p2p();
+            else flush_host_bcast();
+            if (wd) wd->close(id);
+            ops.clear();
+            return;
+        }
+        flush_rccl();
+        if (wd) {
+            hipEvent_t e;
+            HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            HIPCHK(hipEventRecord(e, s));
+            wd->open(describe(), e);
+        }
+        ops.clear();
+    }
+    void flush_host_p2p() { flush_p2p(); }
+    void flush_host_bcast() {
+        {
             HIPCHK(hipStreamSynchronize(s));
             for (auto &o : ops) {
                 hbuf.resize(o.bytes);
@@ -255,7 +355,10 @@ struct Xport {
                     HIPCHK(hipStreamSynchronize(s));
                 }
             }
-        } else {
+        }
+    }
+    void flush_rccl() {
+        {
             // bcast ops as ncclBroadcast; sections as direct sends from the
             // root to each member that needs them (xGMI is point to point:
             // a root's sends to its row / column peers use distinct links)
@@ -277,7 +380,6 @@ struct Xport {
             }
             NCCLCHK(ncclGroupEnd());
         }
-        ops.clear();
     }
     // plan-time all-to-all of variable-length int64 blobs in the world
     // group: out[q] goes to rank q, the result's [p] came from rank p.  Sizes
@@ -790,7 +892,11 @@ struct Plan : PlanBase {
                               sc.off >= 0 ? arena + (size_t)sc.off * sizeof(T) : nullptr,
                               (size_t)sc.cnt * sizeof(T));
                 }
+                X.phase = ph ? "L/U panel exchange (replay)" : "diagonal-package exchange (replay)";
+                X.level = (int)L;
                 X.flush();
+                X.phase = "plan-time exchange";
+                X.level = -1;
                 for (int i = off; i < off + cnt; ++i) {
                     const Sec &sc = secs[i];
                     const int me = sc.g == G_ROW ? mycol : myrow;
@@ -815,7 +921,11 @@ struct Plan : PlanBase {
             if (!recv)
                 for (size_t b = 0; b < bytes; ++b) zb[b] = pat(1000000 + zp, 0, root, iam, b);
             X.section(G_Z, root, 1u << (recv ? zl : peer), zb.data(), bytes);
+            X.phase = "3D ancestor reduction (replay)";
+            X.level = zp;
             X.flush();
+            X.phase = "plan-time exchange";
+            X.level = -1;
             if (recv && bytes) {
                 for (size_t b = 0; b < bytes; ++b)
                     SLU_REQUIRE(zb[b] == pat(1000000 + zp, 0, root, iam, b),
@@ -1451,7 +1561,11 @@ struct Plan : PlanBase {
         X.s = st;
         if (!zsolo) {
             X.section(G_Z, recv ? peer : zl, 1u << (recv ? zl : peer), d_zbuf.p, (size_t)cnt * sizeof(T));
+            X.phase = "3D ancestor reduction";
+            X.level = p;
             X.flush();
+            X.phase = "plan-time exchange";
+            X.level = -1;
         }
         zbytes += (double)cnt * sizeof(T);
         if (recv) launch_zranges(a, b, ZR_ADD, st);
@@ -1491,7 +1605,11 @@ struct Plan : PlanBase {
                                    (int)ZR_PACK);
             X.s = st;
             X.section(G_Z, sender, 1u << (recv ? zl : peer), buf.p, (size_t)bo * sizeof(T));
+            X.phase = "3D gather to layer 0";
+            X.level = il;
             X.flush();
+            X.phase = "plan-time exchange";
+            X.level = -1;
             if (recv && nr)
                 hipLaunchKernelGGL(k_zranges<T>, dim3(nr), dim3(256), 0, st, dr.p, d_L.p, d_U.p, buf.p,
                                    (int)ZR_COPY);
@@ -2674,14 +2792,18 @@ struct Plan : PlanBase {
                            d_ucol_voff.p, d_ucol_fst.p);
     }
 
-    void issue(const vector<Sec> &secs, int off, int n_) {
+    void issue(const vector<Sec> &secs, int off, int n_, const char *phase, int level) {
         for (int i = off; i < off + n_; ++i) {
             const Sec &s = secs[i];
             T *base = s.arena ? d_pan.p : d_dpk.p;
             X.section(s.g, s.root, s.mask, s.off >= 0 ? base + s.off : nullptr,
                       (size_t)s.cnt * sizeof(T));
         }
+        X.phase = phase;
+        X.level = level;
         X.flush();
+        X.phase = "plan-time exchange";
+        X.level = -1;
     }
 
     // ------------------------------------------------------- factor
@@ -2786,7 +2908,7 @@ struct Plan : PlanBase {
                     if (R.dc_n)
                         hipLaunchKernelGGL(k_copy<T>, dim3(R.dc_n), dim3(256), 0, P,
                                            d_dcopy.p + R.dc_off);
-                    issue(dsecs, R.ds_off, R.ds_n);
+                    issue(dsecs, R.ds_off, R.ds_n, "diagonal-package exchange", (int)L);
                 });
             if (R.lf_n || R.uf_n) span(1, P, [&] { launch_trsm_fast(R, P); });
             if (R.tl_n || R.tu_n)
@@ -2803,7 +2925,7 @@ struct Plan : PlanBase {
                     if (R.pc_n)
                         hipLaunchKernelGGL(k_copy<T>, dim3(R.pc_n), dim3(256), 0, P,
                                            d_pcopy.p + R.pc_off);
-                    issue(psecs, R.ps_off, R.ps_n);
+                    issue(psecs, R.ps_off, R.ps_n, "L/U panel exchange", (int)L);
                 });
             HIPCHK(hipEventRecord(ev_pan[L], P));
             // critical tiles of L on the panel stream, after the rest of L-1
@@ -3235,7 +3357,11 @@ struct Plan : PlanBase {
             T *buf = mycol == r.c ? xv + xsup[r.k] : (mycol == own_c ? d_sv_slot.p + r.slot : nullptr);
             X.section(G_ROW, r.c, 1u << own_c, buf, (size_t)W(r.k) * sizeof(T));
         }
+        X.phase = "solve: partial sums to the diagonal owners";
+        X.level = L;
         X.flush();
+        X.phase = "plan-time exchange";
+        X.level = -1;
         const int na = sv_add_off[L + 1] - sv_add_off[L];
         if (na)
             hipLaunchKernelGGL(k_sv_add<T>, dim3(na), dim3(256), 0, stream, d_sv_add.p + sv_add_off[L],
@@ -4403,7 +4529,10 @@ struct GridAmalgPlan : PlanBase {
                 else if (me == q) buf = d_recv.p + r.roff[p];
                 X.section(G_WORLD, root, 1u << dest, buf, (size_t)cnt[p][q] * sizeof(T));
             }
+        X.phase = forward ? "grid amalgamation relayout (values to the coarse owners)"
+                          : "grid amalgamation relayout (factors back to the caller layout)";
         X.flush();
+        X.phase = "plan-time exchange";
     }
 
     void expand() { // caller layout (d_oL / d_oU) -> coarse
@@ -4745,6 +4874,7 @@ int slu_comm_size(const slu_comm *c, int group) {
 
 void slu_comm_destroy(slu_comm *c) {
     if (!c) return;
+    c->wd.reset(); // (its thread polls the communicators)
     if (c->row) ncclCommDestroy(c->row);
     if (c->col) ncclCommDestroy(c->col);
     if (c->world) ncclCommDestroy(c->world);

@@ -37,6 +37,15 @@ class GlooGrid:
         self.base = self.layer * P
         self.myrow, self.mycol = r2 // pc, r2 % pc
         self.row = self.col = None
+        # test hook: SLU_TEST_DROP_SEND="r:k" makes global rank r skip its
+        # k-th send (counted over the whole run) and every later send to the
+        # same peer (sections pair in order: with only the one dropped, the
+        # next message would land in its place) -- the receiver must then end
+        # through the engine's exchange watchdog, not hang
+        self.sends = []  # (peer global rank, bytes) of every send of this rank
+        drop = os.environ.get("SLU_TEST_DROP_SEND")
+        self.drop = int(drop.split(":")[1]) if drop and int(drop.split(":")[0]) == rank else -1
+        self.dropped_peer = None
         if pz == 1:  # (the 3D runs use the point-to-point transport only)
             rows = [dist.new_group([r * pc + c for c in range(pc)]) for r in range(pr)]
             cols = [dist.new_group([r * pc + c for r in range(pr)]) for c in range(pc)]
@@ -68,6 +77,12 @@ class GlooGrid:
             other = self.global_root(group, peer)
             if other == self.rank:
                 raise RuntimeError(f"p2p op with myself (group {group}, peer {peer})")
+            if send:
+                self.sends.append((other, arr.nbytes))
+                if len(self.sends) - 1 == self.drop:
+                    self.dropped_peer = other
+                if other == self.dropped_peer:
+                    continue
             works.append(self.dist.isend(t, other) if send else self.dist.irecv(t, other))
         for w in works:
             w.wait()
@@ -120,6 +135,7 @@ def _worker(rank, world, port, recipe, out_dir, device, fill=False, solve=False,
             comm = Comm.host_p2p(pr, pc, rank, -1, gg.p2p)
             p = Plan(lu, comm=comm, schedule_only=True)
             res["nsec"], res["nbytes"] = p.check_exchange()
+            res["sends"] = np.array(gg.sends, dtype=np.int64).reshape(-1, 2)
             st = p.stats()
             res["nlevels"] = st["nlevels"]
             res["nsupers"], res["nsupers_in"] = st["nsupers"], st["nsupers_in"]

@@ -286,3 +286,43 @@ def test_factored_solve_after_eviction_with_host_factors():
     rc, errs, out = _evict({"SUPERLU_MI355X_HOST_FACTORS": "1"})
     assert rc == 0, out[-3000:]
     assert sorted(errs) == [1, 2, 3] and max(errs.values()) < 1e-10, out[-3000:]
+
+
+# The grid life cycle twice in one process (oracle/gen/regrid_main.c): each
+# round gridinit -> pdgssvx (DOFACT) -> pdgssvx (SamePattern_SameRowPerm, a
+# plan-cache hit) -> gridexit.  gridexit destroys the engine communicators,
+# and the cached plan built on them goes with them: the
+# next round's first call builds a new plan even when MPI reuses the
+# communicator handle and malloc the LUstruct addresses.
+def _regrid(nprocs, pr, pc):
+    env = dict(os.environ)
+    env.update({"OMP_NUM_THREADS": "1", "MKL_NUM_THREADS": "1", "MKL_THREADING_LAYER": "SEQUENTIAL",
+                "HSA_ENABLE_IPC_MODE_LEGACY": "0", "SUPERLU_MI355X_TIMING": "1"})
+    cmd = [MPIEXEC, "-n", str(nprocs), os.path.join(REF, "regrid"), os.path.join(MAT, "big.rua"),
+           str(pr), str(pc)]
+    r = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=300)
+    return r.returncode, r.stdout + r.stderr
+
+
+@pytest.mark.skipif(not _have("regrid"), reason="grid life-cycle driver not built")
+def test_regrid_driver_binds_our_pdgstrf():
+    dyn, und, _ = _binding("regrid")
+    assert "libslu_mi355x.so" in dyn and "pdgstrf" in und
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pr,pc", [(1, 1), (2, 2)])
+@pytest.mark.skipif(not _have("regrid"), reason="grid life-cycle driver not built")
+def test_grid_exit_evicts_the_cached_plan(pr, pc):
+    rc, out = _regrid(pr * pc, pr, pc)
+    assert rc == 0, out[-3000:]
+    res = re.findall(r"round (\d) call (\d): info (\d+) err ([0-9.eE+-]+)", out)
+    assert len(res) == 4, out[-3000:]
+    for _, _, info, err in res:
+        assert int(info) == 0 and float(err) < 1e-10, out[-3000:]
+    # rank 0's plan per call: built, reused, then (new grid) built, reused
+    plans = re.findall(r"\[pdgstrf rank 0\] digest [0-9.]+ ms, plan (built|reused)", out)
+    if pr * pc > 1:
+        assert plans == ["built", "reused", "built", "reused"], out[-3000:]
+    else:  # 1x1: the transport is per device and outlives the grid: the plan may stay
+        assert plans[0] == "built" and plans[1] == plans[3] == "reused", out[-3000:]

@@ -161,3 +161,37 @@ def test_grid_amalgamation_fingerprints_match_reference_pdgstrf(grid, tmp_path):
                                    want_blocksums=True, timeout=600)
     c = pyoracle.compare_blocksums(mine, st["blocksums"])
     assert c["match"] and c["rel_err"] <= 1e-12, c
+
+
+def test_watchdog_reports_a_dropped_section_cpu(tmp_path, monkeypatch, capfd):
+    """the exchange watchdog (csrc/watchdog.h).  A first
+    schedule-only run over the point-to-point transport records every send of
+    rank 0; the second run drops rank 0's last section of the replay (and what follows it to that peer)
+    of factor()'s last exchanges.  The receiver's watchdog must fire within
+    its bound (SLU_WATCHDOG_S = 3) with the phase, the level and the pending
+    section (peer, bytes), and end that rank with exit status 86 instead of a
+    hang."""
+    (tmp_path / "a").mkdir()
+    out = run_grid("refdump:big_2x2_d", 2, 2, tmp_path / "a", device=None, transport="schedule",
+                   timeout=120)
+    sends = out[0]["sends"]
+    # the last section of the replay (the 8-byte all-gathers after it are the
+    # plan's closing statistics)
+    k = max(i for i in range(len(sends)) if sends[i][1] > 8)
+    peer, nbytes = (int(x) for x in sends[k])
+    (tmp_path / "b").mkdir()
+    monkeypatch.setenv("SLU_TEST_DROP_SEND", f"0:{k}")
+    monkeypatch.setenv("SLU_WATCHDOG_S", "3")
+    capfd.readouterr()
+    with pytest.raises(RuntimeError) as ei:
+        run_grid("refdump:big_2x2_d", 2, 2, tmp_path / "b", device=None, transport="schedule",
+                 timeout=90)
+    msg = str(ei.value)
+    assert f"rank {peer}: exit 86" in msg, msg
+    err = capfd.readouterr().err
+    line = [ln for ln in err.splitlines() if ln.startswith(f"[slu watchdog] rank {peer} ")
+            and "oldest open exchange" in ln]
+    assert line, err[-4000:]
+    assert "exchange (replay) of level" in line[0], line[0]
+    assert f"receive from" in line[0] and f"(rank 0): {nbytes} bytes" in line[0], line[0]
+    assert "has not completed after" in err
