@@ -31,7 +31,16 @@ int main(int argc, char **argv) {
         if (!fp) ABORT("cannot open the matrix file");
         dcreate_matrix(&A, 1, &b, &ldb, &xtrue, &ldx, fp, &grid);
         fclose(fp);
-        const int m_loc = ((NRformat_loc *)A.Store)->m_loc;
+        /* pdgssvx scales and permutes A in place: keep its arrays for the
+         * second call, which rebuilds A from them (EXAMPLE/pddrive3.c) */
+        NRformat_loc *As = (NRformat_loc *)A.Store;
+        const int m = A.nrow, n = A.ncol, m_loc = As->m_loc, fst_row = As->fst_row;
+        const int_t nnz_loc = As->nnz_loc;
+        double *nzval1 = doubleMalloc_dist(nnz_loc);
+        int_t *colind1 = intMalloc_dist(nnz_loc), *rowptr1 = intMalloc_dist(m_loc + 1);
+        memcpy(nzval1, As->nzval, sizeof(double) * nnz_loc);
+        memcpy(colind1, As->colind, sizeof(int_t) * nnz_loc);
+        memcpy(rowptr1, As->rowptr, sizeof(int_t) * (m_loc + 1));
         double *b0 = doubleMalloc_dist(ldb);
         memcpy(b0, b, sizeof(double) * ldb);
         superlu_dist_options_t opt;
@@ -63,13 +72,20 @@ int main(int argc, char **argv) {
                 printf("round %d call %d: info %d err %.3e\n", round, call, info, g[0] / g[1]);
                 fflush(stdout);
             }
-            opt.Fact = SamePattern_SameRowPerm;
+            if (call == 0) { /* the same pattern and values, from the saved arrays */
+                opt.Fact = SamePattern_SameRowPerm;
+                Destroy_CompRowLoc_Matrix_dist(&A);
+                dZeroLblocks(grid.iam, n, &grid, &lu);
+                dZeroUblocks(grid.iam, n, &grid, &lu);
+                dCreate_CompRowLoc_Matrix_dist(&A, m, n, nnz_loc, m_loc, fst_row, nzval1, colind1,
+                                               rowptr1, SLU_NR_loc, SLU_D, SLU_GE);
+            }
         }
         dSolveFinalize(&opt, &solve);
         dDestroy_LU(A.ncol, &grid, &lu);
         dLUstructFree(&lu);
         dScalePermstructFree(&sp);
-        Destroy_CompRowLoc_Matrix_dist(&A);
+        Destroy_CompRowLoc_Matrix_dist(&A); /* (frees nzval1 / colind1 / rowptr1) */
         SUPERLU_FREE(b);
         SUPERLU_FREE(b0);
         SUPERLU_FREE(xtrue);

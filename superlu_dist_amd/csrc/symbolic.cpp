@@ -370,22 +370,319 @@ struct Walker {
         }
     }
 
+    // ---------------------------------------------------------------------
+    // The same state machine with the current supernode's last list kept
+    // virtual (the default; SLU_SYMB_CLASSIC=1 runs column() above).
+    //
+    // Column j's search reaches the supernode it may extend through that
+    // supernode's representative j - 1, whose list is L(:, j-1), and appends
+    // every row >= j of it that is not yet marked: at 100^3 that re-scan is
+    // 95 % of the search (1.52e9 of 1.59e9 entries, each column of a wide
+    // supernode copying the whole front).  Here L(:, j-1) lives in a linked
+    // list (lnx / lpv) with membership stamps (cur[r] == its supernode), and
+    // entering j - 1 only records where its rows go: L(:, j) is
+    //   P ++ (L(:, j-1) minus {j-1} minus P, in its order) ++ Q
+    // with P / Q the rows found before / after (Q is empty when j joins).  A
+    // column that joins moves P to the front of the linked list and drops
+    // j - 1; one that starts a new supernode writes the old supernode's last
+    // list and its own list out in full, where the classic compaction puts
+    // them (first list, last list; SRC/symbfact.c:633-671).  Every array and
+    // the returned lsub size are the classic ones (tests/test_symbolic.py).
+    vector<T> cur, lnx, lpv, fl, pos;
+    vector<T> repc; // representative of each row's finished supernode (NONE: the current one)
+    T lhead = (T)NONE, ltail = (T)NONE, cur_s = (T)-2; // cur_s: supernode of the list
+    I cur_fs = 0, last_len = 0, tail_sum = 0;          // tail_sum: classic sizes past the first list
+    I lbelow = 0; // rows of the list below the next column (1; a relaxed copy: its width)
+    T lmin = 0;   // smallest row of the list (the representative's first nonzero row bound)
+
+    void vinit() {
+        cur.assign(m, (T)-3);
+        fl.assign(m, (T)-3);
+        lnx.assign(m, (T)NONE);
+        lpv.assign(m, (T)NONE);
+        pos.assign(m, 0);
+        repc.assign(m, (T)NONE);
+    }
+    void set_rep(I fs, I last) {
+        for (I c = fs; c <= last; ++c) repc[c] = (T)last;
+    }
+    void l_unlink(T c) {
+        const T a = lpv[c], b = lnx[c];
+        if (a != (T)NONE) lnx[a] = b;
+        else lhead = b;
+        if (b != (T)NONE) lpv[b] = a;
+        else ltail = a;
+    }
+    void l_push_front(T c) {
+        lpv[c] = (T)NONE;
+        lnx[c] = lhead;
+        if (lhead != (T)NONE) lpv[lhead] = c;
+        else ltail = c;
+        lhead = c;
+    }
+    void l_build(const T *v, I cnt) {
+        lhead = ltail = (T)NONE;
+        for (I i = cnt - 1; i >= 0; --i) l_push_front(v[i]);
+    }
+    // the supernode starting at fs, whose search representative is rep:
+    // its list (the rep's) into the linked list, its first list's positions
+    void start_supernode(I fs, I rep) {
+        const T s = supno[fs];
+        const I a = xlsub[rep], b = xprune[rep];
+        l_build(lsub.data() + a, b - a);
+        for (I i = a; i < b; ++i) cur[lsub[i]] = s;
+        const I fa = xlsub[fs], fb = xlsub[fs + 1];
+        for (I i = fa; i < fb; ++i) {
+            fl[lsub[i]] = s;
+            pos[lsub[i]] = i - fa;
+        }
+        cur_s = s;
+        cur_fs = fs;
+        last_len = b - a;
+        tail_sum = rep > fs ? b - a : 0;
+        lbelow = 0;
+        lmin = (T)m;
+        for (I i = a; i < b; ++i) {
+            if (lsub[i] <= (T)rep) ++lbelow;
+            lmin = std::min(lmin, lsub[i]);
+        }
+    }
+    // write the linked list (L(:, j-1)) at `at`, skipping rows below `below`
+    // and rows marked `mark`; returns the count written
+    I l_write(I at, T below, T mark) {
+        I o = at;
+        for (T c = lhead; c != (T)NONE; c = lnx[c])
+            if (c >= below && marker[c] != mark) lsub[o++] = c;
+        return o - at;
+    }
+
+    I column_v(I j) {
+        const T tj = (T)j;
+        I ns = supno[j];
+        const bool prev = j > 0; // a current supernode (columns cur_fs .. j-1) exists
+        const T sc = prev ? cur_s : (T)-2;
+        const I start = !prev ? xlsub[j] : (j - 1 > cur_fs ? xlsub[cur_fs + 1] + last_len : xlsub[cur_fs + 1]);
+        I nextl = start, nseg = 0, split = -1, p_in = 0;
+        bool subset = true;
+        reserve(start, m + 1);
+        T *const L = lsub.data(), *const mk = marker.data(), *const rf = repfnz.data(),
+                 *const par = parent.data(), *const sg = segrep.data(), *const cu = cur.data();
+        const T *const rc = repc.data();
+        const I *const xl = xlsub.data(), *const xp = xprune.data();
+        I *const xo = xplore.data();
+        const T vrep = prev ? (T)(j - 1) : (T)NONE; // the representative kept virtual
+        // entering the virtual representative: its rows >= j count as found
+        // from here on; its rows < j (the representative's own, all of a
+        // relaxed supernode's) would each lower repfnz to their index
+        auto enter_virtual = [&]() {
+            split = nextl - start;
+            if (lmin < rf[vrep]) rf[vrep] = lmin;
+        };
+        for (I p = cb[j]; p < ce[j]; ++p) {
+            const T r = ri[p], km = mk[r];
+            if (km == tj) continue;
+            if (r >= tj) {
+                if (split >= 0 && cu[r] == sc) continue; // in the virtual part
+                mk[r] = tj;
+                L[nextl++] = r;
+                if (cu[r] == sc) ++p_in;
+                else subset = false;
+                continue;
+            }
+            mk[r] = tj;
+            T rep = rc[r];
+            if (rep == (T)NONE) rep = vrep;
+            if (rf[rep] != (T)NONE) {
+                if (r < rf[rep]) rf[rep] = r;
+                continue;
+            }
+            par[rep] = (T)NONE;
+            rf[rep] = r;
+            I x = xl[rep], xe = xp[rep];
+            if (rep == vrep) {
+                enter_virtual();
+                x = xe = 0;
+            }
+            for (;;) {
+                while (x < xe) {
+                    const T c = L[x++], cm = mk[c];
+                    if (cm == tj) continue;
+                    if (c >= tj) {
+                        if (split >= 0 && cu[c] == sc) continue;
+                        mk[c] = tj;
+                        L[nextl++] = c;
+                        if (cu[c] == sc) ++p_in;
+                        else subset = false;
+                        continue;
+                    }
+                    mk[c] = tj;
+                    T crep = rc[c];
+                    if (crep == (T)NONE) crep = vrep;
+                    if (rf[crep] != (T)NONE) {
+                        if (c < rf[crep]) rf[crep] = c;
+                        continue;
+                    }
+                    xo[rep] = x; // descend
+                    par[crep] = rep;
+                    rep = crep;
+                    rf[rep] = c;
+                    x = xl[rep];
+                    xe = xp[rep];
+                    if (rep == vrep) {
+                        enter_virtual();
+                        x = xe = 0;
+                    }
+                }
+                sg[nseg++] = rep; // finished: back to the parent
+                const T up = par[rep];
+                if (up == (T)NONE) break;
+                rep = up;
+                x = xo[rep];
+                xe = xp[rep];
+            }
+        }
+        const I nexp = nextl - start;                                  // P and Q
+        const I nvirt = split >= 0 ? last_len - lbelow - p_in : 0;     // the virtual part
+        const I len = nexp + nvirt;                                    // |L(:, j)|
+        if (j == 0) {
+            ns = supno[0] = 0;
+        } else {
+            bool js = subset;
+            if (len != last_len - 1) js = false;
+            if (j - cur_fs >= maxsuper) js = false;
+            if (js) {
+                // L(:, j) = P ++ (L(:, j-1) minus j-1 minus P): P to the front
+                if (split >= 0) {
+                    for (I i = start + nexp - 1; i >= start; --i) {
+                        l_unlink(L[i]);
+                        l_push_front(L[i]);
+                    }
+                    if (lbelow == 1) {
+                        l_unlink(vrep);
+                    } else {
+                        for (T c = lhead; c != (T)NONE;) {
+                            const T nx = lnx[c];
+                            if (c < tj) l_unlink(c);
+                            c = nx;
+                        }
+                    }
+                } else {
+                    l_build(L + start, nexp);
+                }
+                lbelow = 1; // (row j of L(:, j))
+                lmin = tj;
+                last_len = len;
+                tail_sum += len;
+                xsup[ns + 1] = (T)(j + 1);
+                supno[j + 1] = (T)ns;
+                xlsub[j + 1] = xlsub[cur_fs + 1] + len;
+                xprune[j] = xlsub[j + 1];
+                return nseg;
+            }
+            // the current supernode ends at j - 1: its last list where the
+            // classic compaction leaves it
+            if (j - 1 > cur_fs) {
+                const I to = xlsub[cur_fs + 1];
+                l_write(to, (T)0, (T)-4); // (every row: no mark equals -4)
+                xlsub[j - 1] = to;
+                xprune[j - 1] = to + last_len;
+            }
+            set_rep(cur_fs, j - 1);
+            // L(:, j) in full: P, the virtual part, then Q
+            if (split >= 0) {
+                const I nq = nexp - split;
+                if (nq && nvirt) memmove(L + start + split + nvirt, L + start + split, nq * sizeof(T));
+                l_write(start + split, tj, tj);
+            }
+            ++ns;
+            supno[j] = (T)ns;
+        }
+        xsup[ns + 1] = (T)(j + 1);
+        supno[j + 1] = (T)ns;
+        xlsub[j] = start;
+        xprune[j] = start + len;
+        xlsub[j + 1] = start + len;
+        return nseg;
+    }
+
+    // pivot of a column that extends the current supernode: row j to
+    // position j - fsupc of the first list, by the kept positions
+    void pivot_v(I j) {
+        if (j == cur_fs || supno[j] != cur_s) return pivot(j);
+        const I fs = cur_fs, lp = xlsub[fs], nr = xlsub[fs + 1] - lp, d0 = j - fs;
+        const T tj = (T)j;
+        if (fl[tj] != cur_s || pos[tj] < d0 || pos[tj] >= nr)
+            throw Error("symbfact: zero diagonal at column " + std::to_string(j));
+        const I d = pos[tj];
+        if (d != d0) {
+            const T o = lsub[lp + d0];
+            std::swap(lsub[lp + d], lsub[lp + d0]);
+            pos[o] = d;
+            pos[tj] = d0;
+        }
+    }
+
     // columns [a, b) with the relaxed supernode ends `rend`
     void run(I a, I b, const I *rend) {
+        const char *cl = getenv("SLU_SYMB_CLASSIC");
+        if (cl && atoi(cl) == 1) {
+            for (I j = a; j < b;) {
+                if (rend[j] != NONE) {
+                    const I k = rend[j];
+                    relaxed(j, k);
+                    for (I i = j; i <= k; ++i) pivot(i);
+                    j = k + 1;
+                } else {
+                    const I nseg = column(j);
+                    set_usub(j, nseg);
+                    pivot(j);
+                    prune(j, nseg);
+                    for (I s = 0; s < nseg; ++s) repfnz[segrep[s]] = (T)NONE;
+                    ++j;
+                }
+            }
+            return;
+        }
+        vinit();
         for (I j = a; j < b;) {
             if (rend[j] != NONE) {
                 const I k = rend[j];
+                if (j > 0) finish_current(j);
                 relaxed(j, k);
                 for (I i = j; i <= k; ++i) pivot(i);
+                start_supernode(j, k);
                 j = k + 1;
             } else {
-                const I nseg = column(j);
+                const I nseg = column_v(j);
                 set_usub(j, nseg);
-                pivot(j);
+                const bool fresh = supno[j] != cur_s || j == 0;
+                if (fresh) pivot(j);
+                else pivot_v(j);
                 prune(j, nseg);
                 for (I s = 0; s < nseg; ++s) repfnz[segrep[s]] = (T)NONE;
+                if (fresh) start_supernode(j, j);
                 ++j;
             }
+        }
+        if (b > a) finish_current(b);
+    }
+
+    // before a relaxed supernode at column j (or at the end, j = b): the
+    // current supernode's last list written out; at the end the classic
+    // layout keeps every column list of the last supernode uncompacted, so
+    // xlsub[b] is its classic total
+    void finish_current(I j) {
+        if (cur_s == supno[j - 1]) set_rep(cur_fs, j - 1);
+        if (j - 1 > cur_fs && cur_s == supno[j - 1]) {
+            // the classic layout: compaction happens only when a searched
+            // column does not join, so here every column list past the first
+            // stays in place and the last one ends at xlsub[fs+1] + tail_sum
+            const I end = xlsub[cur_fs + 1] + tail_sum, at = end - last_len;
+            reserve(at, last_len);
+            l_write(at, (T)0, (T)-4);
+            xlsub[j - 1] = at;
+            xprune[j - 1] = end;
+            xlsub[j] = end;
         }
     }
 };

@@ -133,3 +133,69 @@ def test_dropin_symbols_with_reference_types():
     for p in (gp.xsup, gp.supno, gf.lsub, gf.xlsub, gf.usub, gf.xusub, S_.colbeg, S_.colend):
         libc.free(C.cast(p, C.c_void_p))
     libc.free(C.c_void_p(AC.Store))
+
+
+def _classic_vs_default(n, colptr, rowind, perm, colperm, relax, maxsup, monkeypatch):
+    co = S.sp_colorder(n, n, colptr, rowind, perm, colperm)
+    ri = S.relabel_rows(rowind, co.perm_c)
+    monkeypatch.setenv("SLU_SYMB_CLASSIC", "1")
+    a = S.symbfact(n, n, co.colbeg, co.colend, ri, co.etree, relax, maxsup)
+    monkeypatch.delenv("SLU_SYMB_CLASSIC")
+    b = S.symbfact(n, n, co.colbeg, co.colend, ri, co.etree, relax, maxsup)
+    for f in ("xsup", "supno", "xlsub", "lsub", "xusub", "usub"):
+        np.testing.assert_array_equal(getattr(a, f), getattr(b, f), err_msg=f)
+    assert (a.ret, a.nnzL, a.nnzU, a.nnzLU) == (b.ret, b.nnzL, b.nnzU, b.nnzLU)
+    return a
+
+
+@pytest.mark.parametrize("seed", range(6))
+@pytest.mark.parametrize("relax,maxsup", [(1, 3), (4, 10), (8, 20), (60, 256), (2, 512)])
+def test_symbfact_virtual_last_list_equals_classic(seed, relax, maxsup, monkeypatch):
+    """The default walker keeps the current supernode's last list virtual
+    (csrc/symbolic.cpp, column_v); SLU_SYMB_CLASSIC=1 runs the literal
+    restatement of SRC/symbfact.c.  Random unsymmetric patterns (rows in
+    random order within each column) with several relax / maxsup: every
+    array and the returned lsub size are the same."""
+    rng = np.random.default_rng(seed)
+    n = int(rng.integers(50, 400))
+    cols = []
+    for c in range(n):
+        k = int(rng.integers(1, 6))
+        rows = set(rng.integers(0, n, k).tolist()) | {c}
+        if c > 0 and rng.random() < 0.7:
+            rows.add(c - 1)  # chains: supernodes of several columns
+        r = list(rows)
+        rng.shuffle(r)
+        cols.append(r)
+    colptr = np.zeros(n + 1, np.int64)
+    colptr[1:] = np.cumsum([len(c) for c in cols])
+    rowind = np.array([r for c in cols for r in c], np.int64)
+    perm = rng.permutation(n).astype(np.int64)
+    for colperm in (S.MMD_AT_PLUS_A, S.MMD_ATA):
+        _classic_vs_default(n, colptr, rowind, perm, colperm, relax, maxsup, monkeypatch)
+
+
+def test_symbfact_virtual_last_list_3d_stencil(monkeypatch):
+    """Wide fundamental supernodes (a 3D 7-point grid in natural order,
+    maxsup 256 and 16): the case the virtual list is for."""
+    k = 14
+    n = k ** 3
+    idx = np.arange(n).reshape(k, k, k)
+    cols = [[] for _ in range(n)]
+    for d in ((0, 0, 0), (1, 0, 0), (-1, 0, 0), (0, 1, 0), (0, -1, 0), (0, 0, 1), (0, 0, -1)):
+        a = np.roll(idx, d, axis=(0, 1, 2))
+        ok = np.ones((k, k, k), bool)
+        for ax in range(3):
+            if d[ax] == 1:
+                ok[(slice(None),) * ax + (0,)] = False
+            elif d[ax] == -1:
+                ok[(slice(None),) * ax + (k - 1,)] = False
+        for c, r in zip(idx[ok].ravel(), a[ok].ravel()):
+            cols[c].append(int(r))
+    colptr = np.zeros(n + 1, np.int64)
+    colptr[1:] = np.cumsum([len(c) for c in cols])
+    rowind = np.array([r for c in cols for r in c], np.int64)
+    for relax, maxsup in ((60, 256), (4, 16)):
+        s = _classic_vs_default(n, colptr, rowind, np.arange(n, dtype=np.int64), S.NATURAL, relax,
+                                maxsup, monkeypatch)
+        assert s.nsupers < n
