@@ -228,6 +228,78 @@ def abi_leg(lu, anorm, factor_ms, fingerprint=None):
                     "L/U values (hostio.h); D2H rides under the factorization"}, sums
 
 
+def device_resident_child(nx):
+    """Child process of the N=1 bench (``--device-resident-child``): the
+    device-resident drop-in (libslu_mi355x_solve.so) as
+    pdgssvx drives it (SRC/pdgssvx.c:1146-1180 and its SOLVE phase) on the
+    headline workload: this library's pddistribute keeps A, pdgstrf fills the
+    factor storage on the device and leaves the factors in HBM, pdgstrs solves
+    on them.  Then the refactorization pddrive3.c does (Fact =
+    SamePattern_SameRowPerm: pddistribute refills the values, pdgstrf reuses
+    the cached plan).  Each call wall-clocked as pdgssvx's utime does.  A
+    fresh process, HIP initialised before the first call (reported apart)."""
+    import ctypes as C
+    from superlu_dist_amd import capi
+    from superlu_dist_amd import symbolic as SY
+    from superlu_dist_amd.frontend import STENCIL_3D7, Csc, nd_order
+    A = Csc.stencil(STENCIL_3D7, nx, nx, nx)
+    n = A.n
+    cp, ri, v = A.arrays()
+    t0 = time.perf_counter()
+    co = SY.sp_colorder(n, n, cp, ri, nd_order(nx, nx, nx), SY.MY_PERMC)
+    sb = SY.symbfact(n, n, co.colbeg, co.colend, SY.relabel_rows(ri, co.perm_c), co.etree, 60, 256)
+    t_symb = time.perf_counter() - t0
+    # the 7-point Laplacian is symmetric: A's CSR arrays are its CSC arrays;
+    # pdgssvx maps the column indices by perm_c before pddistribute
+    s = capi.DeviceResidentSystem(n, cp, co.perm_c[ri], v, co.perm_c, co.etree, sb.xsup, sb.supno,
+                                  sb.xlsub, sb.lsub, sb.xusub, sb.usub, one_norm(A))
+    xt = np.random.default_rng(3).standard_normal(n)
+    import scipy.sparse as sp
+    b = sp.csc_matrix((v, ri, cp), shape=(n, n)) @ xt
+    t0 = time.perf_counter()
+    hip = C.CDLL("libamdhip64.so")
+    hip.hipFree(None)
+    t_hip = time.perf_counter() - t0
+    rec = {"symbolic_s": round(t_symb, 2), "hip_init_ms": round(t_hip * 1e3, 1), "calls": []}
+    for i, fact in enumerate([0, capi.SAMEPATTERN_SAMEROWPERM, capi.SAMEPATTERN_SAMEROWPERM]):
+        t0 = time.perf_counter()
+        s.distribute(fact)
+        t1 = time.perf_counter()
+        rv, info, ops = s.factor()
+        t2 = time.perf_counter()
+        x = s.solve(b)
+        t3 = time.perf_counter()
+        assert rv == 0 and info == 0, (rv, info)
+        rec["calls"].append({"fact": ["DOFACT", "", "SamePattern_SameRowPerm"][fact],
+                             "distribute_ms": round((t1 - t0) * 1e3, 1),
+                             "utime_fact_ms": round((t2 - t1) * 1e3, 1),
+                             "solve_ms": round((t3 - t2) * 1e3, 1),
+                             "fwd_err": float(np.abs(x - xt).max() / np.abs(xt).max()),
+                             "ops_fact": ops})
+    c = rec["calls"]
+    rec.update({"utime_fact_ms_first_call": c[0]["utime_fact_ms"],
+                "utime_fact_ms_refactor": min(x["utime_fact_ms"] for x in c[1:]),
+                "solve_ms": min(x["solve_ms"] for x in c),
+                "note": "libslu_mi355x_solve.so: pddistribute keeps A, pdgstrf fills L/U on the "
+                        "device and keeps the factors in HBM, pdgstrs solves on them (1 rhs); "
+                        "refactor = Fact SamePattern_SameRowPerm (refill + cached plan)"})
+    print(json.dumps(rec), flush=True)
+
+
+def device_resident_leg(nx):
+    """Runs device_resident_child in a fresh process (its LUstruct and HBM
+    plan are freed with it); returns its record or an error note."""
+    try:
+        r = subprocess.run([sys.executable, os.path.abspath(__file__), "--device-resident-child",
+                            "--nx", str(nx)], capture_output=True, text=True, timeout=900)
+        line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+        if r.returncode != 0 or not line:
+            return {"error": f"exit {r.returncode}: {r.stderr[-1500:]}"}
+        return json.loads(line[-1])
+    except Exception as e:  # noqa: BLE001
+        return {"error": str(e)}
+
+
 def one_norm(A):
     """||A||_1 (max column sum of |a_ij|), the anorm pdgssvx passes to pdgstrf."""
     colptr, _, val = A.arrays()
@@ -376,6 +448,9 @@ def main():
                          "(0 skips it)")
     ap.add_argument("--rank-timeout", type=float, default=float(os.environ.get("SLU_BENCH_TIMEOUT_S", 1500)),
                     help="--gpus N without a launcher: seconds before the spawned ranks are killed")
+    ap.add_argument("--device-resident-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--no-device-resident", action="store_true",
+                    help="skip the device-resident drop-in leg (libslu_mi355x_solve.so)")
     ap.add_argument("--host-transport", action="store_true",
                     help="REHEARSAL ONLY: several ranks on one GPU through the host-staged "
                          "point-to-point test transport (the RCCL send / receive pairs over "
@@ -384,6 +459,9 @@ def main():
     W = WORKLOADS[args.workload]
     if args.nx is None:
         args.nx = W[8]
+    if args.device_resident_child:
+        device_resident_child(args.nx)
+        return
     if args.workload != "lap3d":
         args.no_cpu = True  # the CPU baseline is the reference on the headline workload
 
@@ -529,6 +607,12 @@ def main():
         log("drop-in pdgstrf leg (utime[FACT])")
         abi, gpu_sums = abi_leg(lu, anorm, t_step_local,
                                 fingerprint=gpu_fingerprints if want_cpu else None)
+        if args.workload == "lap3d" and args.ordering == "grid" and not args.no_device_resident:
+            log("device-resident drop-in leg (libslu_mi355x_solve.so, child process)")
+            abi["device_resident"] = device_resident_leg(args.nx)
+            abi["device_resident"]["refactor_vs_ms_per_step"] = (
+                round(abi["device_resident"]["utime_fact_ms_refactor"] / t_step_local, 3)
+                if "utime_fact_ms_refactor" in abi["device_resident"] else None)
     if args.roofline_only:
         if rank == 0:
             print(json.dumps({"roofline_only": True, "t_schur_big_ms": sst["t_schur_big_ms"],

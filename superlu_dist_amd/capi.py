@@ -157,6 +157,139 @@ def pxgstrf(lu, anorm, options=None, grid=None, m=None, n=None):
                                  "gpu_buffer": float(st.gpu_buffer)}
 
 
+# ---- the device-resident drop-in: libslu_mi355x_solve.so also exports
+# p[dsz]distribute (SRC/pddistribute.c:327) and p[dsz]gstrs (SRC/pdgstrs.c),
+# so that pdgssvx's DISTRIBUTE keeps A for a device-side fill, pdgstrf leaves
+# the factors in HBM and SOLVE runs on them.
+
+_solve = None
+
+
+def solve_lib():
+    """libslu_mi355x_solve.so: the 12 drop-in symbols + p[dsz]distribute,
+    p[dsz]gstrs (opt-in superset, csrc/dropin_solve.map)."""
+    global _solve
+    if _solve is None:
+        import os
+        path = os.path.join(os.path.dirname(DROPIN_PATH), "libslu_mi355x_solve.so")
+        if not os.path.exists(path):
+            raise RuntimeError(f"{path} missing: build with make -C superlu_dist_amd/csrc")
+        _solve = C.CDLL(path)
+    return _solve
+
+
+SLU_NR_LOC, SLU_GE, NOEQUIL = 7, 0, 0  # Stype_t / Mtype_t / DiagScale_t (SRC/supermatrix.h, superlu_enum_consts.h)
+SAMEPATTERN_SAMEROWPERM = 2
+
+
+class NRformatLoc(C.Structure):
+    """SRC/supermatrix.h NRformat_loc."""
+    _fields_ = [("nnz_loc", C.c_int64), ("m_loc", C.c_int64), ("fst_row", C.c_int64),
+                ("nzval", C.c_void_p), ("rowptr", C.POINTER(C.c_int64)),
+                ("colind", C.POINTER(C.c_int64))]
+
+
+class ScalePermstruct(C.Structure):
+    """SRC/superlu_ddefs.h:60-66."""
+    _fields_ = [("DiagScale", C.c_int), ("R", C.c_void_p), ("C", C.c_void_p),
+                ("perm_r", C.POINTER(C.c_int64)), ("perm_c", C.POINTER(C.c_int64))]
+
+
+class LUstruct(C.Structure):
+    """SRC/superlu_ddefs.h dLUstruct_t (Llu: a calloc'ed dLocalLU_t, 2352
+    bytes, include/slu_abi.h)."""
+    _fields_ = [("etree", C.POINTER(C.c_int64)), ("Glu_persist", C.POINTER(GluPersist)),
+                ("Llu", C.c_void_p), ("dt", C.c_char)]
+
+
+def _p64(a):
+    return a.ctypes.data_as(C.POINTER(C.c_int64))
+
+
+class DeviceResidentSystem:
+    """One fp64 system through the reference's pdgssvx sequence on a 1x1
+    grid, driven from here: A (NRformat_loc, column indices already mapped
+    by perm_c as SRC/pdgssvx.c:1140 leaves them), ScalePermstruct (no
+    equilibration, perm_r = identity), the symbolic factorization's
+    Glu_persist / Glu_freeable, then pddistribute -> pdgstrf -> pdgstrs of
+    libslu_mi355x_solve.so.  The arrays stay referenced for the lifetime of
+    the object (the library keeps pointers to A's copy and to the
+    LUstruct)."""
+
+    def __init__(self, n, rowptr, colind, nzval, perm_c, etree, xsup, supno, xlsub, lsub, xusub,
+                 usub, anorm):
+        self.L = solve_lib()
+        self.n, self.anorm = n, anorm
+        self.keep = [np.ascontiguousarray(x, np.int64) for x in
+                     (rowptr, colind, perm_c, etree, xsup, supno, xlsub, lsub, xusub, usub)]
+        (self.rowptr, self.colind, self.perm_c, self.etree, self.xsup, self.supno, self.xlsub,
+         self.lsub, self.xusub, self.usub) = self.keep
+        self.nzval = np.ascontiguousarray(nzval, np.float64)
+        self.perm_r = np.arange(n, dtype=np.int64)
+        self.store = NRformatLoc(len(self.nzval), n, 0, self.nzval.ctypes.data, _p64(self.rowptr),
+                                 _p64(self.colind))
+        self.A = SuperMatrix(SLU_NR_LOC, SLU_D, SLU_GE, n, n, C.addressof(self.store))
+        self.sp = ScalePermstruct(NOEQUIL, None, None, _p64(self.perm_r), _p64(self.perm_c))
+        self.glu = GluFreeable(_p64(self.lsub), _p64(self.xlsub), _p64(self.usub), _p64(self.xusub),
+                               len(self.lsub), len(self.usub), 0, 0)
+        self.gp = GluPersist(_p64(self.xsup), _p64(self.supno))
+        libc = C.CDLL(None)
+        libc.calloc.restype = C.c_void_p
+        libc.calloc.argtypes = [C.c_size_t, C.c_size_t]
+        self.lu = LUstruct(_p64(self.etree), C.pointer(self.gp), libc.calloc(1, 2352), b"d")
+        self.grid = grid_1x1()
+        self.opt = default_options()
+        self.opt.Equil = NO
+        self.opt.RowPerm = 0  # NOROWPERM
+        self.opt.ColPerm = 7  # MY_PERMC
+        L = self.L
+        L.pddistribute.restype = C.c_float
+        L.pddistribute.argtypes = [C.POINTER(Options), C.c_int64, C.POINTER(SuperMatrix),
+                                   C.POINTER(ScalePermstruct), C.POINTER(GluFreeable),
+                                   C.POINTER(LUstruct), C.POINTER(GridInfo)]
+        L.pdgstrf.restype = C.c_int64
+        L.pdgstrf.argtypes = [C.POINTER(Options), C.c_int, C.c_int, C.c_double,
+                              C.POINTER(LUstruct), C.POINTER(GridInfo), C.POINTER(Stat),
+                              C.POINTER(C.c_int)]
+        L.pdgstrs.restype = None
+        L.pdgstrs.argtypes = [C.POINTER(Options), C.c_int64, C.POINTER(LUstruct),
+                              C.POINTER(ScalePermstruct), C.POINTER(GridInfo),
+                              C.POINTER(C.c_double), C.c_int64, C.c_int64, C.c_int64, C.c_int,
+                              C.c_void_p, C.POINTER(Stat), C.POINTER(C.c_int)]
+
+    def _stat(self):
+        self._ut = (C.c_double * NPHASES)()
+        self._ops = (C.c_float * NPHASES)()
+        st = Stat()
+        st.utime = C.cast(self._ut, C.POINTER(C.c_double))
+        st.ops = C.cast(self._ops, C.POINTER(C.c_float))
+        return st
+
+    def distribute(self, fact):
+        self.opt.Fact = fact
+        return float(self.L.pddistribute(C.byref(self.opt), self.n, C.byref(self.A), C.byref(self.sp),
+                                         C.byref(self.glu), C.byref(self.lu), C.byref(self.grid)))
+
+    def factor(self):
+        st = self._stat()
+        info = C.c_int(-999)
+        rv = self.L.pdgstrf(C.byref(self.opt), self.n, self.n, self.anorm, C.byref(self.lu),
+                            C.byref(self.grid), C.byref(st), C.byref(info))
+        return int(rv), info.value, float(self._ops[FACT])
+
+    def solve(self, b):
+        """b in A's original row order (m_loc = n on 1x1); returns x."""
+        x = np.ascontiguousarray(b, np.float64).copy()
+        st = self._stat()
+        info = C.c_int(-999)
+        self.L.pdgstrs(C.byref(self.opt), self.n, C.byref(self.lu), C.byref(self.sp),
+                       C.byref(self.grid), x.ctypes.data_as(C.POINTER(C.c_double)), self.n, 0,
+                       self.n, 1, None, C.byref(st), C.byref(info))
+        if info.value:
+            raise RuntimeError(f"pdgstrs info {info.value}")
+        return x
+
+
 def layout():
     """Sizes / offsets of the mirror, in the keys of tests/golden/abi_layout.json."""
     return {"sizeof(gridinfo_t)": C.sizeof(GridInfo), "sizeof(superlu_scope_t)": C.sizeof(ScopeT),

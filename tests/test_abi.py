@@ -82,3 +82,16 @@ def test_mirror_layout_matches_reference():
     finally:
         shutil.rmtree(tmp)
     assert mine == golden
+
+
+def test_device_resident_mirror_layout():
+    """The structs capi.DeviceResidentSystem hands to pddistribute / pdgstrf /
+    pdgstrs have the sizes include/slu_abi.h asserts for the reference's
+    (SRC/supermatrix.h NRformat_loc, SRC/superlu_ddefs.h ScalePermstruct /
+    LUstruct)."""
+    import ctypes as C
+    from superlu_dist_amd import capi
+    assert C.sizeof(capi.NRformatLoc) == 48
+    assert C.sizeof(capi.ScalePermstruct) == 40 and capi.ScalePermstruct.perm_r.offset == 24
+    assert C.sizeof(capi.LUstruct) == 32
+    assert C.sizeof(capi.SuperMatrix) == 40

@@ -326,3 +326,32 @@ def test_grid_exit_evicts_the_cached_plan(pr, pc):
         assert plans == ["built", "reused", "built", "reused"], out[-3000:]
     else:  # 1x1: the transport is per device and outlives the grid: the plan may stay
         assert plans[0] == "built" and plans[1] == plans[3] == "reused", out[-3000:]
+
+
+@pytest.mark.gpu
+def test_device_resident_system_through_solve_library():
+    """bench.py's device-resident leg at a test size: libslu_mi355x_solve.so's
+    pddistribute (keeps A), pdgstrf (device fill, factors kept in HBM) and
+    pdgstrs, driven through capi as pdgssvx drives them, then the
+    SamePattern_SameRowPerm refactorization; the solutions are accurate."""
+    import numpy as np
+    import scipy.sparse as sp
+    from superlu_dist_amd import capi
+    from superlu_dist_amd import symbolic as SY
+    from superlu_dist_amd.frontend import STENCIL_3D7, Csc, nd_order
+    nx = 16
+    A = Csc.stencil(STENCIL_3D7, nx, nx, nx)
+    n = A.n
+    cp, ri, v = A.arrays()
+    co = SY.sp_colorder(n, n, cp, ri, nd_order(nx, nx, nx), SY.MY_PERMC)
+    sb = SY.symbfact(n, n, co.colbeg, co.colend, SY.relabel_rows(ri, co.perm_c), co.etree, 60, 256)
+    s = capi.DeviceResidentSystem(n, cp, co.perm_c[ri], v, co.perm_c, co.etree, sb.xsup, sb.supno,
+                                  sb.xlsub, sb.lsub, sb.xusub, sb.usub, 12.0)
+    xt = np.random.default_rng(0).standard_normal(n)
+    b = sp.csc_matrix((v, ri, cp), shape=(n, n)) @ xt
+    for fact in (0, capi.SAMEPATTERN_SAMEROWPERM):
+        s.distribute(fact)
+        rv, info, ops = s.factor()
+        assert rv == 0 and info == 0 and ops > 0
+        x = s.solve(b)
+        assert np.abs(x - xt).max() <= 1e-10 * np.abs(xt).max()
