@@ -397,6 +397,11 @@ void slu_symbfact_sizes(const void *h, int64_t *sizes);
 void slu_symbfact_arrays(const void *h, int64_t *xsup, int64_t *supno, int64_t *xlsub,
                          int64_t *lsub, int64_t *xusub, int64_t *usub);
 void slu_symbfact_free(void *h);
+/* 1 when the last slu_symbfact / symbfact ran its countnz + fixupL epilogue
+   (SRC/util.c:95-199) on the GPU (csrc/symbolic_dev.hip; SLU_SYMB_DEVICE=1
+   forces it, =0 keeps it on the host; default: GPU for square problems with
+   >= 20 000 supernodes when one is visible), 0 when on the host */
+int slu_symbfact_last_epilogue_device(void);
 /* Drop-in: the reference's own prototypes (SRC/superlu_defs.h:1079, 1091;
  * types in slu_abi.h).  A program linked against libslu_mi355x.so ahead of
  * the reference archive runs these in pdgssvx (SRC/pdgssvx.c:1046, 1075).

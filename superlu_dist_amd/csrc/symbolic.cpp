@@ -23,15 +23,39 @@
 #include <cstring>
 #include <stdexcept>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "common.h"
 #include "slu_abi.h"
 
+// csrc/symbolic_dev.hip (the full library links both)
+bool slu_symb_epilogue_dev(int64_t n, int64_t nsup, const int32_t *raw, int64_t raw_len, const int64_t *xlsub_raw,
+                           const int32_t *xsup, const int32_t *supno, const int32_t *usub, int64_t nu,
+                           std::vector<int64_t> &lsub, std::vector<int64_t> &xlsub, int64_t *nnzL, int64_t *nnzU,
+                           std::string &err);
+bool slu_symb_have_device();
+
 namespace slu {
 namespace symb {
 
 using I = int64_t;
+
+// where the last symbfact ran its epilogue (countnz + fixupL): 0 host, 1 device
+static int g_last_epilogue = 0;
+
+// SLU_SYMB_DEVICE=1: the epilogue on the GPU (an error without one), =0: on
+// the host; unset: on the GPU for square problems with >= 20 000 supernodes
+// when a GPU is visible (the search stays on the host either way)
+static bool use_device_epilogue(I m, I n, I nsup) {
+    const char *e = getenv("SLU_SYMB_DEVICE");
+    if (e) {
+        if (atoi(e) == 0) return false;
+        if (!slu_symb_have_device()) throw Error("symbfact: SLU_SYMB_DEVICE=1 but no GPU is visible");
+        return m == n;
+    }
+    return m == n && nsup >= 20000 && slu_symb_have_device();
+}
 using std::vector;
 constexpr I NONE = -1;
 
@@ -715,6 +739,30 @@ static Result symbfact_t(I m, I n, const I *cb, const I *ce, const I *ri64, cons
     w.run(0, mn, rend.data());
     const auto t1 = std::chrono::steady_clock::now();
 
+    g_last_epilogue = 0;
+    if constexpr (std::is_same<T, int32_t>::value) {
+        const I nsup1 = (I)w.supno[n] + 1;
+        if (n > 1 && use_device_epilogue(m, n, nsup1)) {
+            // countnz + fixupL on the device (csrc/symbolic_dev.hip)
+            std::string err;
+            R.lsub_size = w.xlsub[n];
+            if (!slu_symb_epilogue_dev(n, nsup1, w.lsub.data(), w.xlsub[n], w.xlsub.data(), w.xsup.data(),
+                                       w.supno.data(), w.usub.data(), w.xusub[mn], R.lsub, R.xlsub, &R.nnzL,
+                                       &R.nnzU, err))
+                throw Error("symbfact device epilogue: " + err);
+            R.nnzLU = R.nnzL + R.nnzU - mn;
+            R.xsup.assign(w.xsup.begin(), w.xsup.end());
+            R.supno.assign(w.supno.begin(), w.supno.end());
+            R.xusub = std::move(w.xusub);
+            R.usub.assign(w.usub.begin(), w.usub.begin() + R.xusub[mn]);
+            g_last_epilogue = 1;
+            if (getenv("SLU_SYMB_TIME"))
+                fprintf(stderr, "symbfact: search %.3f s, total %.3f s (device epilogue)\n",
+                        std::chrono::duration<double>(t1 - t0).count(),
+                        std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
+            return R;
+        }
+    }
     R.xsup.assign(w.xsup.begin(), w.xsup.end());
     R.supno.assign(w.supno.begin(), w.supno.end());
     R.xlsub = std::move(w.xlsub);
@@ -846,6 +894,9 @@ void slu_symbfact_arrays(const void *h, int64_t *xsup, int64_t *supno, int64_t *
 }
 
 void slu_symbfact_free(void *h) { delete (Result *)h; }
+
+// 1 when the last symbfact ran its countnz / fixupL epilogue on the GPU
+int slu_symbfact_last_epilogue_device(void) { return g_last_epilogue; }
 
 // ---- drop-in entry points with the reference's prototypes
 

@@ -119,6 +119,7 @@ def lib():
         "slu_symbfact_sizes": (None, [P, c_i64p]),
         "slu_symbfact_arrays": (None, [P, c_i64p, c_i64p, c_i64p, c_i64p, c_i64p, c_i64p]),
         "slu_symbfact_free": (None, [P]),
+        "slu_symbfact_last_epilogue_device": (C.c_int, []),
         "METIS_NodeND": (C.c_int, [c_i64p, c_i64p, c_i64p, c_i64p, c_i64p, c_i64p, c_i64p]),
         "slu_symbolic": (P, [C.POINTER(SluCsc), c_i64p, C.c_int, C.c_int, C.c_int]),
         "slu_symb_free": (None, [P]),

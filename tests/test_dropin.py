@@ -321,7 +321,7 @@ def test_grid_exit_evicts_the_cached_plan(pr, pc):
     for _, _, info, err in res:
         assert int(info) == 0 and float(err) < 1e-10, out[-3000:]
     # rank 0's plan per call: built, reused, then (new grid) built, reused
-    plans = re.findall(r"\[pdgstrf rank 0\] digest [0-9.]+ ms, plan (built|reused)", out)
+    plans = re.findall(r"\[PDGSTRF rank 0\] digest [0-9.]+ ms, plan (built|reused)", out)
     if pr * pc > 1:
         assert plans == ["built", "reused", "built", "reused"], out[-3000:]
     else:  # 1x1: the transport is per device and outlives the grid: the plan may stay

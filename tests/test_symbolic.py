@@ -199,3 +199,39 @@ def test_symbfact_virtual_last_list_3d_stencil(monkeypatch):
         s = _classic_vs_default(n, colptr, rowind, np.arange(n, dtype=np.int64), S.NATURAL, relax,
                                 maxsup, monkeypatch)
         assert s.nsupers < n
+
+
+def _epilogue_device():
+    from superlu_dist_amd.lib import lib
+    return int(lib().slu_symbfact_last_epilogue_device())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", CASES)
+def test_symbfact_device_epilogue_matches_reference(name, monkeypatch):
+    """symbfact's countnz + fixupL (SRC/util.c:95-199) on the GPU
+    (csrc/symbolic_dev.hip, SLU_SYMB_DEVICE=1): every array, nnzLU and the
+    return value equal the REFERENCE's on every symb_* golden."""
+    monkeypatch.setenv("SLU_SYMB_DEVICE", "1")
+    test_symbfact_matches_reference(name)
+    assert _epilogue_device() == 1
+
+
+@pytest.mark.gpu
+def test_symbfact_device_epilogue_large(monkeypatch):
+    """A 40^3 Laplacian in nested-dissection order (4 098 supernodes, wide
+    top separators): the device epilogue equals the host one."""
+    from superlu_dist_amd.frontend import STENCIL_3D7, Csc, nd_order
+    k = 40
+    A = Csc.stencil(STENCIL_3D7, k, k, k)
+    cp, ri, _ = A.arrays()
+    co = S.sp_colorder(A.n, A.n, cp, ri, nd_order(k, k, k), S.MY_PERMC)
+    rr = S.relabel_rows(ri, co.perm_c)
+    out = {}
+    for dev in ("0", "1"):
+        monkeypatch.setenv("SLU_SYMB_DEVICE", dev)
+        out[dev] = S.symbfact(A.n, A.n, co.colbeg, co.colend, rr, co.etree, 60, 256)
+        assert _epilogue_device() == int(dev)
+    for f in ("xsup", "supno", "xlsub", "lsub", "xusub", "usub"):
+        np.testing.assert_array_equal(getattr(out["0"], f), getattr(out["1"], f), err_msg=f)
+    assert (out["0"].ret, out["0"].nnzLU) == (out["1"].ret, out["1"].nnzLU)
