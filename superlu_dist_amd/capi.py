@@ -220,8 +220,12 @@ class DeviceResidentSystem:
                  usub, anorm):
         self.L = solve_lib()
         self.n, self.anorm = n, anorm
+        # Glu_persist's xsup as symbfact leaves it: n + 1 entries (the
+        # supernode bounds, then the last one repeated)
+        xs = np.full(n + 2, int(xsup[-1]), np.int64)
+        xs[:len(xsup)] = xsup
         self.keep = [np.ascontiguousarray(x, np.int64) for x in
-                     (rowptr, colind, perm_c, etree, xsup, supno, xlsub, lsub, xusub, usub)]
+                     (rowptr, colind, perm_c, etree, xs, supno, xlsub, lsub, xusub, usub)]
         (self.rowptr, self.colind, self.perm_c, self.etree, self.xsup, self.supno, self.xlsub,
          self.lsub, self.xusub, self.usub) = self.keep
         self.nzval = np.ascontiguousarray(nzval, np.float64)

@@ -294,10 +294,10 @@ def test_factored_solve_after_eviction_with_host_factors():
 # and the cached plan built on them goes with them: the
 # next round's first call builds a new plan even when MPI reuses the
 # communicator handle and malloc the LUstruct addresses.
-def _regrid(nprocs, pr, pc):
+def _regrid(nprocs, pr, pc, **extra):
     env = dict(os.environ)
     env.update({"OMP_NUM_THREADS": "1", "MKL_NUM_THREADS": "1", "MKL_THREADING_LAYER": "SEQUENTIAL",
-                "HSA_ENABLE_IPC_MODE_LEGACY": "0", "SUPERLU_MI355X_TIMING": "1"})
+                "HSA_ENABLE_IPC_MODE_LEGACY": "0", "SUPERLU_MI355X_TIMING": "1"}, **extra)
     cmd = [MPIEXEC, "-n", str(nprocs), os.path.join(REF, "regrid"), os.path.join(MAT, "big.rua"),
            str(pr), str(pc)]
     r = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=300)
@@ -317,9 +317,10 @@ def test_grid_exit_evicts_the_cached_plan(pr, pc):
     rc, out = _regrid(pr * pc, pr, pc)
     assert rc == 0, out[-3000:]
     res = re.findall(r"round (\d) call (\d): info (\d+) err ([0-9.eE+-]+)", out)
+    summary = "\n".join(f"round {a} call {b}: info {c} err {d}" for a, b, c, d in res)
     assert len(res) == 4, out[-3000:]
     for _, _, info, err in res:
-        assert int(info) == 0 and float(err) < 1e-10, out[-3000:]
+        assert int(info) == 0 and float(err) < 1e-10, summary + "\n" + out[-2500:]
     # rank 0's plan per call: built, reused, then (new grid) built, reused
     plans = re.findall(r"\[PDGSTRF rank 0\] digest [0-9.]+ ms, plan (built|reused)", out)
     if pr * pc > 1:
@@ -355,3 +356,15 @@ def test_device_resident_system_through_solve_library():
         assert rv == 0 and info == 0 and ops > 0
         x = s.solve(b)
         assert np.abs(x - xt).max() <= 1e-10 * np.abs(xt).max()
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not _have("regrid"), reason="grid life-cycle driver not built")
+def test_grid_refactorization_without_plan_cache():
+    """The same life cycle on 2x2 with the plan cache off
+    (SUPERLU_MI355X_PLAN_CACHE=0): every call builds its plan."""
+    rc, out = _regrid(4, 2, 2, SUPERLU_MI355X_PLAN_CACHE="0")
+    assert rc == 0, out[-3000:]
+    res = re.findall(r"round (\d) call (\d): info (\d+) err ([0-9.eE+-]+)", out)
+    summary = "\n".join(f"round {a} call {b}: info {c} err {d}" for a, b, c, d in res)
+    assert len(res) == 4 and all(int(i) == 0 and float(e) < 1e-10 for _, _, i, e in res), summary
