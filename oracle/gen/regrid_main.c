@@ -10,6 +10,7 @@
  *
  * usage: mpiexec -n Pr*Pc regrid file Pr Pc   (prints "round r call c: err e")
  */
+#define _POSIX_C_SOURCE 200809L
 #include <stdlib.h>
 #include <string.h>
 
@@ -21,7 +22,14 @@ int main(int argc, char **argv) {
     if (argc < 4) return 2;
     MPI_Init(&argc, &argv);
     const int pr = atoi(argv[2]), pc = atoi(argv[3]);
+    gridinfo_t keep; /* REGRID_KEEP: round 0's grid stays alive through round 1 */
     for (int round = 0; round < 2; ++round) {
+        /* REGRID_SKIP0: round 0 runs with this library's factorization skipped
+         * (SUPERLU_MI355X_FACTOR_SKIP), round 1 is the first real one */
+        if (getenv("REGRID_SKIP0")) {
+            if (round == 0) setenv("SUPERLU_MI355X_FACTOR_SKIP", "1", 1);
+            else unsetenv("SUPERLU_MI355X_FACTOR_SKIP");
+        }
         gridinfo_t grid;
         superlu_gridinit(MPI_COMM_WORLD, pr, pc, &grid);
         SuperMatrix A;
@@ -47,6 +55,7 @@ int main(int argc, char **argv) {
         set_default_options_dist(&opt);
         opt.ColPerm = MMD_AT_PLUS_A; /* (METIS is not in this image) */
         opt.PrintStat = NO;
+        if (getenv("REGRID_NOREFINE")) opt.IterRefine = NOREFINE;
         dScalePermstruct_t sp;
         dLUstruct_t lu;
         dSOLVEstruct_t solve;
@@ -68,6 +77,25 @@ int main(int argc, char **argv) {
             }
             double l[2] = {dmax, xmax};
             MPI_Allreduce(l, g, 2, MPI_DOUBLE, MPI_MAX, grid.comm);
+            if (getenv("REGRID_SUMS")) { /* the factors' sums, per rank (diagnostics) */
+                dLocalLU_t *Llu = lu.Llu;
+                const int nsup = lu.Glu_persist->supno[n - 1] + 1;
+                double ls = 0, us = 0;
+                for (int lb = 0; lb < CEILING(nsup, grid.npcol); ++lb) {
+                    const int_t *ix = Llu->Lrowind_bc_ptr[lb];
+                    if (!ix) continue;
+                    const int jb = lb * grid.npcol + grid.iam % grid.npcol;
+                    const int_t cnt = ix[1] * (lu.Glu_persist->xsup[jb + 1] - lu.Glu_persist->xsup[jb]);
+                    for (int_t i = 0; i < cnt; ++i) ls += fabs(Llu->Lnzval_bc_ptr[lb][i]);
+                }
+                for (int lb = 0; lb < CEILING(nsup, grid.nprow); ++lb) {
+                    const int_t *ix = Llu->Ufstnz_br_ptr[lb];
+                    if (!ix) continue;
+                    for (int_t i = 0; i < ix[1]; ++i) us += fabs(Llu->Unzval_br_ptr[lb][i]);
+                }
+                printf("round %d call %d rank %d: sum|L| %.17g sum|U| %.17g\n", round, call, grid.iam, ls, us);
+                fflush(stdout);
+            }
             if (grid.iam == 0) {
                 printf("round %d call %d: info %d err %.3e\n", round, call, info, g[0] / g[1]);
                 fflush(stdout);
@@ -81,6 +109,23 @@ int main(int argc, char **argv) {
                                                rowptr1, SLU_NR_loc, SLU_D, SLU_GE);
             }
         }
+        if (getenv("REGRID_PROBE")) { /* messages nobody received (diagnostics) */
+            MPI_Comm cs[4] = {grid.comm, grid.rscp.comm, grid.cscp.comm, MPI_COMM_WORLD};
+            const char *nm[4] = {"grid", "row", "column", "world"};
+            MPI_Barrier(grid.comm);
+            for (int k = 0; k < 4; ++k) {
+                int flag = 0;
+                MPI_Status st;
+                MPI_Iprobe(MPI_ANY_SOURCE, MPI_ANY_TAG, cs[k], &flag, &st);
+                if (flag) {
+                    int cnt = 0;
+                    MPI_Get_count(&st, MPI_BYTE, &cnt);
+                    printf("round %d rank %d: pending message on the %s communicator from %d tag %d (%d bytes)\n",
+                           round, grid.iam, nm[k], st.MPI_SOURCE, st.MPI_TAG, cnt);
+                    fflush(stdout);
+                }
+            }
+        }
         dSolveFinalize(&opt, &solve);
         dDestroy_LU(A.ncol, &grid, &lu);
         dLUstructFree(&lu);
@@ -89,8 +134,10 @@ int main(int argc, char **argv) {
         SUPERLU_FREE(b);
         SUPERLU_FREE(b0);
         SUPERLU_FREE(xtrue);
-        superlu_gridexit(&grid);
+        if (getenv("REGRID_KEEP") && round == 0) keep = grid;
+        else superlu_gridexit(&grid);
     }
+    if (getenv("REGRID_KEEP")) superlu_gridexit(&keep);
     MPI_Finalize();
     return 0;
 }

@@ -282,7 +282,10 @@ class DeviceResidentSystem:
         return int(rv), info.value, float(self._ops[FACT])
 
     def solve(self, b):
-        """b in A's original row order (m_loc = n on 1x1); returns x."""
+        """b in A's original row order (m_loc = n on 1x1); returns x in A's
+        original column order: pdgstrs leaves the solution of the column-
+        permuted system, and pdgssvx maps it back with pdPermute_Dense_Matrix
+        by inv_perm_c (SRC/pdgssvx.c, SOLVE phase), i.e. x[j] = X[perm_c[j]]."""
         x = np.ascontiguousarray(b, np.float64).copy()
         st = self._stat()
         info = C.c_int(-999)
@@ -291,7 +294,7 @@ class DeviceResidentSystem:
                        self.n, 1, None, C.byref(st), C.byref(info))
         if info.value:
             raise RuntimeError(f"pdgstrs info {info.value}")
-        return x
+        return x[self.perm_c]
 
 
 def layout():

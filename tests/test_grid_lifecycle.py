@@ -41,7 +41,8 @@ def _worker(rank, world, port, pr, pc, nx, reference, schedule, out_dir):
             info, _ = p.factor(cases.anorm(A))
             p.download()
             del p
-            res[f"L{it}"], res[f"U{it}"], res[f"info{it}"] = lu.Lval, lu.Uval, info
+            # (copies: lu's arrays are freed with it on the next iteration)
+            res[f"L{it}"], res[f"U{it}"], res[f"info{it}"] = lu.Lval.copy(), lu.Uval.copy(), info
             if "drop" in what:
                 del comm
                 comm = None
