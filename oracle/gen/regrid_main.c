@@ -31,7 +31,10 @@ int main(int argc, char **argv) {
             else unsetenv("SUPERLU_MI355X_FACTOR_SKIP");
         }
         gridinfo_t grid;
-        superlu_gridinit(MPI_COMM_WORLD, pr, pc, &grid);
+        /* REGRID_SAMEGRID: both rounds on one grid (a second system, new
+         * LUstruct and SOLVEstruct, on the same communicators) */
+        if (getenv("REGRID_SAMEGRID") && round == 1) grid = keep;
+        else superlu_gridinit(MPI_COMM_WORLD, pr, pc, &grid);
         SuperMatrix A;
         double *b, *xtrue;
         int ldb, ldx;
@@ -86,14 +89,31 @@ int main(int argc, char **argv) {
                     if (!ix) continue;
                     const int jb = lb * grid.npcol + grid.iam % grid.npcol;
                     const int_t cnt = ix[1] * (lu.Glu_persist->xsup[jb + 1] - lu.Glu_persist->xsup[jb]);
-                    for (int_t i = 0; i < cnt; ++i) ls += fabs(Llu->Lnzval_bc_ptr[lb][i]);
+                    for (int_t i = 0; i < cnt; ++i) ls += Llu->Lnzval_bc_ptr[lb][i] * (double)(i % 97 + 1);
                 }
                 for (int lb = 0; lb < CEILING(nsup, grid.nprow); ++lb) {
                     const int_t *ix = Llu->Ufstnz_br_ptr[lb];
                     if (!ix) continue;
-                    for (int_t i = 0; i < ix[1]; ++i) us += fabs(Llu->Unzval_br_ptr[lb][i]);
+                    for (int_t i = 0; i < ix[1]; ++i) us += Llu->Unzval_br_ptr[lb][i] * (double)(i % 97 + 1);
                 }
-                printf("round %d call %d rank %d: sum|L| %.17g sum|U| %.17g\n", round, call, grid.iam, ls, us);
+                /* and the index arrays (an in-place change would show here) */
+                long long li = 0, ui = 0, lv = 0;
+                for (int lb = 0; lb < CEILING(nsup, grid.npcol); ++lb) {
+                    const int_t *ix = Llu->Lrowind_bc_ptr[lb];
+                    if (!ix) continue;
+                    int_t p = BC_HEADER;
+                    for (int_t b = 0; b < ix[0]; ++b) p += LB_DESCRIPTOR + ix[p + 1];
+                    for (int_t i = 0; i < p; ++i) li += (long long)ix[i] * (i + 1);
+                    if (Llu->Lindval_loc_bc_ptr && Llu->Lindval_loc_bc_ptr[lb])
+                        for (int_t i = 0; i < 3 * ix[0]; ++i) lv += (long long)Llu->Lindval_loc_bc_ptr[lb][i] * (i + 1);
+                }
+                for (int lb = 0; lb < CEILING(nsup, grid.nprow); ++lb) {
+                    const int_t *ix = Llu->Ufstnz_br_ptr[lb];
+                    if (!ix) continue;
+                    for (int_t i = 0; i < ix[2]; ++i) ui += (long long)ix[i] * (i + 1);
+                }
+                printf("round %d call %d rank %d: wsum L %.17g wsum U %.17g idx %lld %lld %lld\n", round, call,
+                       grid.iam, ls, us, li, ui, lv);
                 fflush(stdout);
             }
             if (grid.iam == 0) {
@@ -134,10 +154,11 @@ int main(int argc, char **argv) {
         SUPERLU_FREE(b);
         SUPERLU_FREE(b0);
         SUPERLU_FREE(xtrue);
-        if (getenv("REGRID_KEEP") && round == 0) keep = grid;
+        if ((getenv("REGRID_KEEP") || getenv("REGRID_SAMEGRID")) && round == 0) keep = grid;
+        else if (getenv("REGRID_SAMEGRID")) { /* (freed below) */ }
         else superlu_gridexit(&grid);
     }
-    if (getenv("REGRID_KEEP")) superlu_gridexit(&keep);
+    if (getenv("REGRID_KEEP") || getenv("REGRID_SAMEGRID")) superlu_gridexit(&keep);
     MPI_Finalize();
     return 0;
 }
