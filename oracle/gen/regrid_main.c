@@ -10,7 +10,7 @@
  *
  * usage: mpiexec -n Pr*Pc regrid file Pr Pc   (prints "round r call c: err e")
  */
-#define _POSIX_C_SOURCE 200809L
+#define _GNU_SOURCE
 #include <stdlib.h>
 #include <string.h>
 
@@ -18,12 +18,79 @@
 
 int dcreate_matrix(SuperMatrix *, int, double **, int *, double **, int *, FILE *, gridinfo_t *);
 
+#include <dlfcn.h>
+#include <execinfo.h>
+#include <signal.h>
+#include <unistd.h>
+static void segv_bt(int sig) {
+    void *f[64];
+    const int k = backtrace(f, 64);
+    backtrace_symbols_fd(f, k, 2);
+    signal(sig, SIG_DFL);
+    raise(sig);
+}
+/* the factors' position-weighted sums of this rank (diagnostics) */
+static void factor_sums(dLUstruct_t *lu, gridinfo_t *grid, int n, double *ls, double *us) {
+    dLocalLU_t *Llu = lu->Llu;
+    const int nsup = lu->Glu_persist->supno[n - 1] + 1;
+    *ls = *us = 0;
+    for (int lb = 0; lb < CEILING(nsup, grid->npcol); ++lb) {
+        const int_t *ix = Llu->Lrowind_bc_ptr[lb];
+        if (!ix) continue;
+        const int jb = lb * grid->npcol + grid->iam % grid->npcol;
+        const int_t cnt = ix[1] * (lu->Glu_persist->xsup[jb + 1] - lu->Glu_persist->xsup[jb]);
+        for (int_t i = 0; i < cnt; ++i) *ls += Llu->Lnzval_bc_ptr[lb][i] * (double)(i % 97 + 1);
+    }
+    for (int lb = 0; lb < CEILING(nsup, grid->nprow); ++lb) {
+        const int_t *ix = Llu->Ufstnz_br_ptr[lb];
+        if (!ix) continue;
+        for (int_t i = 0; i < ix[1]; ++i) *us += Llu->Unzval_br_ptr[lb][i] * (double)(i % 97 + 1);
+    }
+}
+
+static int g_round;
+#ifdef REGRID_MIX
+int_t ref_pdgstrf(superlu_dist_options_t *, int, int, double, dLUstruct_t *, gridinfo_t *, SuperLUStat_t *, int *);
+#endif
+#ifdef REGRID_MIX
+/* (regrid_mix only) REGRID_WRAP: this executable's pdgstrf interposes the library's (the
+ * reference's pdgssvx binds it first) and checks that the factors do not
+ * change after the call returned (no write still in flight) */
+int_t pdgstrf(superlu_dist_options_t *options, int m, int n, double anorm, dLUstruct_t *LUstruct,
+              gridinfo_t *grid, SuperLUStat_t *stat, int *info) {
+    typedef int_t (*fn_t)(superlu_dist_options_t *, int, int, double, dLUstruct_t *, gridinfo_t *,
+                          SuperLUStat_t *, int *);
+    static fn_t next = NULL;
+    if (!next) next = (fn_t)dlsym(RTLD_NEXT, "pdgstrf");
+    fn_t f = next;
+#ifdef REGRID_MIX
+    /* REGRID_REFROUND=r: round r factors with the reference's own pdgstrf
+     * (linked in renamed), the other round with the library's */
+    const char *rr = getenv("REGRID_REFROUND");
+    if (rr && atoi(rr) == g_round) f = ref_pdgstrf;
+#endif
+    const int_t rv = f(options, m, n, anorm, LUstruct, grid, stat, info);
+    if (getenv("REGRID_WRAP")) {
+        double l0, u0, l1, u1;
+        factor_sums(LUstruct, grid, n, &l0, &u0);
+        usleep(500000);
+        factor_sums(LUstruct, grid, n, &l1, &u1);
+        printf("pdgstrf returned, rank %d: wsum L %.17g U %.17g, 0.5 s later L %.17g U %.17g%s\n", grid->iam,
+               l0, u0, l1, u1, (l0 != l1 || u0 != u1) ? "  CHANGED" : "");
+        fflush(stdout);
+    }
+    return rv;
+}
+#endif
+
 int main(int argc, char **argv) {
     if (argc < 4) return 2;
+    if (getenv("REGRID_BT")) signal(SIGSEGV, segv_bt);
     MPI_Init(&argc, &argv);
     const int pr = atoi(argv[2]), pc = atoi(argv[3]);
     gridinfo_t keep; /* REGRID_KEEP: round 0's grid stays alive through round 1 */
     for (int round = 0; round < 2; ++round) {
+        g_round = round;
         /* REGRID_SKIP0: round 0 runs with this library's factorization skipped
          * (SUPERLU_MI355X_FACTOR_SKIP), round 1 is the first real one */
         if (getenv("REGRID_SKIP0")) {
