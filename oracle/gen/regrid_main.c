@@ -67,7 +67,7 @@ int_t pdgstrf(superlu_dist_options_t *options, int m, int n, double anorm, dLUst
     /* REGRID_REFROUND=r: round r factors with the reference's own pdgstrf
      * (linked in renamed), the other round with the library's */
     const char *rr = getenv("REGRID_REFROUND");
-    if (rr && atoi(rr) == g_round) f = ref_pdgstrf;
+    if (rr && (atoi(rr) == g_round || atoi(rr) < 0)) f = ref_pdgstrf; /* (-1: both rounds) */
 #endif
     const int_t rv = f(options, m, n, anorm, LUstruct, grid, stat, info);
     if (getenv("REGRID_WRAP")) {
@@ -87,6 +87,82 @@ int main(int argc, char **argv) {
     if (argc < 4) return 2;
     if (getenv("REGRID_BT")) signal(SIGSEGV, segv_bt);
     MPI_Init(&argc, &argv);
+#ifdef REGRID_MIX
+    /* REGRID_HIPINIT=1: the HIP runtime initialised (one device allocation)
+     * before anything else, whatever factors */
+    if (getenv("REGRID_HIPINIT")) {
+        void *h = dlopen("libamdhip64.so", RTLD_NOW | RTLD_GLOBAL);
+        int (*hmalloc)(void **, size_t) = h ? (int (*)(void **, size_t))dlsym(h, "hipMalloc") : NULL;
+        void *d = NULL;
+        printf("hipMalloc: %d\n", hmalloc ? hmalloc(&d, 1 << 20) : -1);
+        /* REGRID_HIPINIT=2: and two streams (priority, non-blocking) created
+         * and destroyed; 3: one plain stream */
+        const int mode = atoi(getenv("REGRID_HIPINIT"));
+        int (*prange)(int *, int *) = (int (*)(int *, int *))dlsym(h, "hipDeviceGetStreamPriorityRange");
+        int (*screate)(void **, unsigned, int) = (int (*)(void **, unsigned, int))dlsym(h, "hipStreamCreateWithPriority");
+        int (*splain)(void **) = (int (*)(void **))dlsym(h, "hipStreamCreate");
+        int (*sdestroy)(void *) = (int (*)(void *))dlsym(h, "hipStreamDestroy");
+        void *s1 = NULL, *s2 = NULL;
+        int lo = 0, hi = 0;
+        if (mode == 2) {
+            prange(&lo, &hi);
+            printf("streams: %d %d\n", screate(&s1, 1, lo), screate(&s2, 1, hi));
+            sdestroy(s1);
+            sdestroy(s2);
+        } else if (mode == 3) {
+            printf("stream: %d\n", splain(&s1));
+            sdestroy(s1);
+        } else if (mode == 4) { /* which calls move libc rand()'s sequence */
+            srand(7);
+            const int r0 = rand();
+            srand(7);
+            splain(&s1);
+            const int r1 = rand();
+            srand(7);
+            sdestroy(s1);
+            const int r2 = rand();
+            srand(7);
+            void *d2 = NULL;
+            hmalloc(&d2, 1 << 26);
+            const int r3 = rand();
+            printf("rand after srand(7): %d; after stream create %d, destroy %d, hipMalloc %d\n", r0, r1, r2, r3);
+        }
+    }
+    /* REGRID_MPITEST=1: broadcasts and all-to-alls of patterned buffers,
+     * checked on every rank (after REGRID_HIPINIT's streams, if any) */
+    if (getenv("REGRID_MPITEST")) {
+        int me, np;
+        MPI_Comm_rank(MPI_COMM_WORLD, &me);
+        MPI_Comm_size(MPI_COMM_WORLD, &np);
+        for (long sz = 8; sz <= (8L << 20); sz *= 8) {
+            long bad = 0;
+            for (int rep = 0; rep < 3; ++rep) {
+                double *buf = (double *)malloc(sz * sizeof(double));
+                for (long i = 0; i < sz; ++i) buf[i] = me == 0 ? (double)(i * 7 + rep) : -1.0;
+                MPI_Bcast(buf, (int)sz, MPI_DOUBLE, 0, MPI_COMM_WORLD);
+                for (long i = 0; i < sz; ++i) bad += buf[i] != (double)(i * 7 + rep);
+                free(buf);
+                /* all-to-all-v: rank p sends rank q a block of sz/np values p*1e9+q*1e6+i */
+                const long blk = sz / np > 0 ? sz / np : 1;
+                double *sb = (double *)malloc(blk * np * sizeof(double)), *rb = (double *)malloc(blk * np * sizeof(double));
+                int *cnt = (int *)malloc(np * sizeof(int)), *dsp = (int *)malloc(np * sizeof(int));
+                for (int q = 0; q < np; ++q) {
+                    cnt[q] = (int)blk;
+                    dsp[q] = (int)(q * blk);
+                    for (long i = 0; i < blk; ++i) sb[q * blk + i] = me * 1e9 + q * 1e6 + i + rep;
+                }
+                MPI_Alltoallv(sb, cnt, dsp, MPI_DOUBLE, rb, cnt, dsp, MPI_DOUBLE, MPI_COMM_WORLD);
+                for (int p = 0; p < np; ++p)
+                    for (long i = 0; i < blk; ++i) bad += rb[p * blk + i] != p * 1e9 + me * 1e6 + i + rep;
+                free(sb); free(rb); free(cnt); free(dsp);
+            }
+            long tot = 0;
+            MPI_Allreduce(&bad, &tot, 1, MPI_LONG, MPI_SUM, MPI_COMM_WORLD);
+            if (me == 0) printf("mpitest %ld doubles: %ld wrong\n", sz, tot);
+        }
+        fflush(stdout);
+    }
+#endif
     const int pr = atoi(argv[2]), pc = atoi(argv[3]);
     gridinfo_t keep; /* REGRID_KEEP: round 0's grid stays alive through round 1 */
     for (int round = 0; round < 2; ++round) {
@@ -183,8 +259,16 @@ int main(int argc, char **argv) {
                        grid.iam, ls, us, li, ui, lv);
                 fflush(stdout);
             }
+            /* the reference draws its solve trees' seeds from rand() on every
+             * rank (SRC/pddistribute.c:1557): the sequence must not have moved
+             * differently on any rank */
+            const int rnd = rand();
+            int rmin, rmax;
+            MPI_Allreduce(&rnd, &rmin, 1, MPI_INT, MPI_MIN, grid.comm);
+            MPI_Allreduce(&rnd, &rmax, 1, MPI_INT, MPI_MAX, grid.comm);
             if (grid.iam == 0) {
-                printf("round %d call %d: info %d err %.3e\n", round, call, info, g[0] / g[1]);
+                printf("round %d call %d: info %d err %.3e rand %s\n", round, call, info, g[0] / g[1],
+                       rmin == rmax ? "same" : "DIFFERS");
                 fflush(stdout);
             }
             if (call == 0) { /* the same pattern and values, from the saved arrays */

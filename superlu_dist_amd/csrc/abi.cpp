@@ -75,6 +75,23 @@ const Mpi &mpi() {
     return m;
 }
 
+// The HSA runtime seeds and draws libc rand() when it creates a queue (every
+// HIP stream, RCCL's too).  The reference's pddistribute draws the seeds of
+// its solve's broadcast / reduction trees from rand() on every rank
+// (SRC/pddistribute.c:1557, 1729) and needs every rank to draw the same
+// sequence: a rank whose sequence moved builds other trees than its peers,
+// and pdgstrs then returns garbage on every later system in the process.
+// Every entry point therefore runs on a private random() state and hands the
+// caller's back untouched (tests/test_dropin.py, the grid life-cycle tests).
+struct CallerRandState {
+    char buf[256];
+    char *prev;
+    CallerRandState() : prev(initstate(1u, buf, sizeof buf)) {}
+    ~CallerRandState() { setstate(prev); }
+    CallerRandState(const CallerRandState &) = delete;
+    CallerRandState &operator=(const CallerRandState &) = delete;
+};
+
 // SUPERLU_MI355X_SEGV_TRACE=1 (diagnostics): a host backtrace on SIGSEGV
 void segv_trace(int sig) {
     void *fr[64];
@@ -115,11 +132,14 @@ struct GridComm {
     int nprow = 0, npcol = 0, iam = -1;
     MPI_Comm comms[3]; // grid, process row, process column
     bool host = false;
+    int64_t nbc[3] = {0, 0, 0}, nbytes[3] = {0, 0, 0}; // host broadcasts per group
 };
 
 int mpi_host_bcast(void *ctx, int group, int root, void *buf, int64_t bytes) {
     GridComm *g = (GridComm *)ctx;
     char *p = (char *)buf;
+    ++g->nbc[group];
+    g->nbytes[group] += bytes;
     while (bytes > 0) {
         const int n = (int)std::min<int64_t>(bytes, 1 << 30);
         if (mpi().bcast(p, n, MPI_BYTE, root, g->comms[group]) != MPI_SUCCESS) return 1;
@@ -132,6 +152,7 @@ int mpi_host_bcast(void *ctx, int group, int root, void *buf, int64_t bytes) {
 void evict_for_comm(slu_comm *c); // (plan cache, below)
 
 int grid_attr_delete(MPI_Comm, int, void *val, void *) {
+    CallerRandState rs;
     GridComm *g = (GridComm *)val;
     evict_for_comm(g->c); // a cached plan must never outlive its transport
     slu_comm_destroy(g->c);
@@ -194,6 +215,32 @@ slu_comm *comm_for_grid(gridinfo_t *grid) {
     }
     M.set_attr(grid->comm, g_keyval, g); // replaces (and deletes) a stale entry
     return g->c;
+}
+
+// SLU_BCAST_TRACE=1 (diagnostics): every rank's host-broadcast count and
+// bytes per group so far, compared across each group's members
+void trace_bcasts(gridinfo_t *grid, const char *where) {
+    const char *e = getenv("SLU_BCAST_TRACE");
+    if (!e || atoi(e) != 1 || grid->nprow * grid->npcol == 1) return;
+    const Mpi &M = mpi();
+    void *val = nullptr;
+    int flag = 0;
+    M.get_attr(grid->comm, g_keyval, &val, &flag);
+    if (!flag) return;
+    GridComm *g = (GridComm *)val;
+    const char *gn[3] = {"grid", "row", "column"};
+    for (int k = 0; k < 3; ++k) {
+        int P = 0;
+        int64_t mine[2] = {g->nbc[k], g->nbytes[k]};
+        const int sz = k == 0 ? (int)(grid->nprow * grid->npcol) : k == 1 ? (int)grid->npcol : (int)grid->nprow;
+        P = sz;
+        std::vector<int64_t> all(2 * (size_t)P);
+        M.allgather(mine, 2, MPI_LONG_LONG, all.data(), 2, MPI_LONG_LONG, g->comms[k]);
+        bool same = true;
+        for (int q = 1; q < P; ++q) same = same && all[2 * q] == all[0] && all[2 * q + 1] == all[1];
+        fprintf(stderr, "[slu bcast %s] rank %d %s group: %lld broadcasts, %lld bytes%s\n", where, (int)grid->iam,
+                gn[k], (long long)mine[0], (long long)mine[1], same ? "" : "  MISMATCH in this group");
+    }
 }
 
 // The plan's HBM (the factors' device copy, index tables, staging) is
@@ -609,6 +656,7 @@ int_t pxgstrf(int dtype, const char *name, superlu_dist_options_t *options, int 
             reap_later(plan);
         }
         plan = nullptr;
+        trace_bcasts(grid, name);
         int gi = myinfo ? myinfo : n + 1;
         if (grid->nprow * grid->npcol > 1) {
             int in = gi;
@@ -663,6 +711,7 @@ int mpi_host_p2p(void *ctx, int nops, const slu_host_p2p_op *ops) {
 }
 
 int grid3_attr_delete(MPI_Comm, int, void *val, void *) {
+    CallerRandState rs;
     Grid3Comm *g = (Grid3Comm *)val;
     slu_comm_destroy(g->c);
     delete g;
@@ -1234,32 +1283,38 @@ extern "C" {
 
 int_t pdgstrf(superlu_dist_options_t *options, int m, int n, double anorm,
               dLUstruct_t *LUstruct, gridinfo_t *grid, SuperLUStat_t *stat, int *info) {
+    CallerRandState rs;
     return pxgstrf(SLU_D, "PDGSTRF", options, m, n, anorm, LUstruct, grid, stat, info);
 }
 int_t psgstrf(superlu_dist_options_t *options, int m, int n, float anorm,
               sLUstruct_t *LUstruct, gridinfo_t *grid, SuperLUStat_t *stat, int *info) {
+    CallerRandState rs;
     return pxgstrf(SLU_S, "PSGSTRF", options, m, n, (double)anorm, LUstruct, grid, stat, info);
 }
 int_t pzgstrf(superlu_dist_options_t *options, int m, int n, double anorm,
               zLUstruct_t *LUstruct, gridinfo_t *grid, SuperLUStat_t *stat, int *info) {
+    CallerRandState rs;
     return pxgstrf(SLU_Z, "PZGSTRF", options, m, n, anorm, LUstruct, grid, stat, info);
 }
 
 int_t pdgstrf3d(superlu_dist_options_t *options, int m, int n, double anorm,
                 dtrf3Dpartition_t *trf3Dpartition, SCT_t *, dLUstruct_t *LUstruct,
                 gridinfo3d_t *grid3d, SuperLUStat_t *stat, int *info) {
+    CallerRandState rs;
     return pxgstrf3d(SLU_D, "PDGSTRF3D", options, m, n, anorm, trf3Dpartition, LUstruct, grid3d,
                      stat, info);
 }
 int_t psgstrf3d(superlu_dist_options_t *options, int m, int n, float anorm,
                 strf3Dpartition_t *trf3Dpartition, SCT_t *, sLUstruct_t *LUstruct,
                 gridinfo3d_t *grid3d, SuperLUStat_t *stat, int *info) {
+    CallerRandState rs;
     return pxgstrf3d(SLU_S, "PSGSTRF3D", options, m, n, (double)anorm, trf3Dpartition, LUstruct,
                      grid3d, stat, info);
 }
 int_t pzgstrf3d(superlu_dist_options_t *options, int m, int n, double anorm,
                 ztrf3Dpartition_t *trf3Dpartition, SCT_t *, zLUstruct_t *LUstruct,
                 gridinfo3d_t *grid3d, SuperLUStat_t *stat, int *info) {
+    CallerRandState rs;
     return pxgstrf3d(SLU_Z, "PZGSTRF3D", options, m, n, anorm, trf3Dpartition, LUstruct, grid3d,
                      stat, info);
 }
@@ -1268,6 +1323,7 @@ void pdgstrs(superlu_dist_options_t *, int_t n, dLUstruct_t *LUstruct,
              xScalePermstruct_t *ScalePermstruct, gridinfo_t *grid, double *B, int_t m_loc,
              int_t fst_row, int_t ldb, int nrhs, xSOLVEstruct_t *, SuperLUStat_t *stat,
              int *info) {
+    CallerRandState rs;
     pxgstrs(SLU_D, "PDGSTRS", n, LUstruct, ScalePermstruct, grid, B, m_loc, fst_row, ldb, nrhs,
             stat, info);
 }
@@ -1275,6 +1331,7 @@ void psgstrs(superlu_dist_options_t *, int_t n, sLUstruct_t *LUstruct,
              xScalePermstruct_t *ScalePermstruct, gridinfo_t *grid, float *B, int_t m_loc,
              int_t fst_row, int_t ldb, int nrhs, xSOLVEstruct_t *, SuperLUStat_t *stat,
              int *info) {
+    CallerRandState rs;
     pxgstrs(SLU_S, "PSGSTRS", n, LUstruct, ScalePermstruct, grid, B, m_loc, fst_row, ldb, nrhs,
             stat, info);
 }
@@ -1282,24 +1339,28 @@ void pzgstrs(superlu_dist_options_t *, int_t n, zLUstruct_t *LUstruct,
              xScalePermstruct_t *ScalePermstruct, gridinfo_t *grid, doublecomplex *B,
              int_t m_loc, int_t fst_row, int_t ldb, int nrhs, xSOLVEstruct_t *,
              SuperLUStat_t *stat, int *info) {
+    CallerRandState rs;
     pxgstrs(SLU_Z, "PZGSTRS", n, LUstruct, ScalePermstruct, grid, B, m_loc, fst_row, ldb, nrhs,
             stat, info);
 }
 float pddistribute(superlu_dist_options_t *options, int_t n, SuperMatrix *A,
                    xScalePermstruct_t *ScalePermstruct, Glu_freeable_t *Glu_freeable,
                    dLUstruct_t *LUstruct, gridinfo_t *grid) {
+    CallerRandState rs;
     return pxdistribute<double>(SLU_D, "PDDISTRIBUTE", options, n, A, ScalePermstruct, Glu_freeable,
                                 LUstruct, grid);
 }
 float psdistribute(superlu_dist_options_t *options, int_t n, SuperMatrix *A,
                    xScalePermstruct_t *ScalePermstruct, Glu_freeable_t *Glu_freeable,
                    sLUstruct_t *LUstruct, gridinfo_t *grid) {
+    CallerRandState rs;
     return pxdistribute<float>(SLU_S, "PSDISTRIBUTE", options, n, A, ScalePermstruct, Glu_freeable,
                                LUstruct, grid);
 }
 float pzdistribute(superlu_dist_options_t *options, int_t n, SuperMatrix *A,
                    xScalePermstruct_t *ScalePermstruct, Glu_freeable_t *Glu_freeable,
                    zLUstruct_t *LUstruct, gridinfo_t *grid) {
+    CallerRandState rs;
     return pxdistribute<doublecomplex>(SLU_Z, "PZDISTRIBUTE", options, n, A, ScalePermstruct,
                                        Glu_freeable, LUstruct, grid);
 }

@@ -294,6 +294,14 @@ def test_factored_solve_after_eviction_with_host_factors():
 # and the cached plan built on them goes with them: the
 # next round's first call builds a new plan even when MPI reuses the
 # communicator handle and malloc the LUstruct addresses.
+#
+# The second system in a process also needs the caller's libc rand()
+# sequence to be the same on every rank: the reference's pddistribute draws
+# its solve trees' seeds from it (SRC/pddistribute.c:1557), and the HSA
+# runtime reseeds it whenever it creates a queue (any HIP stream).  The
+# driver draws one rand() per rank after every pdgssvx and reports whether
+# the ranks agree ("rand same"); without the library's guard the ranks'
+# sequences part after the first factorization and round 1's solve errs ~1.
 def _regrid(nprocs, pr, pc, **extra):
     env = dict(os.environ)
     env.update({"OMP_NUM_THREADS": "1", "MKL_NUM_THREADS": "1", "MKL_THREADING_LAYER": "SEQUENTIAL",
@@ -321,6 +329,7 @@ def test_grid_exit_evicts_the_cached_plan(pr, pc):
     assert len(res) == 4, out[-3000:]
     for _, _, info, err in res:
         assert int(info) == 0 and float(err) < 1e-10, summary + "\n" + out[-2500:]
+    assert re.findall(r"err [0-9.eE+-]+ rand (\w+)", out) == ["same"] * 4, out[-3000:]
     # rank 0's plan per call: built, reused, then (new grid) built, reused
     plans = re.findall(r"\[PDGSTRF rank 0\] digest [0-9.]+ ms, plan (built|reused)", out)
     if pr * pc > 1:
@@ -368,3 +377,18 @@ def test_grid_refactorization_without_plan_cache():
     res = re.findall(r"round (\d) call (\d): info (\d+) err ([0-9.eE+-]+)", out)
     summary = "\n".join(f"round {a} call {b}: info {c} err {d}" for a, b, c, d in res)
     assert len(res) == 4 and all(int(i) == 0 and float(e) < 1e-10 for _, _, i, e in res), summary
+    assert re.findall(r"err [0-9.eE+-]+ rand (\w+)", out) == ["same"] * 4, out[-3000:]
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not _have("regrid"), reason="grid life-cycle driver not built")
+def test_second_system_on_the_same_grid():
+    """Two systems one after the other on ONE 2x2 grid (REGRID_SAMEGRID:
+    new LUstruct / SOLVEstruct, same communicators): the second solve is
+    as accurate as the first and the ranks' rand() sequences agree."""
+    rc, out = _regrid(4, 2, 2, REGRID_SAMEGRID="1")
+    assert rc == 0, out[-3000:]
+    res = re.findall(r"round (\d) call (\d): info (\d+) err ([0-9.eE+-]+) rand (\w+)", out)
+    summary = "\n".join(" ".join(r) for r in res)
+    assert len(res) == 4 and all(int(i) == 0 and float(e) < 1e-10 and rs == "same"
+                                 for _, _, i, e, rs in res), summary
