@@ -149,8 +149,11 @@ def run_reference(A, perm_c, nprow, npcol, relax=60, maxsup=256, lookahead=10,
         write_matrix_bin(mfile, A, perm_c)
         outp = os.path.join(tmp, "out") if want_factors else None
         env = dict(os.environ)
+        # SLU_SYMB_DEVICE=0: the harness's symbolic stage stays on the host
+        # (its ranks must not open the GPU: the box allows 16 processes per
+        # GPU, and a 16-rank reference run beside the bench would be 17)
         env.update({"MPICH_CC": "gcc", "OMP_NUM_THREADS": str(omp_threads),
-                    "MKL_NUM_THREADS": "1", "MKL_THREADING_LAYER": "SEQUENTIAL",
+                    "MKL_NUM_THREADS": "1", "MKL_THREADING_LAYER": "SEQUENTIAL", "SLU_SYMB_DEVICE": "0",
                     "LD_LIBRARY_PATH": "/usr/lib/x86_64-linux-gnu:/opt/rocm/lib:" + CONDA + "/lib:" + env.get("LD_LIBRARY_PATH", "")})
         cmd = [os.path.join(CONDA, "bin", "mpiexec"), "-n", str(nprow * npcol), REF_BIN,
                "-lib", LIB_PATH, "-f", mfile, "-r", str(nprow), "-c", str(npcol),
