@@ -1632,3 +1632,4 @@ k_trsm_reg(const TrsmItemF<T> *items) {
 }
 
 } // namespace slu
+#include "schur_pers.h"
