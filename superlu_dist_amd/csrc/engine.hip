@@ -2781,27 +2781,7 @@ struct Plan : PlanBase {
                                R.df_n, d_dsflags.p + (size_t)R.df_off * DS_MAXS, ds_epoch, d_counters.p + 1, thresh,
                                opts.replace_tiny_pivot, d_counters.p, d_zpiv.p);
     }
-    // SLU_SB_PERSIST=1 (fp64): k_schur_pers, two resident workgroups per CU
-    // taking tiles from a per-launch counter (schur_pers.h)
-    int sb_persist = getenv("SLU_SB_PERSIST") ? atoi(getenv("SLU_SB_PERSIST")) : 0;
-    int sb_pers_wgs = getenv("SLU_SB_PERSIST_WGS") ? atoi(getenv("SLU_SB_PERSIST_WGS")) : 2;
-    DevBuf<unsigned> d_tctr; // one counter per persistent launch of a factorization
-    int tctr_next = 0, n_cu = 0;
     void launch_big(const LevelRange &R, int off, int cnt, hipStream_t st) {
-        if constexpr (std::is_same<T, double>::value) {
-            if (sb_persist && tctr_next < (int)d_tctr.n) {
-                if (!n_cu) {
-                    int dev = 0;
-                    HIPCHK(hipGetDevice(&dev));
-                    HIPCHK(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
-                }
-                const int g = std::min(cnt, std::max(1, sb_pers_wgs * n_cu));
-                hipLaunchKernelGGL(k_schur_pers<T>, dim3(g), dim3(BigCfg<T>::THREADS), 0, st,
-                                   d_tiles_big.p + off, d_kinfo.p + R.k_off, d_L.p, d_U.p, d_lblk.p, d_lmap.p,
-                                   d_ublk.p, d_ucol_voff.p, d_ucol_fst.p, cnt, d_tctr.p + tctr_next++);
-                return;
-            }
-        }
         hipLaunchKernelGGL(k_schur_big<T>, dim3(cnt), dim3(BigCfg<T>::THREADS), 0, st,
                            d_tiles_big.p + off, d_kinfo.p + R.k_off, d_L.p, d_U.p,
                            d_lblk.p, d_lmap.p, d_ublk.p, d_ucol_voff.p, d_ucol_fst.p);
@@ -2838,13 +2818,6 @@ struct Plan : PlanBase {
         const float s_eps = 5.9604644775390625e-08f; // FLT_EPSILON * 0.5
         double thresh = sizeof(T) == 4 ? (double)(float)(s_eps * (float)anorm) : (double)s_eps * anorm;
         HIPCHK(hipMemsetAsync(d_counters.p, 0, d_counters.bytes(), stream));
-        if (sb_persist && std::is_same<T, double>::value) {
-            // (3 launches of big tiles per level at most: critical, split, rest)
-            const size_t need = levels.size() * (size_t)(2 + std::max(1, rest_chunks)) + 8;
-            if (d_tctr.n < need) d_tctr.alloc(need);
-            HIPCHK(hipMemsetAsync(d_tctr.p, 0, d_tctr.bytes(), stream));
-            tctr_next = 0;
-        }
         if (++ds_epoch >= 0x7fffffffu) { // (strip flags: a new epoch per factorization)
             HIPCHK(hipMemsetAsync(d_dsflags.p, 0, d_dsflags.bytes(), stream));
             ds_epoch = 1;

@@ -1632,4 +1632,3 @@ k_trsm_reg(const TrsmItemF<T> *items) {
 }
 
 } // namespace slu
-#include "schur_pers.h"

@@ -46,7 +46,7 @@ template <typename T>
 __global__ void __launch_bounds__(BigCfg<T>::THREADS, BigCfg<T>::MINW)
 k_schur_pers(const TileItem *tiles, const KInfo<T> *kinfo, T *Lval, T *Uval, const LBlk *lblk,
              const int *lmap, const UBlk *ublk, const int64_t *ucol_voff, const int *ucol_fst,
-             int ntiles, unsigned *tctr) {
+             int ntiles, unsigned *tctr, int prefetch) {
     static_assert(std::is_same<T, double>::value, "k_schur_pers: fp64 tiles only");
     using Sx = S<T>;
     using M = Mma<T>;
@@ -308,7 +308,7 @@ k_schur_pers(const TileItem *tiles, const KInfo<T> *kinfo, T *Lval, T *Uval, con
 #pragma unroll
                     for (int bl = 0; bl < SB_TB; ++bl) rl[bl] = s_rl[bl * SB_BM + r];
                     next_descriptor();
-                    if (tn < ntiles) {
+                    if (prefetch && tn < ntiles) {
                         next_tables();
                         meta_n = true;
                     }
