@@ -43,6 +43,7 @@
 #include "common.h"
 #include "kernels.h"
 #include "diag_strips.h"
+#include "diag_wave.h"
 #include "fill.h"
 #include "solve.h"
 #include "hostio.h"
@@ -2775,6 +2776,21 @@ struct Plan : PlanBase {
         if (cplx || strips_mode == 0) return false;
         return strips_mode == 2 || (R.df_maxw > DF_SMALLW && R.df_n <= strips_max);
     }
+    // k_diag_lu_w (diag_wave.h): one wave per narrow diagonal block, real
+    // types (SLU_DIAG_WAVE=0: k_diag_lu_f's 256-thread path instead)
+    int diag_wave = getenv("SLU_DIAG_WAVE") ? atoi(getenv("SLU_DIAG_WAVE")) : 1;
+    bool diag_wave_ok() const { return !cplx && diag_wave != 0; }
+    void launch_diag_wave(const LevelRange &R, double thresh, hipStream_t st) {
+        if constexpr (!cplx) {
+            const dim3 g((unsigned)((R.df_n + DW_WAVES - 1) / DW_WAVES)), b(64 * DW_WAVES);
+            if (R.df_maxw <= 32)
+                hipLaunchKernelGGL((k_diag_lu_w<T, 32>), g, b, 0, st, d_df.p + R.df_off, R.df_n, thresh,
+                                   opts.replace_tiny_pivot, d_counters.p, d_zpiv.p);
+            else
+                hipLaunchKernelGGL((k_diag_lu_w<T, 64>), g, b, 0, st, d_df.p + R.df_off, R.df_n, thresh,
+                                   opts.replace_tiny_pivot, d_counters.p, d_zpiv.p);
+        }
+    }
     void launch_strips(const LevelRange &R, double thresh, hipStream_t st) {
         if constexpr (!cplx)
             hipLaunchKernelGGL(k_diag_strips<T>, dim3(ds_grid(R.df_n)), dim3(DS_THREADS), 0, st, d_df.p + R.df_off,
@@ -2894,6 +2910,8 @@ struct Plan : PlanBase {
                 span(0, P, [&] {
                     if (strips_ok(R))
                         launch_strips(R, thresh, P);
+                    else if (R.df_maxw <= DF_SMALLW && diag_wave_ok())
+                        launch_diag_wave(R, thresh, P);
                     else if (R.df_maxw <= DF_SMALLW)
                         hipLaunchKernelGGL((k_diag_lu_f<T, DF_SMALLW, DF_SMALL_THREADS>), dim3(R.df_n),
                                            dim3(DF_SMALL_THREADS), 0, P, d_df.p + R.df_off, thresh,
