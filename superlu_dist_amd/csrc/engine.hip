@@ -490,6 +490,7 @@ struct LevelRange {
     int bigc_n = 0, tilec_n = 0; // critical tiles (destinations in the next level's panels)
     int df_off = 0, df_n = 0;   // fast diag items
     int df_maxw = 0;            // widest of them
+    int tf_maxw = 0;            // widest supernode of the fast L / U panel TRSM items
     int lf_off = 0, lf_n = 0;   // fast L-panel TRSM items
     int uf_off = 0, uf_n = 0;   // fast U-panel TRSM items
     int dc_off = 0, dc_n = 0;   // diag-package copy items (2D grids)
@@ -2033,6 +2034,8 @@ struct Plan : PlanBase {
             for (int i = R.df_off; i < R.df_off + R.df_n; ++i) R.df_maxw = std::max(R.df_maxw, df_items[i].w);
             R.lf_n = (int)(B1[V_LF] - B0[V_LF]);
             R.uf_n = (int)(B1[V_UF] - B0[V_UF]);
+            for (int i = R.lf_off; i < R.lf_off + R.lf_n; ++i) R.tf_maxw = std::max(R.tf_maxw, lf_items[i].w);
+            for (int i = R.uf_off; i < R.uf_off + R.uf_n; ++i) R.tf_maxw = std::max(R.tf_maxw, uf_items[i].w);
             R.diag_n = (int)(B1[V_DIAG] - B0[V_DIAG]);
             R.tl_n = (int)(B1[V_TL] - B0[V_TL]);
             R.tu_n = (int)(B1[V_TU] - B0[V_TU]);
@@ -2737,6 +2740,8 @@ struct Plan : PlanBase {
         }
     }
 
+    // SLU_TRSM_NARROW=0: the 256-wide k_trsm_reg on narrow levels too
+    int trsm_narrow = getenv("SLU_TRSM_NARROW") ? atoi(getenv("SLU_TRSM_NARROW")) : 1;
     void launch_trsm_fast(const LevelRange &R, hipStream_t st) {
         if constexpr (cplx) {
             if (R.lf_n)
@@ -2744,6 +2749,14 @@ struct Plan : PlanBase {
                                    d_lf.p + R.lf_off);
             if (R.uf_n)
                 hipLaunchKernelGGL((k_trsm_blk<T, 1>), dim3(R.uf_n), dim3(256), 0, st,
+                                   d_uf.p + R.uf_off);
+        } else if (R.tf_maxw <= 64 && trsm_narrow) {
+            // narrow levels: the 64-wide instantiation (several workgroups per CU)
+            if (R.lf_n)
+                hipLaunchKernelGGL((k_trsm_reg<T, 0, 64>), dim3(R.lf_n), dim3(64 * TR_WAVES), 0, st,
+                                   d_lf.p + R.lf_off);
+            if (R.uf_n)
+                hipLaunchKernelGGL((k_trsm_reg<T, 1, 64>), dim3(R.uf_n), dim3(64 * TR_WAVES), 0, st,
                                    d_uf.p + R.uf_off);
         } else {
             if (R.lf_n)

@@ -1526,10 +1526,14 @@ k_schur_big(const TileItem *tiles, const KInfo<T> *kinfo, T *Lval, T *Uval,
 // LDS), Z = X_b - acc, X_b = Z Dinv_b; results return to A layout through a
 // per-wave LDS tile.  Same MODE convention as k_trsm_blk.
 constexpr int TR_WAVES = 4;
-template <typename T, int MODE>
-__global__ void __launch_bounds__(64 * TR_WAVES, 1)
+// MAXW: the widest supernode of the launch's items.  The narrow levels
+// (MAXW 64: 16 row registers, 17 KB of LDS) run several workgroups per CU
+// where the 256-wide form (64 registers, 68 KB) runs one.
+template <typename T, int MODE, int MAXW = FAST_MAXW>
+__global__ void __launch_bounds__(64 * TR_WAVES, MAXW <= 64 ? 4 : 1)
 k_trsm_reg(const TrsmItemF<T> *items) {
-    constexpr int PW = 32, NKS = FAST_MAXW / 4, NBMAX = FAST_MAXW / PW;
+    constexpr int PW = 32, NKS = MAXW / 4, NBMAX = MAXW / PW;
+    constexpr int TROWS = MAXW - PW > TR_WAVES * 16 ? MAXW - PW : TR_WAVES * 16; // sT rows
     using Sx = S<T>;
     using M = Mma<T>;
     const TrsmItemF<T> it = items[blockIdx.x];
@@ -1539,8 +1543,8 @@ k_trsm_reg(const TrsmItemF<T> *items) {
     // sT, which the block's MFMAs have read by then (a barrier separates
     // them): 68 KB of LDS instead of 85, so the kernel fits beside a Schur
     // workgroup (engine.hip, rest_split)
-    __shared__ T sT[FAST_MAXW - PW][PW + 1];
-    static_assert(TR_WAVES * 16 <= FAST_MAXW - PW, "sW inside sT");
+    __shared__ T sT[TROWS][PW + 1];
+    static_assert(TR_WAVES * 16 <= TROWS, "sW inside sT");
     T (*W)[PW + 1] = sT + wid * 16;
     __shared__ T sD[PW][PW + 1];
     const int rl = lane & 15, kq = lane >> 4;
