@@ -2740,8 +2740,10 @@ struct Plan : PlanBase {
         }
     }
 
-    // SLU_TRSM_NARROW=0: the 256-wide k_trsm_reg on narrow levels too
-    int trsm_narrow = getenv("SLU_TRSM_NARROW") ? atoi(getenv("SLU_TRSM_NARROW")) : 1;
+    // SLU_TRSM_NARROW: 0 the 256-wide k_trsm_reg everywhere, 1 the 64-wide
+    // instantiation for levels whose TRSM supernodes are <= 64 wide, 2 (default)
+    // also the 128-wide one for <= 128
+    int trsm_narrow = getenv("SLU_TRSM_NARROW") ? atoi(getenv("SLU_TRSM_NARROW")) : 2;
     void launch_trsm_fast(const LevelRange &R, hipStream_t st) {
         if constexpr (cplx) {
             if (R.lf_n)
@@ -2757,6 +2759,13 @@ struct Plan : PlanBase {
                                    d_lf.p + R.lf_off);
             if (R.uf_n)
                 hipLaunchKernelGGL((k_trsm_reg<T, 1, 64>), dim3(R.uf_n), dim3(64 * TR_WAVES), 0, st,
+                                   d_uf.p + R.uf_off);
+        } else if (R.tf_maxw <= 128 && trsm_narrow >= 2) {
+            if (R.lf_n)
+                hipLaunchKernelGGL((k_trsm_reg<T, 0, 128>), dim3(R.lf_n), dim3(64 * TR_WAVES), 0, st,
+                                   d_lf.p + R.lf_off);
+            if (R.uf_n)
+                hipLaunchKernelGGL((k_trsm_reg<T, 1, 128>), dim3(R.uf_n), dim3(64 * TR_WAVES), 0, st,
                                    d_uf.p + R.uf_off);
         } else {
             if (R.lf_n)

@@ -1530,7 +1530,7 @@ constexpr int TR_WAVES = 4;
 // (MAXW 64: 16 row registers, 17 KB of LDS) run several workgroups per CU
 // where the 256-wide form (64 registers, 68 KB) runs one.
 template <typename T, int MODE, int MAXW = FAST_MAXW>
-__global__ void __launch_bounds__(64 * TR_WAVES, MAXW <= 64 ? 4 : 1)
+__global__ void __launch_bounds__(64 * TR_WAVES, MAXW <= 64 ? 4 : MAXW <= 128 ? 2 : 1)
 k_trsm_reg(const TrsmItemF<T> *items) {
     constexpr int PW = 32, NKS = MAXW / 4, NBMAX = MAXW / PW;
     constexpr int TROWS = MAXW - PW > TR_WAVES * 16 ? MAXW - PW : TR_WAVES * 16; // sT rows
