@@ -2268,13 +2268,32 @@ struct Plan : PlanBase {
             }
         ki.pair = (const int *)(intptr_t)pair_off;
         ki.atomic = 0;
-        O.kinfos.push_back(ki);
-        O.khost.push_back(std::move(kh));
-        const int slot = (int)O.kinfos.size() - 1; // relocated by the merge
         constexpr int BBN = BigCfg<T>::BN; // 128 (d, s) or 64 (z) columns per big tile
         const bool big = m >= SB_BM && ncols >= BBN;
         const int BM = big ? SB_BM : SC_BM, BN = big ? BBN : SC_BN;
         const int tm = (m + BM - 1) / BM, tn = (ncols + BN - 1) / BN;
+        // K split near the root: a level of one or two supernodes whose
+        // update is a few 128 x 128 tiles leaves most CUs idle for a whole
+        // tile's latency (K up to 256: ~90 us).  Its K range is cut into
+        // chunks of >= 64, one KInfo per chunk (same tables, kmin / kw
+        // moved); the chunks' tiles add into the same destinations, which
+        // the level's conflict analysis below turns into atomic scatters.
+        int nsplit = 1;
+        if (ksplit_tiles > 0 && big && bylev[level_of[k]].size() <= 2 && tm * tn < ksplit_tiles)
+            nsplit = std::max(1, std::min({4, (w - kmin) / 64, ksplit_tiles / (tm * tn)}));
+        const int kch = ((w - kmin + nsplit - 1) / nsplit + 15) / 16 * 16;
+        const int slot0 = (int)O.kinfos.size(); // relocated by the merge
+        for (int c = 0; c < nsplit; ++c) {
+            KInfo<T> kc = ki;
+            kc.kmin = kmin + c * kch;
+            kc.kw = std::min(kch, w - kc.kmin);
+            if (kc.kw <= 0) {
+                nsplit = c;
+                break;
+            }
+            O.kinfos.push_back(kc);
+            O.khost.push_back(kh);
+        }
         // A destination (ib,jb) belongs to the panel of supernode min(ib,jb);
         // it is critical when that panel is factored at the next level.  All
         // destinations in a row of L block ib (resp. a column of U block jb)
@@ -2285,11 +2304,12 @@ struct Plan : PlanBase {
             if (level_of[lib_[O.h_ra[rows_off + r]]] == nl) crow[r / BM] = 1;
         for (int c = 0; c < ncols; ++c)
             if (level_of[ujb[O.h_cb[cols_off + c]]] == nl) ccol[c / BN] = 1;
-        for (int i = 0; i < tm; ++i)
-            for (int j = 0; j < tn; ++j) {
-                const int cls = (crow[i] || ccol[j]) ? 0 : 1;
-                (big ? O.big[cls] : O.small[cls]).push_back(TileItem{slot, i, j});
-            }
+        for (int c = 0; c < nsplit; ++c)
+            for (int i = 0; i < tm; ++i)
+                for (int j = 0; j < tn; ++j) {
+                    const int cls = (crow[i] || ccol[j]) ? 0 : 1;
+                    (big ? O.big[cls] : O.small[cls]).push_back(TileItem{slot0 + c, i, j});
+                }
         // algorithmic work: exact unpadded flops and padded flops
         double fl = 0;
         for (int c = 0; c < ncols; ++c) fl += 2.0 * m * (w - O.h_ct0[cols_off + c]);
@@ -2740,6 +2760,9 @@ struct Plan : PlanBase {
         }
     }
 
+    // SLU_KSPLIT_TILES: levels of <= 2 supernodes with fewer big tiles than
+    // this split their K range (0: off)
+    int ksplit_tiles = getenv("SLU_KSPLIT_TILES") ? atoi(getenv("SLU_KSPLIT_TILES")) : 128;
     // SLU_TRSM_NARROW: 0 the 256-wide k_trsm_reg everywhere, 1 the 64-wide
     // instantiation for levels whose TRSM supernodes are <= 64 wide, 2 (default)
     // also the 128-wide one for <= 128
