@@ -511,10 +511,8 @@ k_schur(const TileItem *tiles, const KInfo<T> *kinfo, T *Lval, T *Uval,
     constexpr int ALD = SC_BM + 1, BLD = SC_BN + 1, CLD = SC_BM + 1;
     constexpr int STAGE = SC_BK * ALD + SC_BK * BLD;
     constexpr int CSIZE = SC_BN * CLD;
-    __shared__ T smem[STAGE > CSIZE ? STAGE : CSIZE];
+    __shared__ T smem[2 * STAGE > CSIZE ? 2 * STAGE : CSIZE];
     __shared__ int s_rg[SC_BM], s_ra[SC_BM], s_cg[SC_BN], s_cb[SC_BN];
-    T *sA = smem, *sB = smem + SC_BK * ALD;
-
     if (tid < SC_BM) {
         int r = row0 + tid;
         s_rg[tid] = tid < mrows ? ki.rg[r] : 0;
@@ -534,10 +532,11 @@ k_schur(const TileItem *tiles, const KInfo<T> *kinfo, T *Lval, T *Uval,
         bt0 = ki.ct0[col0 + bc];
     }
     const T *ub = ki.ubase + bvoff - bt0; // ub[t] valid for t >= bt0
+    const int tlast = ki.kmin + ki.kw - 1;
     // A gather: thread owns row ar = tid & 63, k = (tid>>6) + 4*s
     const int ar = tid & 63, ak = tid >> 6;
     const bool avalid = ar < mrows;
-    const T *ap = ki.a + row0 + ar;
+    const T *ap = ki.a + row0 + (avalid ? ar : 0);
 
     typename M::acc_t acc[2][2];
 #pragma unroll
@@ -545,37 +544,52 @@ k_schur(const TileItem *tiles, const KInfo<T> *kinfo, T *Lval, T *Uval,
 #pragma unroll
         for (int b = 0; b < 2; ++b) acc[a][b] = M::zero();
 
-    for (int k0 = 0; k0 < ki.kw; k0 += SC_BK) {
-        __syncthreads();
+    // K staged SC_BK deep through two LDS buffers, the next stage's global
+    // loads (clamped in-bounds addresses, masked values) in flight during the
+    // current stage's MFMAs
+    T ra[SC_BK / 4], rb[4];
+    auto gload = [&](int k0) {
 #pragma unroll
         for (int s = 0; s < SC_BK / 4; ++s) {
-            int kk = ak + 4 * s;
-            int t = ki.kmin + k0 + kk;
-            T v = Sx::zero();
-            if (avalid && k0 + kk < ki.kw) v = ap[(int64_t)t * ki.lda];
-            sA[kk * ALD + ar] = v;
+            const int kk = k0 + ak + 4 * s;
+            ra[s] = keep_if(avalid & (kk < ki.kw), gld(ap + (int64_t)(ki.kmin + min(kk, ki.kw - 1)) * ki.lda));
         }
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-            int kk = bk + s;
-            int t = ki.kmin + k0 + kk;
-            T v = Sx::zero();
-            if (bvalid && k0 + kk < ki.kw && t >= bt0) v = ub[t];
-            sB[kk * BLD + bc] = v;
+            const int t = ki.kmin + k0 + bk + s;
+            rb[s] = keep_if(bvalid & (t <= tlast) & (t >= bt0), gld(ub + max(min(t, tlast), bt0)));
         }
-        __syncthreads();
+    };
+    auto lstore = [&](int buf) {
+        T *a = smem + buf * STAGE, *b = a + SC_BK * ALD;
+#pragma unroll
+        for (int s = 0; s < SC_BK / 4; ++s) a[(ak + 4 * s) * ALD + ar] = ra[s];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) b[(bk + s) * BLD + bc] = rb[s];
+    };
+    const int nst = (ki.kw + SC_BK - 1) / SC_BK;
+    gload(0);
+    __syncthreads(); // (the tables above)
+    lstore(0);
+    __syncthreads();
+    for (int st = 0; st < nst; ++st) {
+        const bool more = st + 1 < nst;
+        if (more) gload((st + 1) * SC_BK);
+        const T *a = smem + (st & 1) * STAGE, *b = a + SC_BK * ALD;
 #pragma unroll
         for (int ks = 0; ks < SC_BK; ks += M::KSTEP) {
             const int kl = ks + (lane >> 4);
-            T a0 = sA[kl * ALD + wr * 32 + (lane & 15)];
-            T a1 = sA[kl * ALD + wr * 32 + 16 + (lane & 15)];
-            T b0 = sB[kl * BLD + wc * 32 + (lane & 15)];
-            T b1 = sB[kl * BLD + wc * 32 + 16 + (lane & 15)];
+            T a0 = a[kl * ALD + wr * 32 + (lane & 15)];
+            T a1 = a[kl * ALD + wr * 32 + 16 + (lane & 15)];
+            T b0 = b[kl * BLD + wc * 32 + (lane & 15)];
+            T b1 = b[kl * BLD + wc * 32 + 16 + (lane & 15)];
             M::step(acc[0][0], a0, b0);
             M::step(acc[0][1], a0, b1);
             M::step(acc[1][0], a1, b0);
             M::step(acc[1][1], a1, b1);
         }
+        if (more) lstore((st + 1) & 1);
+        __syncthreads();
     }
     // ---- C tile through LDS, then column-contiguous scatter-subtract
     __syncthreads();
