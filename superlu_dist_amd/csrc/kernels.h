@@ -1135,8 +1135,15 @@ template <> struct BigCfg<zc> {
     static constexpr int THREADS = 512, WN = 2, MINW = 4, BN = 64, BK = 8, FN = 2, PASSW = 16;
 };
 // fp32: three workgroups per CU (6 waves per SIMD, <= 80 VGPRs; 42 KB LDS each)
+// (SLU_F32_BK / SLU_F32_MINW: A/B builds, tools/ab_build.sh)
+#ifndef SLU_F32_BK
+#define SLU_F32_BK 16
+#endif
+#ifndef SLU_F32_MINW
+#define SLU_F32_MINW 6
+#endif
 template <> struct BigCfg<float> {
-    static constexpr int THREADS = 512, WN = 2, MINW = 6, BN = 128, BK = 16, FN = 4, PASSW = 64;
+    static constexpr int THREADS = 512, WN = 2, MINW = SLU_F32_MINW, BN = 128, BK = SLU_F32_BK, FN = 4, PASSW = 64;
 };
 constexpr int SB_BN = BigCfg<double>::BN;
 constexpr int SB_THREADS = 512; // the 512-thread configurations (k_schur_big<float>, <zc>)

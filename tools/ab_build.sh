@@ -15,7 +15,7 @@ INC="-I../../include -I/opt/conda/include -I."
 /opt/rocm/bin/hipcc -O3 -gline-tables-only -fPIC -std=c++17 --offload-arch=gfx950 -munsafe-fp-atomics \
     $INC -Wno-unused-result $FLAGS -c engine.hip -o $OUT/obj/engine.o
 HOST=""
-for o in abi amalg amalg_grid distribute frontend symbolic ordering amalg_api; do HOST="$HOST ../lib/obj/$o.o"; done
+for o in abi amalg amalg_grid distribute frontend symbolic ordering amalg_api symbolic_dev; do HOST="$HOST ../lib/obj/$o.o"; done
 /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -Wl,--version-script=full.map \
     -o $OUT/libslu_mi355x_full.so $HOST $OUT/obj/engine.o -L/opt/rocm/lib -lamdhip64 -lrccl -ldl \
     -Wl,-rpath,/opt/rocm/lib
