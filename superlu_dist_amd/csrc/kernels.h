@@ -1547,6 +1547,9 @@ k_schur_big(const TileItem *tiles, const KInfo<T> *kinfo, T *Lval, T *Uval,
 // LDS), Z = X_b - acc, X_b = Z Dinv_b; results return to A layout through a
 // per-wave LDS tile.  Same MODE convention as k_trsm_blk.
 constexpr int TR_WAVES = 4;
+#ifndef TR_TU
+#define TR_TU 8 // T elements in flight per thread while a block is staged (A/B builds)
+#endif
 // MAXW: the widest supernode of the launch's items.  The narrow levels
 // (MAXW 64: 16 row registers, 17 KB of LDS) run several workgroups per CU
 // where the 256-wide form (64 registers, 68 KB) runs one.
@@ -1598,7 +1601,7 @@ k_trsm_reg(const TrsmItemF<T> *items) {
             [&](int e, T v) { sD[e / PW][e % PW] = v; });
         const int kr = b * PW;
         if (kr > 0)
-            stage_loop<64 * TR_WAVES, 8, T>(
+            stage_loop<64 * TR_WAVES, TR_TU, T>(
                 tid, kr * PW,
                 [&](int e, bool ok) {
                     const int ee = min(e, kr * PW - 1);
