@@ -492,6 +492,8 @@ k_trsm_u(const TrsmUItem<T> *items) {
 // through LDS 16 deep.  A = L rows (column-major, straight from lusup),
 // B = U segments gathered with zero padding above each segment's first row.
 constexpr int SC_BM = 64, SC_BN = 64, SC_BK = 16, SC_THREADS = 256;
+constexpr int SB_TB = 4; // epilogue tables: row blocks x column blocks per tile
+constexpr int SB_AEB = 4; // atomic scatters formed per batch (8: slower, DESIGN §8)
 
 template <typename T>
 __global__ void __launch_bounds__(SC_THREADS)
@@ -521,6 +523,25 @@ k_schur(const TileItem *tiles, const KInfo<T> *kinfo, T *Lval, T *Uval,
         int c = tid - SC_BM;
         s_cg[c] = c < ncols ? ki.cg[col0 + c] : 0;
         s_cb[c] = c < ncols ? ki.cb[col0 + c] : 0;
+    }
+    // destination tables (k_schur_big's fast path): the tile's rows lie in
+    // NA consecutive L blocks of the panel, its columns in NB consecutive U
+    // blocks; with NA, NB <= SB_TB every address is a column part plus a row
+    // part, resolved once per tile (the records come in with the first stage)
+    const int a0 = ki.ra[row0], b0 = ki.cb[col0];
+    const int NA = ki.ra[row0 + mrows - 1] - a0 + 1, NB = ki.cb[col0 + ncols - 1] - b0 + 1;
+    const bool tbl = NA <= SB_TB && NB <= SB_TB;
+    __shared__ int64_t s_db[SB_TB * SB_TB], s_dmb[SB_TB * SB_TB];
+    __shared__ int s_dld[SB_TB * SB_TB];
+    __shared__ int64_t s_cp[SB_TB * SC_BN]; // [row block][column] column parts
+    __shared__ int s_rl[SB_TB * SC_BM];     // [column block][row] lmap positions
+    if (tbl && tid >= SC_BM + SC_BN && tid < SC_BM + SC_BN + SB_TB * SB_TB) {
+        const int e = tid - SC_BM - SC_BN, al = e / SB_TB, bl = e % SB_TB;
+        DRec d{0, 0, -1, 0};
+        if (al < NA && bl < NB) d = ki.prec[(int64_t)(a0 + al) * ki.nub + b0 + bl];
+        s_db[e] = d.base;
+        s_dmb[e] = d.mb;
+        s_dld[e] = d.ld;
     }
     // B gather: thread owns column bc = tid>>2 and 4 consecutive k of the stage
     const int bc = tid >> 2, bk = (tid & 3) * 4;
@@ -572,9 +593,34 @@ k_schur(const TileItem *tiles, const KInfo<T> *kinfo, T *Lval, T *Uval,
     __syncthreads(); // (the tables above)
     lstore(0);
     __syncthreads();
+    static_assert(SB_TB * SC_BN == SC_THREADS && SB_TB * SC_BM == SC_THREADS, "one table entry per thread");
+    int64_t t_code = 0, t_uv = 0;
+    int t_fst = 0, t_rl = 0;
     for (int st = 0; st < nst; ++st) {
         const bool more = st + 1 < nst;
         if (more) gload((st + 1) * SC_BK);
+        if (!more && tbl) { // the destination tables' loads, beside the last stage's MFMAs
+            {
+                const int al = tid / SC_BN, c = tid % SC_BN;
+                if (al < NA && c < ncols) {
+                    const int bl = s_cb[c] - b0, rec = al * SB_TB + bl, ld = s_dld[rec];
+                    if (ld >= 0) {
+                        t_code = (s_db[rec] + (int64_t)s_cg[c] * ld) * 8 + 1 + bl;
+                    } else {
+                        const int64_t x = s_db[rec] + s_cg[c];
+                        t_uv = ucol_voff[x];
+                        t_fst = ucol_fst[x];
+                    }
+                }
+            }
+            {
+                const int bl = tid / SC_BM, rr = tid % SC_BM;
+                if (bl < NB && rr < mrows) {
+                    const int rec = (s_ra[rr] - a0) * SB_TB + bl;
+                    if (s_dld[rec] >= 0) t_rl = lmap[s_dmb[rec] + s_rg[rr]];
+                }
+            }
+        }
         const T *a = smem + (st & 1) * STAGE, *b = a + SC_BK * ALD;
 #pragma unroll
         for (int ks = 0; ks < SC_BK; ks += M::KSTEP) {
@@ -604,10 +650,48 @@ k_schur(const TileItem *tiles, const KInfo<T> *kinfo, T *Lval, T *Uval,
                 int c = wc * 32 + fn * 16 + (lane & 15);
                 sC[c * CLD + r] = M::get(acc[fm][fn], i);
             }
+    if (tbl) {
+        s_cp[tid] = t_code ? t_code : (t_uv - t_fst) * 8;
+        s_rl[tid] = t_rl;
+    }
     __syncthreads();
     const int r = tid & 63;
     if (r >= mrows) return;
     const int gr = s_rg[r], a = s_ra[r];
+    if (tbl) { // one LDS word per element besides the destination (k_schur_big)
+        int rl[SB_TB];
+#pragma unroll
+        for (int bl = 0; bl < SB_TB; ++bl) rl[bl] = s_rl[bl * SC_BM + r];
+        const int al = a - a0;
+        for (int c0 = tid >> 6; c0 < ncols; c0 += 4 * SB_AEB) {
+            T *dp[SB_AEB];
+            T v[SB_AEB];
+#pragma unroll
+            for (int j = 0; j < SB_AEB; ++j) {
+                const int c = c0 + 4 * j;
+                dp[j] = nullptr;
+                v[j] = Sx::zero();
+                if (c < ncols) {
+                    v[j] = sC[c * CLD + r];
+                    const int64_t code = s_cp[al * SC_BN + c];
+                    const int tag = (int)(code & 7);
+                    int rp = gr;
+                    rp = tag == 1 ? rl[0] : rp;
+                    rp = tag == 2 ? rl[1] : rp;
+                    rp = tag == 3 ? rl[2] : rp;
+                    rp = tag == 4 ? rl[3] : rp;
+                    dp[j] = (tag ? Lval : Uval) + ((code >> 3) + rp);
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < SB_AEB; ++j)
+                if (dp[j]) {
+                    if (ki.atomic) Sx::atomic_sub(dp[j], v[j]);
+                    else Sx::sub_to(dp[j], v[j]);
+                }
+        }
+        return;
+    }
     const int *prow = ki.pair + (int64_t)a * ki.nub;
     int lastb = -1, h = 0;
     int64_t rbase = 0; // L dest: colvoff + pos ; U dest: unused
@@ -1147,8 +1231,6 @@ template <> struct BigCfg<float> {
 };
 constexpr int SB_BN = BigCfg<double>::BN;
 constexpr int SB_THREADS = 512; // the 512-thread configurations (k_schur_big<float>, <zc>)
-constexpr int SB_TB = 4; // epilogue tables: row blocks x column blocks per tile
-constexpr int SB_AEB = 4; // atomic scatters formed per batch (8: slower, DESIGN §8)
 
 #ifdef SLU_SB_STAMP
 // Diagnostics build only (tools/ab_build.sh NAME "-DSLU_SB_STAMP"): per-tile
