@@ -583,8 +583,9 @@ struct Plan : PlanBase {
     int nlc = 0, nlr = 0;
     hipStream_t stream = nullptr;  // Schur updates that are off the critical path
     hipStream_t pstream = nullptr; // panels, exchanges, critical Schur tiles
+    hipStream_t ustream = nullptr; // the U panels' TRSM beside the L panels' (launch_trsm_fast)
     vector<hipEvent_t> ev_pan, ev_rest; // per level
-    hipEvent_t ev_start = nullptr, ev_pend = nullptr;
+    hipEvent_t ev_start = nullptr, ev_pend = nullptr, ev_tu0 = nullptr, ev_tu1 = nullptr;
     bool xmode = false; // 2D grid with exchanges
     Xport X;
 
@@ -749,6 +750,7 @@ struct Plan : PlanBase {
         HIPCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
         HIPCHK(hipStreamCreateWithPriority(&stream, hipStreamNonBlocking, prio_lo));
         HIPCHK(hipStreamCreateWithPriority(&pstream, hipStreamNonBlocking, prio_hi));
+        HIPCHK(hipStreamCreateWithPriority(&ustream, hipStreamNonBlocking, prio_hi));
         if (getenv("SLU_PROFILE_PLAN"))
             fprintf(stderr, "[slu plan %d] streams               %6.1f ms\n", iam, ms_since(ts0));
         X.s = pstream;
@@ -972,8 +974,11 @@ struct Plan : PlanBase {
         for (auto e : ev_rest) (void)hipEventDestroy(e);
         if (ev_start) (void)hipEventDestroy(ev_start);
         if (ev_pend) (void)hipEventDestroy(ev_pend);
+        if (ev_tu0) (void)hipEventDestroy(ev_tu0);
+        if (ev_tu1) (void)hipEventDestroy(ev_tu1);
         if (stream) (void)hipStreamDestroy(stream);
         if (pstream) (void)hipStreamDestroy(pstream);
+        if (ustream) (void)hipStreamDestroy(ustream);
     }
 
     // ------------------------------------------------------- local layout
@@ -2423,6 +2428,8 @@ struct Plan : PlanBase {
         }
         HIPCHK(hipEventCreateWithFlags(&ev_start, hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&ev_pend, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&ev_tu0, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&ev_tu1, hipEventDisableTiming));
         d_info.alloc(Pr * Pc);
         stats.lu_bytes = (double)(lval_total + uval_total) * sizeof(T);
         stats.index_bytes = (double)(d_lblk.bytes() + d_lmap.bytes() + d_ublk.bytes() +
@@ -2767,13 +2774,24 @@ struct Plan : PlanBase {
     // instantiation for levels whose TRSM supernodes are <= 64 wide, 2 (default)
     // also the 128-wide one for <= 128
     int trsm_narrow = getenv("SLU_TRSM_NARROW") ? atoi(getenv("SLU_TRSM_NARROW")) : 2;
+    // SLU_TRSM_2STREAM=1 (default): the U panel's TRSM on a stream of its
+    // own beside the L panel's (both only wait for the diagonal block; near
+    // the root each is a few slabs, latency-bound)
+    int trsm_2stream = getenv("SLU_TRSM_2STREAM") ? atoi(getenv("SLU_TRSM_2STREAM")) : 1;
     void launch_trsm_fast(const LevelRange &R, hipStream_t st) {
+        // the U launch on ustream when both panels have slabs
+        const bool two = trsm_2stream && ustream && st == pstream && R.lf_n && R.uf_n;
+        hipStream_t su = two ? ustream : st;
+        if (two) {
+            HIPCHK(hipEventRecord(ev_tu0, st));
+            HIPCHK(hipStreamWaitEvent(ustream, ev_tu0, 0));
+        }
         if constexpr (cplx) {
             if (R.lf_n)
                 hipLaunchKernelGGL((k_trsm_blk<T, 0>), dim3(R.lf_n), dim3(256), 0, st,
                                    d_lf.p + R.lf_off);
             if (R.uf_n)
-                hipLaunchKernelGGL((k_trsm_blk<T, 1>), dim3(R.uf_n), dim3(256), 0, st,
+                hipLaunchKernelGGL((k_trsm_blk<T, 1>), dim3(R.uf_n), dim3(256), 0, su,
                                    d_uf.p + R.uf_off);
         } else if (R.tf_maxw <= 64 && trsm_narrow) {
             // narrow levels: the 64-wide instantiation (several workgroups per CU)
@@ -2781,22 +2799,26 @@ struct Plan : PlanBase {
                 hipLaunchKernelGGL((k_trsm_reg<T, 0, 64>), dim3(R.lf_n), dim3(64 * TR_WAVES), 0, st,
                                    d_lf.p + R.lf_off);
             if (R.uf_n)
-                hipLaunchKernelGGL((k_trsm_reg<T, 1, 64>), dim3(R.uf_n), dim3(64 * TR_WAVES), 0, st,
+                hipLaunchKernelGGL((k_trsm_reg<T, 1, 64>), dim3(R.uf_n), dim3(64 * TR_WAVES), 0, su,
                                    d_uf.p + R.uf_off);
         } else if (R.tf_maxw <= 128 && trsm_narrow >= 2) {
             if (R.lf_n)
                 hipLaunchKernelGGL((k_trsm_reg<T, 0, 128>), dim3(R.lf_n), dim3(64 * TR_WAVES), 0, st,
                                    d_lf.p + R.lf_off);
             if (R.uf_n)
-                hipLaunchKernelGGL((k_trsm_reg<T, 1, 128>), dim3(R.uf_n), dim3(64 * TR_WAVES), 0, st,
+                hipLaunchKernelGGL((k_trsm_reg<T, 1, 128>), dim3(R.uf_n), dim3(64 * TR_WAVES), 0, su,
                                    d_uf.p + R.uf_off);
         } else {
             if (R.lf_n)
                 hipLaunchKernelGGL((k_trsm_reg<T, 0>), dim3(R.lf_n), dim3(64 * TR_WAVES), 0, st,
                                    d_lf.p + R.lf_off);
             if (R.uf_n)
-                hipLaunchKernelGGL((k_trsm_reg<T, 1>), dim3(R.uf_n), dim3(64 * TR_WAVES), 0, st,
+                hipLaunchKernelGGL((k_trsm_reg<T, 1>), dim3(R.uf_n), dim3(64 * TR_WAVES), 0, su,
                                    d_uf.p + R.uf_off);
+        }
+        if (two) {
+            HIPCHK(hipEventRecord(ev_tu1, ustream));
+            HIPCHK(hipStreamWaitEvent(st, ev_tu1, 0));
         }
     }
 
