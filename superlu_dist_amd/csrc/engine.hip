@@ -2778,6 +2778,9 @@ struct Plan : PlanBase {
     // own beside the L panel's (both only wait for the diagonal block; near
     // the root each is a few slabs, latency-bound)
     int trsm_2stream = getenv("SLU_TRSM_2STREAM") ? atoi(getenv("SLU_TRSM_2STREAM")) : 1;
+    // SLU_CRIT_2STREAM=1: a level's small critical tiles beside its big ones (measured
+    // neutral at 100^3, profiles/r05t2c/; off by default)
+    int crit_2stream = getenv("SLU_CRIT_2STREAM") ? atoi(getenv("SLU_CRIT_2STREAM")) : 0;
     void launch_trsm_fast(const LevelRange &R, hipStream_t st) {
         // the U launch on ustream when both panels have slabs
         const bool two = trsm_2stream && ustream && st == pstream && R.lf_n && R.uf_n;
@@ -3015,14 +3018,27 @@ struct Plan : PlanBase {
             HIPCHK(hipEventRecord(ev_pan[L], P));
             // critical tiles of L on the panel stream, after the rest of L-1
             if (L > 0) HIPCHK(hipStreamWaitEvent(P, ev_rest[L - 1], 0));
+            // big and small critical tiles side by side (the U-panel TRSM's
+            // stream carries the small ones; conflicting destinations within
+            // a level are atomic, the rest have one writer)
+            const bool two_c = crit_2stream && ustream && P == pstream && R.bigc_n && R.tilec_n;
+            hipStream_t PS = two_c ? ustream : P;
+            if (two_c) {
+                HIPCHK(hipEventRecord(ev_tu0, P));
+                HIPCHK(hipStreamWaitEvent(ustream, ev_tu0, 0));
+            }
             if (R.bigc_n) {
                 span(2, P, [&] { launch_big(R, R.big_off, R.bigc_n, P); });
                 stats.n_schur_launches++;
                 stats.n_schur_big_launches++;
             }
             if (R.tilec_n) {
-                span(3, P, [&] { launch_small(R, R.tile_off, R.tilec_n, P); });
+                span(3, PS, [&] { launch_small(R, R.tile_off, R.tilec_n, PS); });
                 stats.n_schur_launches++;
+            }
+            if (two_c) {
+                HIPCHK(hipEventRecord(ev_tu1, ustream));
+                HIPCHK(hipStreamWaitEvent(P, ev_tu1, 0));
             }
             // the rest of L on the Schur stream, once the panels of L exist
             HIPCHK(hipStreamWaitEvent(stream, ev_pan[L], 0));
