@@ -584,6 +584,8 @@ struct Plan : PlanBase {
     hipStream_t stream = nullptr;  // Schur updates that are off the critical path
     hipStream_t pstream = nullptr; // panels, exchanges, critical Schur tiles
     hipStream_t ustream = nullptr; // the U panels' TRSM beside the L panels' (launch_trsm_fast)
+    hipStream_t sstream = nullptr; // small rest tiles beside the big ones (SLU_REST_2STREAM)
+    hipEvent_t ev_sr0 = nullptr, ev_sr1 = nullptr;
     vector<hipEvent_t> ev_pan, ev_rest; // per level
     hipEvent_t ev_start = nullptr, ev_pend = nullptr, ev_tu0 = nullptr, ev_tu1 = nullptr;
     bool xmode = false; // 2D grid with exchanges
@@ -751,6 +753,7 @@ struct Plan : PlanBase {
         HIPCHK(hipStreamCreateWithPriority(&stream, hipStreamNonBlocking, prio_lo));
         HIPCHK(hipStreamCreateWithPriority(&pstream, hipStreamNonBlocking, prio_hi));
         HIPCHK(hipStreamCreateWithPriority(&ustream, hipStreamNonBlocking, prio_hi));
+        HIPCHK(hipStreamCreateWithPriority(&sstream, hipStreamNonBlocking, prio_lo));
         if (getenv("SLU_PROFILE_PLAN"))
             fprintf(stderr, "[slu plan %d] streams               %6.1f ms\n", iam, ms_since(ts0));
         X.s = pstream;
@@ -976,6 +979,9 @@ struct Plan : PlanBase {
         if (ev_pend) (void)hipEventDestroy(ev_pend);
         if (ev_tu0) (void)hipEventDestroy(ev_tu0);
         if (ev_tu1) (void)hipEventDestroy(ev_tu1);
+        if (ev_sr0) (void)hipEventDestroy(ev_sr0);
+        if (ev_sr1) (void)hipEventDestroy(ev_sr1);
+        if (sstream) (void)hipStreamDestroy(sstream);
         if (stream) (void)hipStreamDestroy(stream);
         if (pstream) (void)hipStreamDestroy(pstream);
         if (ustream) (void)hipStreamDestroy(ustream);
@@ -2430,6 +2436,8 @@ struct Plan : PlanBase {
         HIPCHK(hipEventCreateWithFlags(&ev_pend, hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&ev_tu0, hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&ev_tu1, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&ev_sr0, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&ev_sr1, hipEventDisableTiming));
         d_info.alloc(Pr * Pc);
         stats.lu_bytes = (double)(lval_total + uval_total) * sizeof(T);
         stats.index_bytes = (double)(d_lblk.bytes() + d_lmap.bytes() + d_ublk.bytes() +
@@ -2835,6 +2843,7 @@ struct Plan : PlanBase {
     // gain nothing further, tools/ab_env.sh).
     int rest_split = getenv("SLU_REST_SPLIT") ? atoi(getenv("SLU_REST_SPLIT")) : 30;
     int rest_chunks = getenv("SLU_REST_CHUNKS") ? atoi(getenv("SLU_REST_CHUNKS")) : 1;
+    int rest_2stream = getenv("SLU_REST_2STREAM") ? atoi(getenv("SLU_REST_2STREAM")) : 0;
     // k_diag_strips (diag_strips.h) for the levels near the root: a few wide
     // real blocks, each factored by one workgroup per 32-column strip
     // (SLU_DIAG_STRIPS=0: k_diag_lu_f everywhere; SLU_DIAG_STRIPS_MAX: the
@@ -3042,6 +3051,15 @@ struct Plan : PlanBase {
             }
             // the rest of L on the Schur stream, once the panels of L exist
             HIPCHK(hipStreamWaitEvent(stream, ev_pan[L], 0));
+            // the small rest tiles beside the big ones on a stream of their own
+            // (SLU_REST_2STREAM=1; conflicting destinations within a level are
+            // atomic, the rest have one writer)
+            const bool two_r = rest_2stream && sstream && !opts.serial && R.big_n > R.bigc_n &&
+                               R.tile_n > R.tilec_n;
+            if (two_r) {
+                HIPCHK(hipEventRecord(ev_sr0, stream));
+                HIPCHK(hipStreamWaitEvent(sstream, ev_sr0, 0));
+            }
             if (R.big_n > R.bigc_n) {
                 // the first rest_split %% of the rest tiles as a launch of their own
                 const int nrest = R.big_n - R.bigc_n;
@@ -3059,10 +3077,15 @@ struct Plan : PlanBase {
                 stats.n_schur_big_launches++;
             }
             if (R.tile_n > R.tilec_n) {
-                span(3, stream, [&] {
-                    launch_small(R, R.tile_off + R.tilec_n, R.tile_n - R.tilec_n, stream);
+                hipStream_t SS = two_r ? sstream : stream;
+                span(3, SS, [&] {
+                    launch_small(R, R.tile_off + R.tilec_n, R.tile_n - R.tilec_n, SS);
                 });
                 stats.n_schur_launches++;
+                if (two_r) {
+                    HIPCHK(hipEventRecord(ev_sr1, sstream));
+                    HIPCHK(hipStreamWaitEvent(stream, ev_sr1, 0));
+                }
             }
             HIPCHK(hipEventRecord(ev_rest[L], stream));
             if (opts.timing >= 2) lvl_end.push_back(mark_on(stream)); // level wall time
