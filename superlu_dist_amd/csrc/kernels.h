@@ -1632,6 +1632,17 @@ constexpr int TR_WAVES = 4;
 #ifndef TR_TU
 #define TR_TU 8 // T elements in flight per thread while a block is staged (A/B builds)
 #endif
+#ifndef TR_PREFETCH
+// TR_PREFETCH=1: the next block's Dinv and T in registers during the current
+// block.  Off: near the root it cuts the serialized 256-wide TRSM from 118 to
+// 81 us, but in the pipelined factorization (beside the Schur tiles) the U
+// launch's extra registers cost more than it saves (100^3: 289 -> 297 ms,
+// U TRSM 130 -> 158 us per launch; profiles/r05tpf/).
+#define TR_PREFETCH 0
+#endif
+#ifndef TR_PF_MAX
+#define TR_PF_MAX 64 // at most this many T elements per thread prefetched (A/B builds)
+#endif
 // MAXW: the widest supernode of the launch's items.  The narrow levels
 // (MAXW 64: 16 row registers, 17 KB of LDS) run several workgroups per CU
 // where the 256-wide form (64 registers, 68 KB) runs one.
@@ -1673,10 +1684,59 @@ k_trsm_reg(const TrsmItemF<T> *items) {
         }
         xa[s] = v;
     }
+#if TR_PREFETCH
+    // block b + 1's Dinv and T_{<b+1,b+1} travel to registers while block b
+    // computes (none of it depends on X), and go to LDS at the top of the next
+    // block: the chain of global-load latencies under the 256-wide panels'
+    // eight blocks is overlapped with the MFMAs and barriers instead of
+    // serialized with them.  kr * PW is a multiple of the thread count, so
+    // every thread holds exactly 4 (b + 1) T elements.
+    constexpr int NT = 64 * TR_WAVES, PT = (TROWS * PW + NT - 1) / NT, PD = PW * PW / NT;
+    static_assert(PW * PW % NT == 0, "whole Dinv rows per thread");
+    constexpr int PFM = TR_PF_MAX < PT ? TR_PF_MAX : PT; // prefetched; the rest at put()
+    T pt[PFM], pd[PD];
+    auto tload = [&](int bb, int u) {
+        const int kr = bb * PW, e = tid + u * NT;
+        const int i = MODE == 0 ? e % kr : e / PW, j = MODE == 0 ? e / kr : e % PW;
+        const int col = min(bb * PW + j, w - 1);
+        const T *src = MODE == 0 ? it.t + i + (int64_t)col * it.ldt : it.t + col + (int64_t)i * it.ldt;
+        return keep_if(bb * PW + j < w, gld(src));
+    };
+    auto fetch = [&](int bb) {
+        const int kr = bb * PW;
+#pragma unroll
+        for (int u = 0; u < PD; ++u) pd[u] = gld(it.dinv + (int64_t)bb * PW * PW + tid + u * NT);
+#pragma unroll
+        for (int u = 0; u < PFM; ++u)
+            if (u * NT < kr * PW) pt[u] = tload(bb, u); // (uniform; a constant once the block loop unrolls)
+    };
+    auto put = [&](int bb) {
+        const int kr = bb * PW;
+#pragma unroll
+        for (int u = 0; u < PD; ++u) sD[(tid + u * NT) / PW][(tid + u * NT) % PW] = pd[u];
+        T late[PT - PFM > 0 ? PT - PFM : 1];
+#pragma unroll
+        for (int u = PFM; u < PT; ++u)
+            if (u * NT < kr * PW) late[u - PFM] = tload(bb, u);
+#pragma unroll
+        for (int u = 0; u < PT; ++u)
+            if (u * NT < kr * PW) {
+                const int e = tid + u * NT;
+                const T v = u < PFM ? pt[u < PFM ? u : 0] : late[u < PFM ? 0 : u - PFM];
+                if (MODE == 0) sT[e % kr][e / kr] = v;
+                else sT[e / PW][e % PW] = v;
+            }
+    };
+    fetch(0);
+#endif
 #pragma unroll
     for (int b = 0; b < NBMAX; ++b) {
         if (b >= nb) break;
         __syncthreads();
+#if TR_PREFETCH
+        put(b);
+        if (b + 1 < nb) fetch(b + 1);
+#else
         stage_loop<64 * TR_WAVES, 4, T>(
             tid, PW * PW,
             [&](int e, bool ok) { return keep_if(ok, gld(it.dinv + (int64_t)b * PW * PW + min(e, PW * PW - 1))); },
@@ -1696,6 +1756,7 @@ k_trsm_reg(const TrsmItemF<T> *items) {
                     if (MODE == 0) sT[e % kr][e / kr] = v;
                     else sT[e / PW][e % PW] = v;
                 });
+#endif
         __syncthreads();
         typename M::acc_t a0 = M::zero(), a1 = M::zero();
 #pragma unroll
