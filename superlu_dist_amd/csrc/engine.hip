@@ -2789,6 +2789,9 @@ struct Plan : PlanBase {
     // SLU_CRIT_2STREAM=1: a level's small critical tiles beside its big ones (measured
     // neutral at 100^3, profiles/r05t2c/; off by default)
     int crit_2stream = getenv("SLU_CRIT_2STREAM") ? atoi(getenv("SLU_CRIT_2STREAM")) : 0;
+    // SLU_TRSM_PF=N: levels with at most N L + U slabs use k_trsm_reg's
+    // next-block register prefetch (kernels.h, TR_PREFETCH; 0 = never)
+    int trsm_pf = getenv("SLU_TRSM_PF") ? atoi(getenv("SLU_TRSM_PF")) : 0;
     void launch_trsm_fast(const LevelRange &R, hipStream_t st) {
         // the U launch on ustream when both panels have slabs
         const bool two = trsm_2stream && ustream && st == pstream && R.lf_n && R.uf_n;
@@ -2818,6 +2821,15 @@ struct Plan : PlanBase {
                                    d_lf.p + R.lf_off);
             if (R.uf_n)
                 hipLaunchKernelGGL((k_trsm_reg<T, 1, 128>), dim3(R.uf_n), dim3(64 * TR_WAVES), 0, su,
+                                   d_uf.p + R.uf_off);
+        } else if (trsm_pf > 0 && R.lf_n + R.uf_n <= trsm_pf) {
+            // few slabs (the levels near the root): one wave of workgroups whose
+            // time is the eight blocks' load latency -> the prefetching form
+            if (R.lf_n)
+                hipLaunchKernelGGL((k_trsm_reg<T, 0, FAST_MAXW, true>), dim3(R.lf_n), dim3(64 * TR_WAVES), 0, st,
+                                   d_lf.p + R.lf_off);
+            if (R.uf_n)
+                hipLaunchKernelGGL((k_trsm_reg<T, 1, FAST_MAXW, true>), dim3(R.uf_n), dim3(64 * TR_WAVES), 0, su,
                                    d_uf.p + R.uf_off);
         } else {
             if (R.lf_n)

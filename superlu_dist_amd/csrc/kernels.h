@@ -1646,7 +1646,7 @@ constexpr int TR_WAVES = 4;
 // MAXW: the widest supernode of the launch's items.  The narrow levels
 // (MAXW 64: 16 row registers, 17 KB of LDS) run several workgroups per CU
 // where the 256-wide form (64 registers, 68 KB) runs one.
-template <typename T, int MODE, int MAXW = FAST_MAXW>
+template <typename T, int MODE, int MAXW = FAST_MAXW, bool PF = TR_PREFETCH != 0>
 __global__ void __launch_bounds__(64 * TR_WAVES, MAXW <= 64 ? 4 : MAXW <= 128 ? 2 : 1)
 k_trsm_reg(const TrsmItemF<T> *items) {
     constexpr int PW = 32, NKS = MAXW / 4, NBMAX = MAXW / PW;
@@ -1684,7 +1684,6 @@ k_trsm_reg(const TrsmItemF<T> *items) {
         }
         xa[s] = v;
     }
-#if TR_PREFETCH
     // block b + 1's Dinv and T_{<b+1,b+1} travel to registers while block b
     // computes (none of it depends on X), and go to LDS at the top of the next
     // block: the chain of global-load latencies under the 256-wide panels'
@@ -1694,7 +1693,7 @@ k_trsm_reg(const TrsmItemF<T> *items) {
     constexpr int NT = 64 * TR_WAVES, PT = (TROWS * PW + NT - 1) / NT, PD = PW * PW / NT;
     static_assert(PW * PW % NT == 0, "whole Dinv rows per thread");
     constexpr int PFM = TR_PF_MAX < PT ? TR_PF_MAX : PT; // prefetched; the rest at put()
-    T pt[PFM], pd[PD];
+    T pt[PF ? PFM : 1], pd[PF ? PD : 1];
     auto tload = [&](int bb, int u) {
         const int kr = bb * PW, e = tid + u * NT;
         const int i = MODE == 0 ? e % kr : e / PW, j = MODE == 0 ? e / kr : e % PW;
@@ -1727,16 +1726,15 @@ k_trsm_reg(const TrsmItemF<T> *items) {
                 else sT[e / PW][e % PW] = v;
             }
     };
-    fetch(0);
-#endif
+    if constexpr (PF) fetch(0);
 #pragma unroll
     for (int b = 0; b < NBMAX; ++b) {
         if (b >= nb) break;
         __syncthreads();
-#if TR_PREFETCH
-        put(b);
-        if (b + 1 < nb) fetch(b + 1);
-#else
+        if constexpr (PF) {
+            put(b);
+            if (b + 1 < nb) fetch(b + 1);
+        } else {
         stage_loop<64 * TR_WAVES, 4, T>(
             tid, PW * PW,
             [&](int e, bool ok) { return keep_if(ok, gld(it.dinv + (int64_t)b * PW * PW + min(e, PW * PW - 1))); },
@@ -1756,7 +1754,7 @@ k_trsm_reg(const TrsmItemF<T> *items) {
                     if (MODE == 0) sT[e % kr][e / kr] = v;
                     else sT[e / PW][e % PW] = v;
                 });
-#endif
+        }
         __syncthreads();
         typename M::acc_t a0 = M::zero(), a1 = M::zero();
 #pragma unroll
