@@ -44,6 +44,9 @@
 namespace slu {
 
 constexpr int DS_THREADS = 256, DS_PW = 32, DS_MAXS = FAST_MAXW / DS_PW;
+#ifndef DS_TU
+#define DS_TU 16 // a received panel's elements in flight per thread (A/B builds)
+#endif
 
 #ifdef SLU_DS_PROBE
 // Diagnostics build only (tools/micro/diag_strips_micro.hip): cycles per
@@ -212,7 +215,7 @@ k_diag_strips(const DiagItemF<T> *items, int nitems, unsigned *flags, unsigned e
         // only L21_p (rows r0 + 32 ..): L_pp enters through its inverse
         const int nb21 = nr - PW, rb = r0 + PW;
         if (nb21 > 0)
-            stage_loop<DS_THREADS, 16, T>(
+            stage_loop<DS_THREADS, DS_TU, T>(
                 tid, nb21 * PW,
                 [&](int e, bool ok) {
                     const int ee = min(e, nb21 * PW - 1);
