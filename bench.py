@@ -465,6 +465,9 @@ def main():
     if args.workload != "lap3d":
         args.no_cpu = True  # the CPU baseline is the reference on the headline workload
 
+    # the library's exchange watchdog is opt-in: armed for the bench's ranks
+    # (a hung exchange then ends with a diagnosis and exit 86, csrc/watchdog.h)
+    os.environ.setdefault("SLU_WATCHDOG_S", "300")
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # `bench.py --gpus N` without a launcher: start the N ranks here,
         # before anything touches the GPU (torch.distributed.run does the same)

@@ -214,7 +214,14 @@ class DeviceResidentSystem:
     Glu_persist / Glu_freeable, then pddistribute -> pdgstrf -> pdgstrs of
     libslu_mi355x_solve.so.  The arrays stay referenced for the lifetime of
     the object (the library keeps pointers to A's copy and to the
-    LUstruct)."""
+    LUstruct).
+
+    One-shot use only, in a child process that exits afterwards (bench.py's
+    device-resident leg runs it so): nothing frees the calloc'ed Llu, the
+    arrays pddistribute allocates into it, or the library's cached plan and
+    its device factors -- the reference's Destroy_LU / LUstructFree live in
+    the reference library, which this process does not load.  Process exit
+    releases them."""
 
     def __init__(self, n, rowptr, colind, nzval, perm_c, etree, xsup, supno, xlsub, lsub, xusub,
                  usub, anorm):

@@ -44,9 +44,9 @@
 namespace slu {
 
 constexpr int DS_THREADS = 256, DS_PW = 32, DS_MAXS = FAST_MAXW / DS_PW;
-#ifndef DS_TU
-#define DS_TU 16 // a received panel's elements in flight per thread (A/B builds)
-#endif
+// a received panel staged 16 elements per thread in flight (32: no faster,
+// profiles/r05ds/)
+constexpr int DS_TU = 16;
 
 #ifdef SLU_DS_PROBE
 // Diagnostics build only (tools/micro/diag_strips_micro.hip): cycles per

@@ -203,33 +203,69 @@ struct Xport {
     void section(int g, int root, uint32_t mask, void *buf, size_t bytes) {
         if (bytes && gsize(g) > 1 && (mask & ~(1u << root))) ops.push_back({g, root, buf, bytes, mask});
     }
-    // The point-to-point test transport: exactly the send / receive pairs
-    // the RCCL branch below issues, in the same order (a broadcast becomes
-    // the root's sends to every other member), staged through host memory
-    // and handed to the caller as one group (its sends and receives are all
-    // posted before any completes, as inside ncclGroupStart / End).  A rank
-    // that expects a section its root does not send, or a different order of
-    // sections between one pair, then hangs or fails in the test instead of
-    // on the RCCL node.
+    // This rank's point-to-point calls for the queued group, in issue order:
+    // a section (and a broadcast, mask = all) becomes the root's sends to
+    // every other member in the mask, in member order, and each member's
+    // receive from the root.  The RCCL branch issues exactly this list as
+    // ncclSend / ncclRecv inside one ncclGroupStart / End, and the
+    // point-to-point test transport hands exactly this list to its callback
+    // (staged through host memory, all posted before any completes), so the
+    // send / receive pairing every grid test runs is the one the RCCL node
+    // runs (tests/test_grid.py::test_rccl_call_sequence_is_the_tested_one_cpu
+    // compares the two lists and checks the pairing across ranks).
+    struct P2P {
+        int g, peer, send; // group, group rank of the other side, 1 = send
+        size_t bytes;
+        int op; // index into ops
+    };
+    vector<P2P> expand() const {
+        vector<P2P> q;
+        for (size_t i = 0; i < ops.size(); ++i) {
+            const Op &o = ops[i];
+            const int me = grank(o.g), P = gsize(o.g);
+            if (me == o.root) {
+                for (int m = 0; m < P; ++m)
+                    if (m != me && (o.mask >> m & 1)) q.push_back({o.g, m, 1, o.bytes, (int)i});
+            } else if (o.mask >> me & 1) {
+                q.push_back({o.g, o.root, 0, o.bytes, (int)i});
+            }
+        }
+        return q;
+    }
+    int world_of(int g, int m) const {
+        return g == G_WORLD ? m : g == G_ROW ? c->myrow * c->npcol + m : g == G_COL ? m * c->npcol + c->mycol : c->iam;
+    }
+    // SLU_XPORT_TRACE=<dir>: every flush appends this rank's call list to
+    // <dir>/xport_<kind>.<world rank> (kind: the list the transport ran, and
+    // on the host transports also "rccl", the calls the RCCL branch would
+    // issue for the same group, recorded by a dry run of flush_rccl)
+    const char *trace_dir = getenv("SLU_XPORT_TRACE");
+    long trace_seq = 0;
+    void trace(const char *kind, const vector<P2P> &q) const {
+        if (!trace_dir) return;
+        char fn[1024];
+        snprintf(fn, sizeof fn, "%s/xport_%s.%d", trace_dir, kind, c->iam);
+        FILE *f = fopen(fn, "a");
+        if (!f) return;
+        fprintf(f, "F %ld %s %d\n", trace_seq, phase, level);
+        for (const P2P &p : q)
+            fprintf(f, "%c %d %d %zu\n", p.send ? 'S' : 'R', p.g, world_of(p.g, p.peer), p.bytes);
+        fclose(f);
+    }
     vector<vector<char>> p2p_bufs;
     bool host_mem = false; // schedule-only plans: buffers are host memory
     void flush_p2p() {
+        const vector<P2P> q0 = expand();
+        trace("host", q0);
+        if (trace_dir) flush_rccl(true);
+        vector<slu_host_p2p_op> q;
         if (host_mem) {
             // no staging: the host buffers go to the transport as they are
-            vector<slu_host_p2p_op> q;
-            for (const Op &o : ops) {
-                const int me = grank(o.g), P = gsize(o.g);
-                if (me == o.root) {
-                    for (int m = 0; m < P; ++m)
-                        if (m != me && (o.mask >> m & 1)) {
-                            q.push_back({o.g, m, 1, 0, o.buf, (int64_t)o.bytes});
-                            sent += (double)o.bytes;
-                        }
-                } else if (o.mask >> me & 1) {
-                    SLU_REQUIRE(o.buf, "section of group %d root %d has no buffer", o.g, o.root);
-                    q.push_back({o.g, o.root, 0, 0, o.buf, (int64_t)o.bytes});
-                    recvd += (double)o.bytes;
-                }
+            for (const P2P &p : q0) {
+                const Op &o = ops[p.op];
+                SLU_REQUIRE(o.buf, "section of group %d root %d has no buffer", o.g, o.root);
+                q.push_back({p.g, p.peer, p.send, 0, o.buf, (int64_t)p.bytes});
+                (p.send ? sent : recvd) += (double)p.bytes;
             }
             if (!q.empty())
                 SLU_REQUIRE(c->host_p2p(c->host_ctx, (int)q.size(), q.data()) == 0,
@@ -237,45 +273,33 @@ struct Xport {
             return;
         }
         HIPCHK(hipStreamSynchronize(s));
-        vector<slu_host_p2p_op> q;
-        vector<std::pair<int, size_t>> recv_of; // (op, q index) of each receive
+        // one host staging buffer per op: the root's D2H once, its sends read it
         p2p_bufs.resize(std::max(p2p_bufs.size(), ops.size()));
-        for (size_t i = 0; i < ops.size(); ++i) {
-            const Op &o = ops[i];
-            const int me = grank(o.g), P = gsize(o.g);
-            vector<char> &hb = p2p_bufs[i];
-            if (me == o.root) {
-                hb.resize(o.bytes);
+        vector<char> staged(ops.size(), 0);
+        for (const P2P &p : q0) {
+            const Op &o = ops[p.op];
+            SLU_REQUIRE(o.buf, "section of group %d root %d has no buffer", o.g, o.root);
+            vector<char> &hb = p2p_bufs[p.op];
+            hb.resize(o.bytes);
+            if (p.send && !staged[p.op]) {
                 HIPCHK(hipMemcpyAsync(hb.data(), o.buf, o.bytes, hipMemcpyDeviceToHost, s));
-                for (int m = 0; m < P; ++m)
-                    if (m != me && (o.mask >> m & 1)) {
-                        q.push_back({o.g, m, 1, 0, hb.data(), (int64_t)o.bytes});
-                        sent += (double)o.bytes;
-                    }
-            } else if (o.mask >> me & 1) {
-                SLU_REQUIRE(o.buf, "section of group %d root %d has no buffer", o.g, o.root);
-                hb.resize(o.bytes);
-                recv_of.push_back({(int)i, q.size()});
-                q.push_back({o.g, o.root, 0, 0, hb.data(), (int64_t)o.bytes});
-                recvd += (double)o.bytes;
+                staged[p.op] = 1;
             }
+            q.push_back({p.g, p.peer, p.send, 0, hb.data(), (int64_t)p.bytes});
+            (p.send ? sent : recvd) += (double)p.bytes;
         }
         HIPCHK(hipStreamSynchronize(s));
         if (!q.empty())
             SLU_REQUIRE(c->host_p2p(c->host_ctx, (int)q.size(), q.data()) == 0,
                         "host point-to-point group of %zu ops failed", q.size());
-        for (auto &r : recv_of)
-            HIPCHK(hipMemcpyAsync(ops[r.first].buf, p2p_bufs[r.first].data(), ops[r.first].bytes,
-                                  hipMemcpyHostToDevice, s));
+        for (const P2P &p : q0)
+            if (!p.send)
+                HIPCHK(hipMemcpyAsync(ops[p.op].buf, p2p_bufs[p.op].data(), p.bytes, hipMemcpyHostToDevice, s));
         HIPCHK(hipStreamSynchronize(s));
     }
     // this rank's part of the queued group, for the watchdog
     std::string describe() const {
         static const char *gn[4] = {"layer", "row", "column", "z"};
-        auto world_of = [&](int g, int m) {
-            return g == G_WORLD ? m : g == G_ROW ? c->myrow * c->npcol + m
-                                   : g == G_COL ? m * c->npcol + c->mycol : c->iam;
-        };
         std::string s = phase;
         if (level >= 0) s += " of level " + std::to_string(level);
         int shown = 0, more = 0;
@@ -295,15 +319,7 @@ struct Xport {
                          gn[g], m, world_of(g, m), bytes);
             lst += (shown++ ? "; " : "") + std::string(b);
         };
-        for (const Op &o : ops) {
-            const int me = grank(o.g), P = gsize(o.g);
-            if (me == o.root) {
-                for (int m = 0; m < P; ++m)
-                    if (m != me && (o.mask >> m & 1)) add(true, o.g, m, o.bytes);
-            } else if (o.mask >> me & 1) {
-                add(false, o.g, o.root, o.bytes);
-            }
-        }
+        for (const P2P &p : expand()) add(p.send != 0, p.g, p.peer, p.bytes);
         char b[160];
         snprintf(b, sizeof b, " (%zu ops; this rank sends %.0f and receives %.0f bytes): ", ops.size(), sb, rb);
         s += b + lst;
@@ -312,17 +328,21 @@ struct Xport {
     }
     void flush() {
         if (ops.empty()) return;
+        ++trace_seq;
         Watchdog *wd = c->watchdog();
         if (c->host_p2p || c->host_fn) {
             // host transports block in the callback: the record is open for its duration
             const uint64_t id = wd ? wd->open(describe(), nullptr) : 0;
             if (c->host_p2p) flush_host_p2p();
-            else flush_host_bcast();
+            else {
+                if (trace_dir) flush_rccl(true);
+                flush_host_bcast();
+            }
             if (wd) wd->close(id);
             ops.clear();
             return;
         }
-        flush_rccl();
+        flush_rccl(false);
         if (wd) {
             hipEvent_t e;
             HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -358,29 +378,27 @@ struct Xport {
             }
         }
     }
-    void flush_rccl() {
-        {
-            // bcast ops as ncclBroadcast; sections as direct sends from the
-            // root to each member that needs them (xGMI is point to point:
-            // a root's sends to its row / column peers use distinct links)
-            NCCLCHK(ncclGroupStart());
-            for (auto &o : ops) {
-                const int me = grank(o.g), P = gsize(o.g);
-                if (o.mask == ~0u) {
-                    NCCLCHK(ncclBroadcast(o.buf, o.buf, o.bytes, ncclChar, o.root, comm_of(o.g), s));
-                } else if (me == o.root) {
-                    for (int m = 0; m < P; ++m)
-                        if (m != me && (o.mask >> m & 1)) {
-                            NCCLCHK(ncclSend(o.buf, o.bytes, ncclChar, m, comm_of(o.g), s));
-                            sent += (double)o.bytes;
-                        }
-                } else if (o.mask >> me & 1) {
-                    NCCLCHK(ncclRecv(o.buf, o.bytes, ncclChar, o.root, comm_of(o.g), s));
-                    recvd += (double)o.bytes;
-                }
-            }
-            NCCLCHK(ncclGroupEnd());
+    // Every op as direct sends from the root to each member that needs it
+    // (xGMI is point to point: a root's sends to its row / column peers use
+    // distinct links; the plan-time all-gathers' broadcasts too, so there is
+    // one call sequence, expand()'s, for RCCL and the tested transport).
+    // dry: record the calls (SLU_XPORT_TRACE, kind "rccl") instead of
+    // issuing them -- the host transports' check of this very code path.
+    void flush_rccl(bool dry) {
+        const vector<P2P> q = expand();
+        if (dry) {
+            trace("rccl", q);
+            return;
         }
+        trace("rccl", q);
+        NCCLCHK(ncclGroupStart());
+        for (const P2P &p : q) {
+            const Op &o = ops[p.op];
+            if (p.send) NCCLCHK(ncclSend(o.buf, o.bytes, ncclChar, p.peer, comm_of(o.g), s));
+            else NCCLCHK(ncclRecv(o.buf, o.bytes, ncclChar, p.peer, comm_of(o.g), s));
+            (p.send ? sent : recvd) += (double)p.bytes;
+        }
+        NCCLCHK(ncclGroupEnd());
     }
     // plan-time all-to-all of variable-length int64 blobs in the world
     // group: out[q] goes to rank q, the result's [p] came from rank p.  Sizes
@@ -584,8 +602,6 @@ struct Plan : PlanBase {
     hipStream_t stream = nullptr;  // Schur updates that are off the critical path
     hipStream_t pstream = nullptr; // panels, exchanges, critical Schur tiles
     hipStream_t ustream = nullptr; // the U panels' TRSM beside the L panels' (launch_trsm_fast)
-    hipStream_t sstream = nullptr; // small rest tiles beside the big ones (SLU_REST_2STREAM)
-    hipEvent_t ev_sr0 = nullptr, ev_sr1 = nullptr;
     vector<hipEvent_t> ev_pan, ev_rest; // per level
     hipEvent_t ev_start = nullptr, ev_pend = nullptr, ev_tu0 = nullptr, ev_tu1 = nullptr;
     bool xmode = false; // 2D grid with exchanges
@@ -753,7 +769,6 @@ struct Plan : PlanBase {
         HIPCHK(hipStreamCreateWithPriority(&stream, hipStreamNonBlocking, prio_lo));
         HIPCHK(hipStreamCreateWithPriority(&pstream, hipStreamNonBlocking, prio_hi));
         HIPCHK(hipStreamCreateWithPriority(&ustream, hipStreamNonBlocking, prio_hi));
-        HIPCHK(hipStreamCreateWithPriority(&sstream, hipStreamNonBlocking, prio_lo));
         if (getenv("SLU_PROFILE_PLAN"))
             fprintf(stderr, "[slu plan %d] streams               %6.1f ms\n", iam, ms_since(ts0));
         X.s = pstream;
@@ -979,9 +994,6 @@ struct Plan : PlanBase {
         if (ev_pend) (void)hipEventDestroy(ev_pend);
         if (ev_tu0) (void)hipEventDestroy(ev_tu0);
         if (ev_tu1) (void)hipEventDestroy(ev_tu1);
-        if (ev_sr0) (void)hipEventDestroy(ev_sr0);
-        if (ev_sr1) (void)hipEventDestroy(ev_sr1);
-        if (sstream) (void)hipStreamDestroy(sstream);
         if (stream) (void)hipStreamDestroy(stream);
         if (pstream) (void)hipStreamDestroy(pstream);
         if (ustream) (void)hipStreamDestroy(ustream);
@@ -2436,8 +2448,6 @@ struct Plan : PlanBase {
         HIPCHK(hipEventCreateWithFlags(&ev_pend, hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&ev_tu0, hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&ev_tu1, hipEventDisableTiming));
-        HIPCHK(hipEventCreateWithFlags(&ev_sr0, hipEventDisableTiming));
-        HIPCHK(hipEventCreateWithFlags(&ev_sr1, hipEventDisableTiming));
         d_info.alloc(Pr * Pc);
         stats.lu_bytes = (double)(lval_total + uval_total) * sizeof(T);
         stats.index_bytes = (double)(d_lblk.bytes() + d_lmap.bytes() + d_ublk.bytes() +
@@ -2776,8 +2786,10 @@ struct Plan : PlanBase {
     }
 
     // SLU_KSPLIT_TILES: levels of <= 2 supernodes with fewer big tiles than
-    // this split their K range (0: off)
-    int ksplit_tiles = getenv("SLU_KSPLIT_TILES") ? atoi(getenv("SLU_KSPLIT_TILES")) : 128;
+    // this split their K range (default 0, off: the chunks of a destination
+    // add atomically in no fixed order, so the root levels' factors would not
+    // be bit-reproducible from run to run, for ~0.3 ms at 100^3)
+    int ksplit_tiles = getenv("SLU_KSPLIT_TILES") ? atoi(getenv("SLU_KSPLIT_TILES")) : 0;
     // SLU_TRSM_NARROW: 0 the 256-wide k_trsm_reg everywhere, 1 the 64-wide
     // instantiation for levels whose TRSM supernodes are <= 64 wide, 2 (default)
     // also the 128-wide one for <= 128
@@ -2786,12 +2798,9 @@ struct Plan : PlanBase {
     // own beside the L panel's (both only wait for the diagonal block; near
     // the root each is a few slabs, latency-bound)
     int trsm_2stream = getenv("SLU_TRSM_2STREAM") ? atoi(getenv("SLU_TRSM_2STREAM")) : 1;
-    // SLU_CRIT_2STREAM=1: a level's small critical tiles beside its big ones (measured
-    // neutral at 100^3, profiles/r05t2c/; off by default)
-    int crit_2stream = getenv("SLU_CRIT_2STREAM") ? atoi(getenv("SLU_CRIT_2STREAM")) : 0;
-    // SLU_TRSM_PF=N: levels with at most N L + U slabs use k_trsm_reg's
-    // next-block register prefetch (kernels.h, TR_PREFETCH; 0 = never)
-    int trsm_pf = getenv("SLU_TRSM_PF") ? atoi(getenv("SLU_TRSM_PF")) : 0;
+    // SLU_TRSM_WV=1 (default): k_trsm_wv (wave-independent, operands from
+    // L2); 0: k_trsm_reg (LDS-staged blocks)
+    int trsm_wv = getenv("SLU_TRSM_WV") ? atoi(getenv("SLU_TRSM_WV")) : 0;
     void launch_trsm_fast(const LevelRange &R, hipStream_t st) {
         // the U launch on ustream when both panels have slabs
         const bool two = trsm_2stream && ustream && st == pstream && R.lf_n && R.uf_n;
@@ -2807,6 +2816,31 @@ struct Plan : PlanBase {
             if (R.uf_n)
                 hipLaunchKernelGGL((k_trsm_blk<T, 1>), dim3(R.uf_n), dim3(256), 0, su,
                                    d_uf.p + R.uf_off);
+        } else if (trsm_wv) {
+            // wave-independent form, instantiated for the level's widest
+            // TRSM supernode (narrow levels: more workgroups per CU)
+            if (R.tf_maxw <= 64) {
+                if (R.lf_n)
+                    hipLaunchKernelGGL((k_trsm_wv<T, 0, 64>), dim3(R.lf_n), dim3(64 * TR_WAVES), 0, st,
+                                       d_lf.p + R.lf_off);
+                if (R.uf_n)
+                    hipLaunchKernelGGL((k_trsm_wv<T, 1, 64>), dim3(R.uf_n), dim3(64 * TR_WAVES), 0, su,
+                                       d_uf.p + R.uf_off);
+            } else if (R.tf_maxw <= 128) {
+                if (R.lf_n)
+                    hipLaunchKernelGGL((k_trsm_wv<T, 0, 128>), dim3(R.lf_n), dim3(64 * TR_WAVES), 0, st,
+                                       d_lf.p + R.lf_off);
+                if (R.uf_n)
+                    hipLaunchKernelGGL((k_trsm_wv<T, 1, 128>), dim3(R.uf_n), dim3(64 * TR_WAVES), 0, su,
+                                       d_uf.p + R.uf_off);
+            } else {
+                if (R.lf_n)
+                    hipLaunchKernelGGL((k_trsm_wv<T, 0>), dim3(R.lf_n), dim3(64 * TR_WAVES), 0, st,
+                                       d_lf.p + R.lf_off);
+                if (R.uf_n)
+                    hipLaunchKernelGGL((k_trsm_wv<T, 1>), dim3(R.uf_n), dim3(64 * TR_WAVES), 0, su,
+                                       d_uf.p + R.uf_off);
+            }
         } else if (R.tf_maxw <= 64 && trsm_narrow) {
             // narrow levels: the 64-wide instantiation (several workgroups per CU)
             if (R.lf_n)
@@ -2821,15 +2855,6 @@ struct Plan : PlanBase {
                                    d_lf.p + R.lf_off);
             if (R.uf_n)
                 hipLaunchKernelGGL((k_trsm_reg<T, 1, 128>), dim3(R.uf_n), dim3(64 * TR_WAVES), 0, su,
-                                   d_uf.p + R.uf_off);
-        } else if (trsm_pf > 0 && R.lf_n + R.uf_n <= trsm_pf) {
-            // few slabs (the levels near the root): one wave of workgroups whose
-            // time is the eight blocks' load latency -> the prefetching form
-            if (R.lf_n)
-                hipLaunchKernelGGL((k_trsm_reg<T, 0, FAST_MAXW, true>), dim3(R.lf_n), dim3(64 * TR_WAVES), 0, st,
-                                   d_lf.p + R.lf_off);
-            if (R.uf_n)
-                hipLaunchKernelGGL((k_trsm_reg<T, 1, FAST_MAXW, true>), dim3(R.uf_n), dim3(64 * TR_WAVES), 0, su,
                                    d_uf.p + R.uf_off);
         } else {
             if (R.lf_n)
@@ -2846,7 +2871,7 @@ struct Plan : PlanBase {
     }
 
     // The rest of a level's Schur tiles go out as two launches, the first
-    // with rest_split %% of them (SLU_REST_SPLIT, SLU_REST_CHUNKS: A/B).  The
+    // with rest_split %% of them (SLU_REST_SPLIT: A/B).  The
     // next level's diag LU and TRSM workgroups (150 / 85 KB of LDS, up to 256
     // VGPRs) fit only on a CU that no Schur workgroup holds; inside one
     // launch every freed slot is refilled with the next Schur tile, so they
@@ -2854,8 +2879,6 @@ struct Plan : PlanBase {
     // CUs and run beside the second (100^3: 363 -> 345 ms; more split points
     // gain nothing further, tools/ab_env.sh).
     int rest_split = getenv("SLU_REST_SPLIT") ? atoi(getenv("SLU_REST_SPLIT")) : 30;
-    int rest_chunks = getenv("SLU_REST_CHUNKS") ? atoi(getenv("SLU_REST_CHUNKS")) : 1;
-    int rest_2stream = getenv("SLU_REST_2STREAM") ? atoi(getenv("SLU_REST_2STREAM")) : 0;
     // k_diag_strips (diag_strips.h) for the levels near the root: a few wide
     // real blocks, each factored by one workgroup per 32-column strip
     // (SLU_DIAG_STRIPS=0: k_diag_lu_f everywhere; SLU_DIAG_STRIPS_MAX: the
@@ -3039,65 +3062,33 @@ struct Plan : PlanBase {
             HIPCHK(hipEventRecord(ev_pan[L], P));
             // critical tiles of L on the panel stream, after the rest of L-1
             if (L > 0) HIPCHK(hipStreamWaitEvent(P, ev_rest[L - 1], 0));
-            // big and small critical tiles side by side (the U-panel TRSM's
-            // stream carries the small ones; conflicting destinations within
-            // a level are atomic, the rest have one writer)
-            const bool two_c = crit_2stream && ustream && P == pstream && R.bigc_n && R.tilec_n;
-            hipStream_t PS = two_c ? ustream : P;
-            if (two_c) {
-                HIPCHK(hipEventRecord(ev_tu0, P));
-                HIPCHK(hipStreamWaitEvent(ustream, ev_tu0, 0));
-            }
             if (R.bigc_n) {
                 span(2, P, [&] { launch_big(R, R.big_off, R.bigc_n, P); });
                 stats.n_schur_launches++;
                 stats.n_schur_big_launches++;
             }
             if (R.tilec_n) {
-                span(3, PS, [&] { launch_small(R, R.tile_off, R.tilec_n, PS); });
+                span(3, P, [&] { launch_small(R, R.tile_off, R.tilec_n, P); });
                 stats.n_schur_launches++;
-            }
-            if (two_c) {
-                HIPCHK(hipEventRecord(ev_tu1, ustream));
-                HIPCHK(hipStreamWaitEvent(P, ev_tu1, 0));
             }
             // the rest of L on the Schur stream, once the panels of L exist
             HIPCHK(hipStreamWaitEvent(stream, ev_pan[L], 0));
-            // the small rest tiles beside the big ones on a stream of their own
-            // (SLU_REST_2STREAM=1; conflicting destinations within a level are
-            // atomic, the rest have one writer)
-            const bool two_r = rest_2stream && sstream && !opts.serial && R.big_n > R.bigc_n &&
-                               R.tile_n > R.tilec_n;
-            if (two_r) {
-                HIPCHK(hipEventRecord(ev_sr0, stream));
-                HIPCHK(hipStreamWaitEvent(sstream, ev_sr0, 0));
-            }
             if (R.big_n > R.bigc_n) {
                 // the first rest_split %% of the rest tiles as a launch of their own
                 const int nrest = R.big_n - R.bigc_n;
                 const int n1 = rest_split > 0 && !opts.serial ? (int)((i64)nrest * rest_split / 100) : 0;
-                const int nch = rest_chunks > 1 && !opts.serial ? rest_chunks : 1;
                 span(2, stream, [&] {
                     if (n1 > 0) launch_big(R, R.big_off + R.bigc_n, n1, stream);
-                    for (int c = 0; c < nch; ++c) {
-                        const int a0 = n1 + (int)((i64)(nrest - n1) * c / nch);
-                        const int a1 = n1 + (int)((i64)(nrest - n1) * (c + 1) / nch);
-                        if (a1 > a0) launch_big(R, R.big_off + R.bigc_n + a0, a1 - a0, stream);
-                    }
+                    if (nrest > n1) launch_big(R, R.big_off + R.bigc_n + n1, nrest - n1, stream);
                 });
                 stats.n_schur_launches++;
                 stats.n_schur_big_launches++;
             }
             if (R.tile_n > R.tilec_n) {
-                hipStream_t SS = two_r ? sstream : stream;
-                span(3, SS, [&] {
-                    launch_small(R, R.tile_off + R.tilec_n, R.tile_n - R.tilec_n, SS);
+                span(3, stream, [&] {
+                    launch_small(R, R.tile_off + R.tilec_n, R.tile_n - R.tilec_n, stream);
                 });
                 stats.n_schur_launches++;
-                if (two_r) {
-                    HIPCHK(hipEventRecord(ev_sr1, sstream));
-                    HIPCHK(hipStreamWaitEvent(stream, ev_sr1, 0));
-                }
             }
             HIPCHK(hipEventRecord(ev_rest[L], stream));
             if (opts.timing >= 2) lvl_end.push_back(mark_on(stream)); // level wall time

@@ -1629,24 +1629,15 @@ k_schur_big(const TileItem *tiles, const KInfo<T> *kinfo, T *Lval, T *Uval,
 // LDS), Z = X_b - acc, X_b = Z Dinv_b; results return to A layout through a
 // per-wave LDS tile.  Same MODE convention as k_trsm_blk.
 constexpr int TR_WAVES = 4;
-#ifndef TR_TU
-#define TR_TU 8 // T elements in flight per thread while a block is staged (A/B builds)
-#endif
-#ifndef TR_PREFETCH
-// TR_PREFETCH=1: the next block's Dinv and T in registers during the current
-// block.  Off: near the root it cuts the serialized 256-wide TRSM from 118 to
-// 81 us, but in the pipelined factorization (beside the Schur tiles) the U
-// launch's extra registers cost more than it saves (100^3: 289 -> 297 ms,
-// U TRSM 130 -> 158 us per launch; profiles/r05tpf/).
-#define TR_PREFETCH 0
-#endif
-#ifndef TR_PF_MAX
-#define TR_PF_MAX 64 // at most this many T elements per thread prefetched (A/B builds)
-#endif
+// T staged 8 elements per thread in flight (16: slower, profiles/r05tu/).  A
+// next-block register prefetch of Dinv / T was measured and dropped: faster
+// serialized near the root, but beside the Schur tiles the extra registers
+// cost more than it saved (100^3 289 -> 297 ms, profiles/r05tpf/).
+constexpr int TR_TU = 8;
 // MAXW: the widest supernode of the launch's items.  The narrow levels
 // (MAXW 64: 16 row registers, 17 KB of LDS) run several workgroups per CU
 // where the 256-wide form (64 registers, 68 KB) runs one.
-template <typename T, int MODE, int MAXW = FAST_MAXW, bool PF = TR_PREFETCH != 0>
+template <typename T, int MODE, int MAXW = FAST_MAXW>
 __global__ void __launch_bounds__(64 * TR_WAVES, MAXW <= 64 ? 4 : MAXW <= 128 ? 2 : 1)
 k_trsm_reg(const TrsmItemF<T> *items) {
     constexpr int PW = 32, NKS = MAXW / 4, NBMAX = MAXW / PW;
@@ -1684,57 +1675,10 @@ k_trsm_reg(const TrsmItemF<T> *items) {
         }
         xa[s] = v;
     }
-    // block b + 1's Dinv and T_{<b+1,b+1} travel to registers while block b
-    // computes (none of it depends on X), and go to LDS at the top of the next
-    // block: the chain of global-load latencies under the 256-wide panels'
-    // eight blocks is overlapped with the MFMAs and barriers instead of
-    // serialized with them.  kr * PW is a multiple of the thread count, so
-    // every thread holds exactly 4 (b + 1) T elements.
-    constexpr int NT = 64 * TR_WAVES, PT = (TROWS * PW + NT - 1) / NT, PD = PW * PW / NT;
-    static_assert(PW * PW % NT == 0, "whole Dinv rows per thread");
-    constexpr int PFM = TR_PF_MAX < PT ? TR_PF_MAX : PT; // prefetched; the rest at put()
-    T pt[PF ? PFM : 1], pd[PF ? PD : 1];
-    auto tload = [&](int bb, int u) {
-        const int kr = bb * PW, e = tid + u * NT;
-        const int i = MODE == 0 ? e % kr : e / PW, j = MODE == 0 ? e / kr : e % PW;
-        const int col = min(bb * PW + j, w - 1);
-        const T *src = MODE == 0 ? it.t + i + (int64_t)col * it.ldt : it.t + col + (int64_t)i * it.ldt;
-        return keep_if(bb * PW + j < w, gld(src));
-    };
-    auto fetch = [&](int bb) {
-        const int kr = bb * PW;
-#pragma unroll
-        for (int u = 0; u < PD; ++u) pd[u] = gld(it.dinv + (int64_t)bb * PW * PW + tid + u * NT);
-#pragma unroll
-        for (int u = 0; u < PFM; ++u)
-            if (u * NT < kr * PW) pt[u] = tload(bb, u); // (uniform; a constant once the block loop unrolls)
-    };
-    auto put = [&](int bb) {
-        const int kr = bb * PW;
-#pragma unroll
-        for (int u = 0; u < PD; ++u) sD[(tid + u * NT) / PW][(tid + u * NT) % PW] = pd[u];
-        T late[PT - PFM > 0 ? PT - PFM : 1];
-#pragma unroll
-        for (int u = PFM; u < PT; ++u)
-            if (u * NT < kr * PW) late[u - PFM] = tload(bb, u);
-#pragma unroll
-        for (int u = 0; u < PT; ++u)
-            if (u * NT < kr * PW) {
-                const int e = tid + u * NT;
-                const T v = u < PFM ? pt[u < PFM ? u : 0] : late[u < PFM ? 0 : u - PFM];
-                if (MODE == 0) sT[e % kr][e / kr] = v;
-                else sT[e / PW][e % PW] = v;
-            }
-    };
-    if constexpr (PF) fetch(0);
 #pragma unroll
     for (int b = 0; b < NBMAX; ++b) {
         if (b >= nb) break;
         __syncthreads();
-        if constexpr (PF) {
-            put(b);
-            if (b + 1 < nb) fetch(b + 1);
-        } else {
         stage_loop<64 * TR_WAVES, 4, T>(
             tid, PW * PW,
             [&](int e, bool ok) { return keep_if(ok, gld(it.dinv + (int64_t)b * PW * PW + min(e, PW * PW - 1))); },
@@ -1754,7 +1698,6 @@ k_trsm_reg(const TrsmItemF<T> *items) {
                     if (MODE == 0) sT[e % kr][e / kr] = v;
                     else sT[e / PW][e % PW] = v;
                 });
-        }
         __syncthreads();
         typename M::acc_t a0 = M::zero(), a1 = M::zero();
 #pragma unroll
@@ -1789,6 +1732,108 @@ k_trsm_reg(const TrsmItemF<T> *items) {
         __syncthreads();
 #pragma unroll
         for (int s = 0; s < 8; ++s) xa[8 * b + s] = W[rl][4 * s + kq];
+    }
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) {
+        const int k = 4 * s + kq;
+        if (rv && k < w) {
+            if (MODE == 0) it.x[myr + (int64_t)k * it.ldx] = xa[s];
+            else if (k >= t0) it.x[rbase + k] = xa[s];
+        }
+    }
+}
+
+// TRSM, wave-independent form (replaces k_trsm_reg on the real types).
+// Each wave owns 16 rows of the 64-row slab and runs the 32-column block
+// recurrence X_b = (X_b - X_{<b} T_{<b,b}) Dinv_b on its own: X in MFMA
+// A-operand registers (lane keeps X[row lane&15][4s + lane>>4]), the B
+// operands -- T_{<b,b} from the diagonal block, Dinv_b -- straight from
+// global memory into registers (every slab of a level reads the same
+// diagonal block: L2 / L1 hits), the C -> A layout change through a 16 x 33
+// LDS tile private to the wave.  No workgroup barrier and no LDS staging:
+// the loads of T / Dinv do not depend on X, so the compiler issues them
+// ahead of the MFMAs they feed, where k_trsm_reg staged every block through
+// LDS behind two barriers per block (one global round trip per block on the
+// critical path: 118-165 us for a 256-wide panel).
+// MODE 0: X := X U^{-1} (L panel rows, column-major, ld ldx), T(i, c) =
+// U(i, c) = t[i + c ldt]; MODE 1: U columns as rows (segments from t0),
+// X := X L^{-T}, T(i, c) = L(c, i) = t[c + i ldt].
+template <typename T, int MODE, int MAXW = FAST_MAXW>
+__global__ void __launch_bounds__(64 * TR_WAVES, MAXW <= 64 ? 4 : MAXW <= 128 ? 2 : 1)
+k_trsm_wv(const TrsmItemF<T> *items) {
+    constexpr int PW = 32, NKS = MAXW / 4, NBMAX = MAXW / PW;
+    using Sx = S<T>;
+    using M = Mma<T>;
+    const TrsmItemF<T> it = items[blockIdx.x];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int w = it.w, nb = (w + PW - 1) / PW;
+    __shared__ T sW[TR_WAVES][16][PW + 1];
+    T (*W)[PW + 1] = sW[wid];
+    if (wid * 16 >= it.nrows) return; // (no workgroup barrier below)
+    const int rl = lane & 15, kq = lane >> 4;
+    const int myr = wid * 16 + rl;
+    const bool rv = myr < it.nrows;
+    int64_t rbase = 0;
+    int t0 = 0;
+    if (MODE == 1 && rv) {
+        t0 = it.t0[myr];
+        rbase = it.voff[myr] - t0;
+    }
+    T xa[NKS];
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) {
+        const int k = 4 * s + kq;
+        T v = Sx::zero();
+        if (rv && k < w) {
+            if (MODE == 0) v = it.x[myr + (int64_t)k * it.ldx];
+            else if (k >= t0) v = it.x[rbase + k];
+        }
+        xa[s] = v;
+    }
+    // T(i, c) of this mode, c clamped into the block (columns >= w read 0)
+    auto tb = [&](int i, int c) -> T {
+        const int cc = min(c, w - 1);
+        const T *src = MODE == 0 ? it.t + i + (int64_t)cc * it.ldt : it.t + cc + (int64_t)i * it.ldt;
+        return keep_if(c < w, gld(src));
+    };
+#pragma unroll
+    for (int b = 0; b < NBMAX; ++b) {
+        if (b >= nb) break;
+        typename M::acc_t a0 = M::zero(), a1 = M::zero();
+#pragma unroll
+        for (int s = 0; s < 8 * b; ++s) {
+            const int i = 4 * s + kq;
+            M::step(a0, xa[s], tb(i, b * PW + rl));
+            M::step(a1, xa[s], tb(i, b * PW + 16 + rl));
+        }
+        // Z = X_b - acc: acc (C layout) -> the wave's tile, read back in A layout
+        // (one wave: its LDS accesses complete in order)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            W[M::row(lane, i)][rl] = M::get(a0, i);
+            W[M::row(lane, i)][16 + rl] = M::get(a1, i);
+        }
+        asm volatile("" ::: "memory");
+        T za[8];
+#pragma unroll
+        for (int s = 0; s < 8; ++s) za[s] = Sx::fms(xa[8 * b + s], W[rl][4 * s + kq], one_of(xa[0]));
+        asm volatile("" ::: "memory");
+        const T *dv = it.dinv + (int64_t)b * PW * PW;
+        typename M::acc_t c0 = M::zero(), c1 = M::zero();
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+            M::step(c0, za[s], gld(dv + (4 * s + kq) * PW + rl));
+            M::step(c1, za[s], gld(dv + (4 * s + kq) * PW + 16 + rl));
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            W[M::row(lane, i)][rl] = M::get(c0, i);
+            W[M::row(lane, i)][16 + rl] = M::get(c1, i);
+        }
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int s = 0; s < 8; ++s) xa[8 * b + s] = W[rl][4 * s + kq];
+        asm volatile("" ::: "memory");
     }
 #pragma unroll
     for (int s = 0; s < NKS; ++s) {

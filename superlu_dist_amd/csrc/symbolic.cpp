@@ -45,16 +45,18 @@ using I = int64_t;
 static int g_last_epilogue = 0;
 
 // SLU_SYMB_DEVICE=1: the epilogue on the GPU (an error without one), =0: on
-// the host; unset: on the GPU for square problems with >= 20 000 supernodes
-// when a GPU is visible (the search stays on the host either way)
-static bool use_device_epilogue(I m, I n, I nsup) {
+// the host; unset: the caller's default -- the engine API (slu_symbfact, one
+// process per GPU) on the GPU for square problems with >= 20 000 supernodes
+// when a GPU is visible; the drop-in `symbfact`, which pdgssvx calls on every
+// rank of an MPI job, on the host (the search stays on the host either way)
+static bool use_device_epilogue(I m, I n, I nsup, bool dev_default) {
     const char *e = getenv("SLU_SYMB_DEVICE");
     if (e) {
         if (atoi(e) == 0) return false;
         if (!slu_symb_have_device()) throw Error("symbfact: SLU_SYMB_DEVICE=1 but no GPU is visible");
         return m == n;
     }
-    return m == n && nsup >= 20000 && slu_symb_have_device();
+    return dev_default && m == n && nsup >= 20000 && slu_symb_have_device();
 }
 using std::vector;
 constexpr I NONE = -1;
@@ -715,7 +717,7 @@ struct Walker {
 // of ri (A Pc', rows relabelled by perm_c); etree postordered.
 template <class T>
 static Result symbfact_t(I m, I n, const I *cb, const I *ce, const I *ri64, const I *etree,
-                         I relax, I maxsuper) {
+                         I relax, I maxsuper, bool dev_default) {
     Result R;
     R.n = n;
     const I mn = std::min(m, n);
@@ -742,7 +744,7 @@ static Result symbfact_t(I m, I n, const I *cb, const I *ce, const I *ri64, cons
     g_last_epilogue = 0;
     if constexpr (std::is_same<T, int32_t>::value) {
         const I nsup1 = (I)w.supno[n] + 1;
-        if (n > 1 && use_device_epilogue(m, n, nsup1)) {
+        if (n > 1 && use_device_epilogue(m, n, nsup1, dev_default)) {
             // countnz + fixupL on the device (csrc/symbolic_dev.hip)
             std::string err;
             R.lsub_size = w.xlsub[n];
@@ -813,9 +815,10 @@ static Result symbfact_t(I m, I n, const I *cb, const I *ce, const I *ri64, cons
 }
 
 static Result symbfact(I m, I n, const I *cb, const I *ce, const I *ri, const I *etree, I relax,
-                       I maxsuper) {
-    if (std::max(m, n) + 2 < (I)INT32_MAX) return symbfact_t<int32_t>(m, n, cb, ce, ri, etree, relax, maxsuper);
-    return symbfact_t<int64_t>(m, n, cb, ce, ri, etree, relax, maxsuper);
+                       I maxsuper, bool dev_default) {
+    if (std::max(m, n) + 2 < (I)INT32_MAX)
+        return symbfact_t<int32_t>(m, n, cb, ce, ri, etree, relax, maxsuper, dev_default);
+    return symbfact_t<int64_t>(m, n, cb, ce, ri, etree, relax, maxsuper, dev_default);
 }
 
 // sp_ienv_dist(2) / (3) (SRC/sp_ienv.c:85-112): environment first, then
@@ -863,7 +866,7 @@ int slu_colorder(int64_t m, int64_t n, const int64_t *colptr, const int64_t *row
 void *slu_symbfact(int64_t m, int64_t n, const int64_t *colbeg, const int64_t *colend,
                    const int64_t *rowind, const int64_t *etree, int64_t relax, int64_t maxsuper) {
     try {
-        return new Result(symbfact(m, n, colbeg, colend, rowind, etree, relax, maxsuper));
+        return new Result(symbfact(m, n, colbeg, colend, rowind, etree, relax, maxsuper, true));
     } catch (const std::exception &e) {
         slu::set_last_error(e.what());
         return nullptr;
@@ -939,9 +942,18 @@ int_t symbfact(superlu_dist_options_t *options, int pnum, SuperMatrix *A, int_t 
                int_t *etree, Glu_persist_t *Glu_persist, Glu_freeable_t *Glu_freeable) {
     (void)perm_c;
     const NCPformat *S = (const NCPformat *)A->Store;
+    // a device epilogue (SLU_SYMB_DEVICE=1) creates a HIP queue, which
+    // reseeds libc rand(); pddistribute after this draws its solve trees'
+    // seeds from rand() on every rank (abi.cpp, CallerRandState)
+    char rbuf[256];
+    char *rprev = initstate(1u, rbuf, sizeof rbuf);
+    struct Restore {
+        char *p;
+        ~Restore() { setstate(p); }
+    } restore{rprev};
     try {
         const Result R = symbfact(A->nrow, A->ncol, S->colbeg, S->colend, S->rowind, etree,
-                                  relax_of(options), maxsup_of(options));
+                                  relax_of(options), maxsup_of(options), false);
         if (!pnum && options->PrintStat == SLU_YES) { // SRC/symbfact.c:187-194
             printf("\tMatrix size min_mn  %lld\n", (long long)std::min<I>(A->nrow, A->ncol));
             printf("\tNonzeros in L       %lld\n", (long long)R.nnzL);

@@ -99,6 +99,17 @@ bool epilogue(I n, I nsup, const int32_t *raw, I raw_len, const I *xlsub_raw, co
     }
     const I total = off[nsup];
     lsub.resize(total);
+    // one process per GPU: the device of this process's local rank, as the
+    // factorization picks it (abi.cpp pick_device)
+    {
+        int nd = 0;
+        const char *e = getenv("SUPERLU_DEVICE");
+        const char *lr = getenv("MPI_LOCALRANKID");
+        if (!lr) lr = getenv("OMPI_COMM_WORLD_LOCAL_RANK");
+        if (!lr) lr = getenv("LOCAL_RANK");
+        if ((e || lr) && hipGetDeviceCount(&nd) == hipSuccess && nd > 0)
+            SDCHK(hipSetDevice(e ? atoi(e) : atoi(lr) % nd));
+    }
     xlsub.resize(n + 1);
     Dev<int32_t> d_raw, d_xsup, d_supno, d_usub;
     Dev<I> d_src, d_off, d_out, d_xl;

@@ -91,6 +91,7 @@ class GlooGrid:
 def _worker(rank, world, port, recipe, out_dir, device, fill=False, solve=False,
             transport="bcast", pz=1):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ.setdefault("SLU_WATCHDOG_S", "120")  # the library's watchdog is opt-in
     try:
         import torch.distributed as dist
         dist.init_process_group("gloo", rank=rank, world_size=world)

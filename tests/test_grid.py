@@ -62,6 +62,63 @@ def test_exchange_schedule_through_p2p_transport_cpu(case, tmp_path):
     assert sum(int(o["nsec"]) for o in out) > 0
 
 
+def _read_trace(fn):
+    """[(phase, level, [(kind, group, peer world rank, bytes), ...]), ...]"""
+    out = []
+    for ln in open(fn):
+        t = ln.split()
+        if t[0] == "F":
+            out.append((" ".join(t[2:-1]), int(t[-1]), []))
+        else:
+            out[-1][2].append((t[0], int(t[1]), int(t[2]), int(t[3])))
+    return out
+
+
+@pytest.mark.parametrize("case,pr,pc", [("refdump:big_2x2_d", 2, 2), ("stencil", 2, 4)])
+def test_rccl_call_sequence_is_the_tested_one_cpu(case, pr, pc, tmp_path, monkeypatch):
+    """the RCCL branch's ncclSend / ncclRecv list (recorded
+    by a dry run of flush_rccl, SLU_XPORT_TRACE) equals, group by group, the
+    list the point-to-point test transport runs, on every rank; and across
+    ranks every send A -> B of a group has its receive on B from A, in the
+    same order, of the same size, in the same phase and level -- the
+    condition under which RCCL's in-order point-to-point matching neither
+    hangs nor mixes sections up (the plan-time all-gathers included: no
+    ncclBroadcast is left)."""
+    trace = tmp_path / "trace"
+    trace.mkdir()
+    monkeypatch.setenv("SLU_XPORT_TRACE", str(trace))
+    if case == "stencil":
+        rec = functools.partial(_stencil_recipe, STENCIL_3D7, (12,) * 3, 0, (pr, pc), 60, 256)
+    else:
+        rec = case
+    run_grid(rec, pr, pc, tmp_path, device=None, transport="schedule", timeout=120)
+    P = pr * pc
+    host = [_read_trace(trace / f"xport_host.{r}") for r in range(P)]
+    rccl = [_read_trace(trace / f"xport_rccl.{r}") for r in range(P)]
+    for r in range(P):
+        assert host[r] == rccl[r], f"rank {r}: RCCL call list differs from the tested one"
+        assert len(host[r]) > 10
+    # cross-rank pairing per (group, sender, receiver) stream
+    sends, recvs = {}, {}
+    for r in range(P):
+        for phase, level, calls in host[r]:
+            for kind, g, peer, nbytes in calls:
+                if kind == "S":
+                    sends.setdefault((g, r, peer), []).append((nbytes, phase, level))
+                else:
+                    recvs.setdefault((g, peer, r), []).append((nbytes, phase, level))
+    assert set(sends) == set(recvs)
+    for key in sends:
+        g, a, b = key
+        if g == 1:
+            assert a // pc == b // pc       # row group: same process row
+        elif g == 2:
+            assert a % pc == b % pc         # column group: same process column
+        assert sends[key] == recvs[key], key
+    nlev = {lv for r in range(P) for _, lv, _ in host[r] if lv >= 0}
+    assert len(nlev) > 3                     # the per-level exchanges are in it
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("name,fill", [(n, False) for n in GRID_CASES] +
                          [("lap3d_10_2x4_small_d", True), ("cg20_2x2_small_z", True)])
