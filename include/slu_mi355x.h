@@ -396,6 +396,9 @@ void slu_symbfact_sizes(const void *h, int64_t *sizes);
 /* xsup (nsupers+1 of n+1 written), supno / xlsub / xusub (n+1), lsub, usub */
 void slu_symbfact_arrays(const void *h, int64_t *xsup, int64_t *supno, int64_t *xlsub,
                          int64_t *lsub, int64_t *xusub, int64_t *usub);
+/* the same six arrays in place (valid until slu_symbfact_free): ptrs[0..5]
+ * = xsup, supno, xlsub, lsub, xusub, usub (lengths as above) */
+void slu_symbfact_views(const void *h, const int64_t **ptrs);
 void slu_symbfact_free(void *h);
 /* 1 when the last slu_symbfact / symbfact ran its countnz + fixupL epilogue
    (SRC/util.c:95-199) on the GPU (csrc/symbolic_dev.hip; SLU_SYMB_DEVICE=1

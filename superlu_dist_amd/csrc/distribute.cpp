@@ -37,7 +37,11 @@
 #include <algorithm>
 #include <atomic>
 #include <cstdlib>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <numeric>
 #include <vector>
 
@@ -80,22 +84,77 @@ void *distribute_glu_t(i64 n, const int_t *xsup_in, const int_t *supno_in, const
     auto W = [&](i64 k) { return xsup[k + 1] - xsup[k]; };
     const i64 nlc = (ns + Pc - 1) / Pc, nlr = (ns + Pr - 1) / Pr;
 
+    // SLU_DIST_TIME=1: phase times on stderr (diagnostics)
+    const bool dtime = getenv("SLU_DIST_TIME") != nullptr;
+    auto dt0 = std::chrono::steady_clock::now();
+    auto dtick = [&](const char *what) {
+        if (!dtime) return;
+        const auto t = std::chrono::steady_clock::now();
+        fprintf(stderr, "[distribute] %-28s %8.1f ms\n", what, std::chrono::duration<double, std::milli>(t - dt0).count());
+        dt0 = t;
+    };
     // ---- U segments by block row: (column j, first row irow), j ascending
     //      (so jb ascending, then column), as the reference's jb loop meets them
+    //      A counting sort on host threads: the columns in NCH chunks of about
+    //      equal usub length, per (chunk, block row) counts, then each chunk
+    //      fills its slice of every bucket (chunk order = column order)
     vector<i64> ucnt(ns + 1, 0);
-    for (i64 j = 0; j < n; ++j)
-        for (i64 i = xusub[j]; i < xusub[j + 1]; ++i) ucnt[supno[usub[i]] + 1]++;
-    for (i64 k = 0; k < ns; ++k) ucnt[k + 1] += ucnt[k];
-    vector<std::pair<i64, i64>> useg((size_t)ucnt[ns]);
+    // (uninitialised storage: the fill below touches every entry on the
+    // threads, where a vector's value-initialisation wrote GBs serially)
+    // (int32 pairs: n < 2^31 is checked below; half the bytes to write)
+    std::unique_ptr<std::pair<int32_t, int32_t>[]> useg;
     {
-        vector<i64> fill(ucnt.begin(), ucnt.end() - 1);
-        for (i64 j = 0; j < n; ++j)
-            for (i64 i = xusub[j]; i < xusub[j + 1]; ++i) {
-                const i64 irow = usub[i], gb = supno[irow];
-                SLU_REQUIRE(gb < supno[j], "usub: row %lld of column %lld is not above the diagonal block",
-                            (long long)irow, (long long)j);
-                useg[fill[gb]++] = {j, irow};
+        const int NCH = std::max(1, std::min(4 * slu::plan_threads(), (int)std::min<i64>(n, 64)));
+        vector<i64> cb(NCH + 1, 0); // chunk c: columns [cb[c], cb[c + 1])
+        for (int c = 1; c < NCH; ++c) {
+            const i64 target = (i64)xusub[n] * c / NCH;
+            cb[c] = std::max(cb[c - 1], (i64)(std::lower_bound(xusub, xusub + n + 1, (int_t)target) - xusub));
+        }
+        cb[NCH] = n;
+        vector<i64> cc((size_t)NCH * ns, 0); // [chunk][block row] counts, then fill cursors
+        std::atomic<int> bad(0);
+        slu::parallel_for(NCH, [&](int c) {
+            i64 *cnt = cc.data() + (size_t)c * ns;
+            for (i64 j = cb[c]; j < cb[c + 1]; ++j)
+                for (i64 i = xusub[j]; i < xusub[j + 1]; ++i) {
+                    const i64 gb = supno[usub[i]];
+                    if (gb >= supno[j]) bad = 1;
+                    else cnt[gb]++;
+                }
+        }, 1);
+        SLU_REQUIRE(!bad, "usub: a row is not above its column's diagonal block");
+        dtick("U segments: counts");
+        // bucket sizes, offsets, and per (chunk, bucket) start positions
+        const int NB = (int)((ns + 4095) / 4096);
+        slu::parallel_for(NB, [&](int t) {
+            for (i64 gb = (i64)t * 4096; gb < std::min<i64>(ns, (i64)(t + 1) * 4096); ++gb) {
+                i64 tot = 0;
+                for (int c = 0; c < NCH; ++c) tot += cc[(size_t)c * ns + gb];
+                ucnt[gb + 1] = tot;
             }
+        }, 1);
+        for (i64 k = 0; k < ns; ++k) ucnt[k + 1] += ucnt[k];
+        slu::parallel_for(NB, [&](int t) {
+            for (i64 gb = (i64)t * 4096; gb < std::min<i64>(ns, (i64)(t + 1) * 4096); ++gb) {
+                i64 pos = ucnt[gb];
+                for (int c = 0; c < NCH; ++c) {
+                    const i64 k = cc[(size_t)c * ns + gb];
+                    cc[(size_t)c * ns + gb] = pos;
+                    pos += k;
+                }
+            }
+        }, 1);
+        SLU_REQUIRE(n < INT32_MAX, "distribute: n = %lld too large", (long long)n);
+        dtick("U segments: offsets");
+        useg.reset(new std::pair<int32_t, int32_t>[(size_t)ucnt[ns]]);
+        slu::parallel_for(NCH, [&](int c) {
+            i64 *fill = cc.data() + (size_t)c * ns;
+            for (i64 j = cb[c]; j < cb[c + 1]; ++j)
+                for (i64 i = xusub[j]; i < xusub[j + 1]; ++i) {
+                    const i64 irow = usub[i];
+                    useg[fill[supno[irow]]++] = {(int32_t)j, (int32_t)irow};
+                }
+        }, 1);
     }
 
     LUstruct *LU = (LUstruct *)calloc(1, sizeof(LUstruct));
@@ -108,6 +167,8 @@ void *distribute_glu_t(i64 n, const int_t *xsup_in, const int_t *supno_in, const
     LU->Llu = Llu;
     LU->dt = sizeof(T) == 4 ? 's' : sizeof(T) == 8 ? 'd' : 'z';
 
+    if (dtime) fprintf(stderr, "[distribute] %lld U segments\n", (long long)ucnt[ns]);
+    dtick("U segments");
     // ---- U: per block row and process column, the reference's Urb_length,
     //      Urb_fstnz, Ucbs (:786-791) -> index / value sizes; bufmax[2], [3]
     //      over all ranks; the schedule arrays (:779-797) for this rank
@@ -157,6 +218,7 @@ void *distribute_glu_t(i64 n, const int_t *xsup_in, const int_t *supno_in, const
             }
     }, 256);
 
+    dtick("U sizes");
     // ---- L: per block column and process row, rows and blocks (:1057-1134);
     //      bufmax[0], [1], [4] over all ranks; this rank's sizes
     vector<i64> l_len(nlc, 0), l_nrbl(nlc, 0);
@@ -199,6 +261,7 @@ void *distribute_glu_t(i64 n, const int_t *xsup_in, const int_t *supno_in, const
         Llu->bufmax[4] = std::max<int_t>(Llu->bufmax[4], bmax4[k]);
     }
 
+    dtick("L sizes");
     // ---- contiguous *_dat arrays in local block order (+1 spare element)
     Llu->Lrowind_bc_ptr = (int_t **)calloc(std::max<i64>(nlc, 1), sizeof(int_t *));
     Llu->Lnzval_bc_ptr = (T **)calloc(std::max<i64>(nlc, 1), sizeof(T *));
@@ -220,7 +283,10 @@ void *distribute_glu_t(i64 n, const int_t *xsup_in, const int_t *supno_in, const
     Llu->Lrowind_bc_dat = (int_t *)malloc((li + 1) * sizeof(int_t));
     // a == nullptr: index arrays only (no value storage; the coarse symbolic
     // of frontend.cpp reads the structure of the 1x1 layout)
-    Llu->Lnzval_bc_dat = a ? (T *)malloc((lv + 1) * sizeof(T)) : nullptr;
+    // value arrays zeroed by calloc: fresh zero pages from the kernel for
+    // these sizes, so only the pages A's entries land on are ever touched
+    // here (the factorization writes the rest; 16.8 GB at 100^3)
+    Llu->Lnzval_bc_dat = a ? (T *)calloc((size_t)(lv + 1), sizeof(T)) : nullptr;
     SLU_REQUIRE(Llu->Lrowind_bc_dat && (Llu->Lnzval_bc_dat || !a), "distribute: out of host memory (L)");
     Llu->Lrowind_bc_dat[li] = 0;
     if (a) Llu->Lnzval_bc_dat[lv] = zero_of<T>();
@@ -242,11 +308,12 @@ void *distribute_glu_t(i64 n, const int_t *xsup_in, const int_t *supno_in, const
     Llu->Ufstnz_br_cnt = ui + 1;
     Llu->Unzval_br_cnt = uv + 1;
     Llu->Ufstnz_br_dat = (int_t *)malloc((ui + 1) * sizeof(int_t));
-    Llu->Unzval_br_dat = a ? (T *)malloc((uv + 1) * sizeof(T)) : nullptr;
+    Llu->Unzval_br_dat = a ? (T *)calloc((size_t)(uv + 1), sizeof(T)) : nullptr;
     SLU_REQUIRE(Llu->Ufstnz_br_dat && (Llu->Unzval_br_dat || !a), "distribute: out of host memory (U)");
     Llu->Ufstnz_br_dat[ui] = 0;
     if (a) Llu->Unzval_br_dat[uv] = zero_of<T>();
 
+    dtick("dat arrays");
     // ---- U block rows (one thread per row: index, zeroed segments, A's values)
     slu::parallel_for((int)nlr, [&](int lb) {
         if (!u_len[lb]) return;
@@ -276,8 +343,7 @@ void *distribute_glu_t(i64 n, const int_t *xsup_in, const int_t *supno_in, const
             const i64 k = klst - irow;
             index[desc + 1] += k;
             if (a) {
-                T *seg = uval + vo;
-                std::fill(seg, seg + k, zero_of<T>());
+                T *seg = uval + vo; // (zero from calloc)
                 for (i64 p = xa[j]; p < xa[j + 1]; ++p) {
                     const i64 r = asub[p];
                     if (r >= irow && r < klst) seg[r - irow] = a[p];
@@ -289,6 +355,7 @@ void *distribute_glu_t(i64 n, const int_t *xsup_in, const int_t *supno_in, const
         SLU_REQUIRE(vo == u_len[lb] && ip == len1, "distribute: U row %lld sizes", (long long)gb);
     }, 16);
 
+    dtick("U rows");
     // ---- L block columns (one thread per column)
     slu::parallel_for((int)nlc, [&](int ljb) {
         if (!l_len[ljb]) return;
@@ -346,7 +413,7 @@ void *distribute_glu_t(i64 n, const int_t *xsup_in, const int_t *supno_in, const
             index[start[s]++] = row;
             pos[row] = cnt[s]++;
         }
-        if (a) std::fill(lusup, lusup + len * w, zero_of<T>());
+        // (lusup is zero from calloc)
         for (i64 c = 0; a && c < w; ++c) {
             const i64 j = f + c;
             for (i64 p = xa[j]; p < xa[j + 1]; ++p) {
@@ -359,6 +426,7 @@ void *distribute_glu_t(i64 n, const int_t *xsup_in, const int_t *supno_in, const
         for (i64 gb : order) blk_of[gb] = -1;
         for (i64 i = xlsub[f]; i < xlsub[f + 1]; ++i) pos[lsub[i]] = -1;
     }, 16);
+    dtick("L columns");
     return LU;
 }
 

@@ -2798,9 +2798,6 @@ struct Plan : PlanBase {
     // own beside the L panel's (both only wait for the diagonal block; near
     // the root each is a few slabs, latency-bound)
     int trsm_2stream = getenv("SLU_TRSM_2STREAM") ? atoi(getenv("SLU_TRSM_2STREAM")) : 1;
-    // SLU_TRSM_WV=1 (default): k_trsm_wv (wave-independent, operands from
-    // L2); 0: k_trsm_reg (LDS-staged blocks)
-    int trsm_wv = getenv("SLU_TRSM_WV") ? atoi(getenv("SLU_TRSM_WV")) : 0;
     void launch_trsm_fast(const LevelRange &R, hipStream_t st) {
         // the U launch on ustream when both panels have slabs
         const bool two = trsm_2stream && ustream && st == pstream && R.lf_n && R.uf_n;
@@ -2816,31 +2813,6 @@ struct Plan : PlanBase {
             if (R.uf_n)
                 hipLaunchKernelGGL((k_trsm_blk<T, 1>), dim3(R.uf_n), dim3(256), 0, su,
                                    d_uf.p + R.uf_off);
-        } else if (trsm_wv) {
-            // wave-independent form, instantiated for the level's widest
-            // TRSM supernode (narrow levels: more workgroups per CU)
-            if (R.tf_maxw <= 64) {
-                if (R.lf_n)
-                    hipLaunchKernelGGL((k_trsm_wv<T, 0, 64>), dim3(R.lf_n), dim3(64 * TR_WAVES), 0, st,
-                                       d_lf.p + R.lf_off);
-                if (R.uf_n)
-                    hipLaunchKernelGGL((k_trsm_wv<T, 1, 64>), dim3(R.uf_n), dim3(64 * TR_WAVES), 0, su,
-                                       d_uf.p + R.uf_off);
-            } else if (R.tf_maxw <= 128) {
-                if (R.lf_n)
-                    hipLaunchKernelGGL((k_trsm_wv<T, 0, 128>), dim3(R.lf_n), dim3(64 * TR_WAVES), 0, st,
-                                       d_lf.p + R.lf_off);
-                if (R.uf_n)
-                    hipLaunchKernelGGL((k_trsm_wv<T, 1, 128>), dim3(R.uf_n), dim3(64 * TR_WAVES), 0, su,
-                                       d_uf.p + R.uf_off);
-            } else {
-                if (R.lf_n)
-                    hipLaunchKernelGGL((k_trsm_wv<T, 0>), dim3(R.lf_n), dim3(64 * TR_WAVES), 0, st,
-                                       d_lf.p + R.lf_off);
-                if (R.uf_n)
-                    hipLaunchKernelGGL((k_trsm_wv<T, 1>), dim3(R.uf_n), dim3(64 * TR_WAVES), 0, su,
-                                       d_uf.p + R.uf_off);
-            }
         } else if (R.tf_maxw <= 64 && trsm_narrow) {
             // narrow levels: the 64-wide instantiation (several workgroups per CU)
             if (R.lf_n)

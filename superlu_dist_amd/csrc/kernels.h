@@ -1743,106 +1743,4 @@ k_trsm_reg(const TrsmItemF<T> *items) {
     }
 }
 
-// TRSM, wave-independent form (replaces k_trsm_reg on the real types).
-// Each wave owns 16 rows of the 64-row slab and runs the 32-column block
-// recurrence X_b = (X_b - X_{<b} T_{<b,b}) Dinv_b on its own: X in MFMA
-// A-operand registers (lane keeps X[row lane&15][4s + lane>>4]), the B
-// operands -- T_{<b,b} from the diagonal block, Dinv_b -- straight from
-// global memory into registers (every slab of a level reads the same
-// diagonal block: L2 / L1 hits), the C -> A layout change through a 16 x 33
-// LDS tile private to the wave.  No workgroup barrier and no LDS staging:
-// the loads of T / Dinv do not depend on X, so the compiler issues them
-// ahead of the MFMAs they feed, where k_trsm_reg staged every block through
-// LDS behind two barriers per block (one global round trip per block on the
-// critical path: 118-165 us for a 256-wide panel).
-// MODE 0: X := X U^{-1} (L panel rows, column-major, ld ldx), T(i, c) =
-// U(i, c) = t[i + c ldt]; MODE 1: U columns as rows (segments from t0),
-// X := X L^{-T}, T(i, c) = L(c, i) = t[c + i ldt].
-template <typename T, int MODE, int MAXW = FAST_MAXW>
-__global__ void __launch_bounds__(64 * TR_WAVES, MAXW <= 64 ? 4 : MAXW <= 128 ? 2 : 1)
-k_trsm_wv(const TrsmItemF<T> *items) {
-    constexpr int PW = 32, NKS = MAXW / 4, NBMAX = MAXW / PW;
-    using Sx = S<T>;
-    using M = Mma<T>;
-    const TrsmItemF<T> it = items[blockIdx.x];
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int w = it.w, nb = (w + PW - 1) / PW;
-    __shared__ T sW[TR_WAVES][16][PW + 1];
-    T (*W)[PW + 1] = sW[wid];
-    if (wid * 16 >= it.nrows) return; // (no workgroup barrier below)
-    const int rl = lane & 15, kq = lane >> 4;
-    const int myr = wid * 16 + rl;
-    const bool rv = myr < it.nrows;
-    int64_t rbase = 0;
-    int t0 = 0;
-    if (MODE == 1 && rv) {
-        t0 = it.t0[myr];
-        rbase = it.voff[myr] - t0;
-    }
-    T xa[NKS];
-#pragma unroll
-    for (int s = 0; s < NKS; ++s) {
-        const int k = 4 * s + kq;
-        T v = Sx::zero();
-        if (rv && k < w) {
-            if (MODE == 0) v = it.x[myr + (int64_t)k * it.ldx];
-            else if (k >= t0) v = it.x[rbase + k];
-        }
-        xa[s] = v;
-    }
-    // T(i, c) of this mode, c clamped into the block (columns >= w read 0)
-    auto tb = [&](int i, int c) -> T {
-        const int cc = min(c, w - 1);
-        const T *src = MODE == 0 ? it.t + i + (int64_t)cc * it.ldt : it.t + cc + (int64_t)i * it.ldt;
-        return keep_if(c < w, gld(src));
-    };
-#pragma unroll
-    for (int b = 0; b < NBMAX; ++b) {
-        if (b >= nb) break;
-        typename M::acc_t a0 = M::zero(), a1 = M::zero();
-#pragma unroll
-        for (int s = 0; s < 8 * b; ++s) {
-            const int i = 4 * s + kq;
-            M::step(a0, xa[s], tb(i, b * PW + rl));
-            M::step(a1, xa[s], tb(i, b * PW + 16 + rl));
-        }
-        // Z = X_b - acc: acc (C layout) -> the wave's tile, read back in A layout
-        // (one wave: its LDS accesses complete in order)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            W[M::row(lane, i)][rl] = M::get(a0, i);
-            W[M::row(lane, i)][16 + rl] = M::get(a1, i);
-        }
-        asm volatile("" ::: "memory");
-        T za[8];
-#pragma unroll
-        for (int s = 0; s < 8; ++s) za[s] = Sx::fms(xa[8 * b + s], W[rl][4 * s + kq], one_of(xa[0]));
-        asm volatile("" ::: "memory");
-        const T *dv = it.dinv + (int64_t)b * PW * PW;
-        typename M::acc_t c0 = M::zero(), c1 = M::zero();
-#pragma unroll
-        for (int s = 0; s < 8; ++s) {
-            M::step(c0, za[s], gld(dv + (4 * s + kq) * PW + rl));
-            M::step(c1, za[s], gld(dv + (4 * s + kq) * PW + 16 + rl));
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            W[M::row(lane, i)][rl] = M::get(c0, i);
-            W[M::row(lane, i)][16 + rl] = M::get(c1, i);
-        }
-        asm volatile("" ::: "memory");
-#pragma unroll
-        for (int s = 0; s < 8; ++s) xa[8 * b + s] = W[rl][4 * s + kq];
-        asm volatile("" ::: "memory");
-    }
-#pragma unroll
-    for (int s = 0; s < NKS; ++s) {
-        const int k = 4 * s + kq;
-        if (rv && k < w) {
-            if (MODE == 0) it.x[myr + (int64_t)k * it.ldx] = xa[s];
-            else if (k >= t0) it.x[rbase + k] = xa[s];
-        }
-    }
-}
-
 } // namespace slu

@@ -896,6 +896,16 @@ void slu_symbfact_arrays(const void *h, int64_t *xsup, int64_t *supno, int64_t *
     if (!R.usub.empty()) memcpy(usub, R.usub.data(), R.usub.size() * sizeof(int64_t));
 }
 
+void slu_symbfact_views(const void *h, const int64_t **ptrs) {
+    const Result &R = *(const Result *)h;
+    ptrs[0] = R.xsup.data();
+    ptrs[1] = R.supno.data();
+    ptrs[2] = R.xlsub.data();
+    ptrs[3] = R.lsub.data();
+    ptrs[4] = R.xusub.data();
+    ptrs[5] = R.usub.data();
+}
+
 void slu_symbfact_free(void *h) { delete (Result *)h; }
 
 // 1 when the last symbfact ran its countnz / fixupL epilogue on the GPU

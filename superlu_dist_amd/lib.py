@@ -118,6 +118,7 @@ def lib():
                              C.c_int64]),
         "slu_symbfact_sizes": (None, [P, c_i64p]),
         "slu_symbfact_arrays": (None, [P, c_i64p, c_i64p, c_i64p, c_i64p, c_i64p, c_i64p]),
+        "slu_symbfact_views": (None, [P, C.POINTER(C.c_void_p)]),
         "slu_symbfact_free": (None, [P]),
         "slu_symbfact_last_epilogue_device": (C.c_int, []),
         "METIS_NodeND": (C.c_int, [c_i64p, c_i64p, c_i64p, c_i64p, c_i64p, c_i64p, c_i64p]),

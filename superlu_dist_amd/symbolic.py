@@ -100,6 +100,18 @@ class Symb:
         return len(self.xsup) - 1
 
 
+class _SymbHandle:
+    """Frees a slu_symbfact result when the last array viewing it is gone."""
+
+    def __init__(self, lib_, h):
+        self.lib, self.h = lib_, h
+
+    def __del__(self):
+        if self.h:
+            self.lib.slu_symbfact_free(self.h)
+            self.h = None
+
+
 def symbfact(m, n, colbeg, colend, rowind, etree, relax, maxsuper):
     """rowind: A Pc''s row indices already relabelled by perm_c."""
     cb = np.ascontiguousarray(colbeg, np.int64)
@@ -110,20 +122,22 @@ def symbfact(m, n, colbeg, colend, rowind, etree, relax, maxsuper):
     h = L.slu_symbfact(m, n, as_i64p(cb), as_i64p(ce), as_i64p(ri), as_i64p(et), relax, maxsuper)
     if not h:
         raise RuntimeError(last_error())
-    try:
-        sz = np.zeros(7, np.int64)
-        L.slu_symbfact_sizes(h, as_i64p(sz))
-        ns, nl, nu = int(sz[0]), int(sz[1]), int(sz[2])
-        xsup = np.zeros(n + 1, np.int64)
-        supno = np.zeros(n + 1, np.int64)
-        xlsub = np.zeros(n + 1, np.int64)
-        xusub = np.zeros(n + 1, np.int64)
-        lsub = np.zeros(max(nl, 1), np.int64)
-        usub = np.zeros(max(nu, 1), np.int64)
-        L.slu_symbfact_arrays(h, as_i64p(xsup), as_i64p(supno), as_i64p(xlsub), as_i64p(lsub),
-                              as_i64p(xusub), as_i64p(usub))
-    finally:
-        L.slu_symbfact_free(h)
+    # the library's arrays in place (no copy of the GBs of lsub / usub at
+    # 100^3): each view's buffer keeps the owner alive, which frees the
+    # handle when the last view goes
+    sz = np.zeros(7, np.int64)
+    L.slu_symbfact_sizes(h, as_i64p(sz))
+    ns, nl, nu = int(sz[0]), int(sz[1]), int(sz[2])
+    owner = _SymbHandle(L, h)
+    ptrs = (C.c_void_p * 6)()
+    L.slu_symbfact_views(h, ptrs)
+
+    def view(i, ln):
+        buf = (C.c_int64 * max(ln, 0)).from_address(ptrs[i]) if ln and ptrs[i] else (C.c_int64 * 0)()
+        buf._owner = owner
+        return np.frombuffer(buf, dtype=np.int64)
+    xsup, supno, xlsub = view(0, n + 1), view(1, n + 1), view(2, n + 1)
+    lsub, xusub, usub = view(3, nl), view(4, n + 1), view(5, nu)
     return Symb(xsup[:ns + 1], supno, xlsub, lsub[:nl], xusub, usub[:nu], int(sz[3]),
                 int(sz[4]), int(sz[5]), -int(sz[6]))
 

@@ -113,7 +113,7 @@ def recv_volumes(lvl, sn, pr, pc):
     return vol
 
 
-def model(rows, vol, pr, pc, bw, lat):
+def model(rows, vol, pr, pc, bw, lat, chunks=1, trsm_scale=1.0):
     P = pr * pc
     waves = lambda t: max(1, math.ceil(t / 512))  # noqa: E731
     chain, schur = [], []
@@ -125,10 +125,15 @@ def model(rows, vol, pr, pc, bw, lat):
             continue
         recv = vol[L]
         ncoll = (pr > 1) + (pc > 1)  # one grouped diag broadcast + one grouped panel broadcast
-        comm = 2 * ncoll * lat * 1e-3 + recv / bw / 1e6
-        chain.append(r["diag"] + r["trsm"] / ((pr + pc) / 2) + comm)
+        xfer = recv / bw / 1e6
+        # chunks > 1: the panel sections go out in `chunks` groups and the
+        # level's Schur tiles start with the first one (the rest of the
+        # transfer runs beside the level's own update)
+        comm = (2 + chunks - 1) * ncoll * lat * 1e-3 + xfer / chunks
+        chain.append(r["diag"] + trsm_scale * r["trsm"] / ((pr + pc) / 2) + comm)
         tiles = r["big"] + r["small"]
-        schur.append(r["schur"] * waves(tiles / P) / waves(tiles))
+        s1 = r["schur"] * waves(tiles / P) / waves(tiles)
+        schur.append(max(s1, xfer * (chunks - 1) / chunks + s1 / chunks) if chunks > 1 else s1)
     if P == 1:
         return sum(r["wall"] for r in rows), chain, schur
     t = chain[0] + sum(max(schur[i], chain[i + 1] if i + 1 < len(rows) else 0.0)
@@ -148,6 +153,10 @@ def main():
                     help="measured 1-GPU factor time (ms); default: sum of the log's level walls")
     ap.add_argument("--diag-scale", type=float, default=1.0,
                     help="what-if: multiply every level's diagonal-LU time (grid chains only)")
+    ap.add_argument("--trsm-scale", type=float, default=1.0,
+                    help="what-if: multiply every level's TRSM time (grid chains only)")
+    ap.add_argument("--chunks", type=int, default=1,
+                    help="panel exchange in this many groups, the Schur update starting with the first")
     a = ap.parse_args()
     rows = parse_log(a.log)
     t1, _, _ = model(rows, None, 1, 1, a.bw, a.lat)
@@ -157,10 +166,10 @@ def main():
     if a.t1:
         t1 = a.t1
     out = {"levels": len(rows), "bw_GBs": a.bw, "lat_us": a.lat, "t1_ms": round(t1, 1),
-           "diag_scale": a.diag_scale}
+           "diag_scale": a.diag_scale, "trsm_scale": a.trsm_scale, "chunks": a.chunks}
     for pr, pc in ((1, 2), (2, 2), (2, 4), (4, 2)):
         vol = recv_volumes(lvl, sn, pr, pc)
-        t, chain, schur = model(rows, vol, pr, pc, a.bw, a.lat)
+        t, chain, schur = model(rows, vol, pr, pc, a.bw, a.lat, a.chunks, a.trsm_scale)
         bound = sum(1 for i in range(len(rows) - 1) if chain[i + 1] > schur[i])
         out[f"{pr}x{pc}"] = {"t_ms": round(t, 1), "speedup": round(t1 / t, 2),
                              "levels_chain_bound": bound,
