@@ -518,6 +518,16 @@ struct LevelRange {
     double schur_flops = 0, big_flops = 0;
     int atomic_tiles = 0; // tiles of supernodes whose destinations collide within the level
     bool big = false;
+    // 2D grids: the level's panel exchange in nch chunks (Plan::pchunks).
+    // Chunk c = row group c of every L panel and column group c of every U
+    // panel; prefix offsets (relative to lf_off, uf_off, pc_off, ps_off and,
+    // for the tiles, to the critical / rest parts of big_off / tile_off) of
+    // each chunk's TRSM items, pack copies, sections and Schur tiles (a tile
+    // waits for the chunks of its rows and of its columns: max of the two)
+    static constexpr int NCHM = 4;
+    int nch = 1;
+    int lf_o[NCHM + 1] = {}, uf_o[NCHM + 1] = {}, pc_o[NCHM + 1] = {}, ps_o[NCHM + 1] = {};
+    int bc_o[NCHM + 1] = {}, br_o[NCHM + 1] = {}, sc_o[NCHM + 1] = {}, sr_o[NCHM + 1] = {};
 };
 
 // one broadcast of a contiguous section of a device arena
@@ -602,6 +612,12 @@ struct Plan : PlanBase {
     hipStream_t stream = nullptr;  // Schur updates that are off the critical path
     hipStream_t pstream = nullptr; // panels, exchanges, critical Schur tiles
     hipStream_t ustream = nullptr; // the U panels' TRSM beside the L panels' (launch_trsm_fast)
+    // 2D grids: the exchanges on a stream of their own, between events from
+    // the panel stream (packed sections) and to the panel and Schur streams
+    // (received chunks): the next chunk's TRSM runs beside the current
+    // chunk's transfer, a chunk's Schur tiles start when it is in
+    hipStream_t cstream = nullptr;
+    hipEvent_t ev_pk = nullptr, ev_dx = nullptr, ev_cx[LevelRange::NCHM] = {};
     vector<hipEvent_t> ev_pan, ev_rest; // per level
     hipEvent_t ev_start = nullptr, ev_pend = nullptr, ev_tu0 = nullptr, ev_tu1 = nullptr;
     bool xmode = false; // 2D grid with exchanges
@@ -627,6 +643,22 @@ struct Plan : PlanBase {
     vector<const int_t *> uidx; // U(k,:) on my process column or null
     vector<vector<i64>> xL, xU; // received index blobs (own the remote lidx/uidx)
     vector<i64> lpos, upos;     // remote panel value offsets in d_pan (-1: local / none)
+    // Chunked panel exchange (2D grids, SLU_PANEL_CHUNKS, default 4; 1 =
+    // one exchange per level): supernode k's L panel rows on my process row
+    // in groups of lgsz[k] rows (a multiple of 128, so every Schur tile and
+    // TRSM slab lies in one group), its U panel columns on my process column
+    // in groups of ucsz[k] columns; lgpos / ugpos: each received group's
+    // offset in d_pan (an L group column-major with ld = its rows); ugrun:
+    // the U panel's value offset at each group's first column
+    static constexpr int NCHM = LevelRange::NCHM;
+    int pchunks = 1;
+    vector<int> lgsz, ucsz, ucols;
+    vector<std::array<i64, NCHM>> lgpos, ugpos, ugrun;
+    int ngroups(int len, int gsz) const { return len > 0 ? (len + gsz - 1) / gsz : 0; }
+    int group_size(int len) const {
+        const int per = (len + pchunks - 1) / std::max(pchunks, 1);
+        return std::max(128, (per + 127) / 128 * 128);
+    }
     vector<i64> pkg;            // diag package offset in d_dpk (2D grids), -1 none
     vector<i64> dscr;           // 1x1: Dinv offset in the per-level scratch
     i64 dpk_total = 0, pan_total = 0, dscr_max = 0;
@@ -720,6 +752,10 @@ struct Plan : PlanBase {
         comm = c;
         if (o) opts = *o;
         xmode = Pr * Pc > 1;
+        if (xmode) {
+            const char *e = getenv("SLU_PANEL_CHUNKS");
+            pchunks = std::max(1, std::min(NCHM, e ? atoi(e) : 4));
+        }
         SLU_REQUIRE(!xmode || (comm && (comm->world || comm->host_fn || comm->host_p2p)),
                     "a %dx%d grid needs a communicator (slu_comm_create)", Pr, Pc);
         zmode = comm && comm->npdep > 1;
@@ -769,6 +805,7 @@ struct Plan : PlanBase {
         HIPCHK(hipStreamCreateWithPriority(&stream, hipStreamNonBlocking, prio_lo));
         HIPCHK(hipStreamCreateWithPriority(&pstream, hipStreamNonBlocking, prio_hi));
         HIPCHK(hipStreamCreateWithPriority(&ustream, hipStreamNonBlocking, prio_hi));
+        if (xmode) HIPCHK(hipStreamCreateWithPriority(&cstream, hipStreamNonBlocking, prio_hi));
         if (getenv("SLU_PROFILE_PLAN"))
             fprintf(stderr, "[slu plan %d] streams               %6.1f ms\n", iam, ms_since(ts0));
         X.s = pstream;
@@ -886,6 +923,8 @@ struct Plan : PlanBase {
         const size_t L0 = zmode ? phase_lv[zp] : 0, L1 = zmode ? phase_lv[zp + 1] : levels.size();
         for (size_t L = L0; L < L1; ++L) {
             const LevelRange &R = levels[L];
+            // phase 0: the diagonal packages; phase 1: the panels, one flush
+            // per chunk as factor() issues them
             for (int ph = 0; ph < 2; ++ph) {
                 const vector<Sec> &secs = ph ? psecs : dsecs;
                 const int off = ph ? R.ps_off : R.ds_off, cnt = ph ? R.ps_n : R.ds_n;
@@ -896,7 +935,10 @@ struct Plan : PlanBase {
                     std::map<std::pair<int, int>, int> seen;
                     for (int i = 0; i < cnt; ++i) kth[i] = seen[{secs[off + i].g, secs[off + i].root}]++;
                 }
-                for (int i = off; i < off + cnt; ++i) {
+                const int nparts = ph ? R.nch : 1;
+                for (int part = 0; part < nparts; ++part) {
+                const int a0 = ph ? off + R.ps_o[part] : off, a1 = ph ? off + R.ps_o[part + 1] : off + cnt;
+                for (int i = a0; i < a1; ++i) {
                     const Sec &sc = secs[i];
                     const int me = sc.g == G_ROW ? mycol : myrow;
                     const size_t bytes = (size_t)sc.cnt * sizeof(T);
@@ -908,7 +950,7 @@ struct Plan : PlanBase {
                         memset(arena + (size_t)sc.off * sizeof(T), 0, bytes);
                     }
                 }
-                for (int i = off; i < off + cnt; ++i) {
+                for (int i = a0; i < a1; ++i) {
                     const Sec &sc = secs[i];
                     X.section(sc.g, sc.root, sc.mask,
                               sc.off >= 0 ? arena + (size_t)sc.off * sizeof(T) : nullptr,
@@ -919,7 +961,7 @@ struct Plan : PlanBase {
                 X.flush();
                 X.phase = "plan-time exchange";
                 X.level = -1;
-                for (int i = off; i < off + cnt; ++i) {
+                for (int i = a0; i < a1; ++i) {
                     const Sec &sc = secs[i];
                     const int me = sc.g == G_ROW ? mycol : myrow;
                     if (me == sc.root || !(sc.mask >> me & 1)) continue;
@@ -932,6 +974,7 @@ struct Plan : PlanBase {
                                     sc.root, b);
                     ++ns;
                     nb += (i64)bytes;
+                }
                 }
             }
         }
@@ -994,6 +1037,11 @@ struct Plan : PlanBase {
         if (ev_pend) (void)hipEventDestroy(ev_pend);
         if (ev_tu0) (void)hipEventDestroy(ev_tu0);
         if (ev_tu1) (void)hipEventDestroy(ev_tu1);
+        if (ev_pk) (void)hipEventDestroy(ev_pk);
+        if (ev_dx) (void)hipEventDestroy(ev_dx);
+        for (hipEvent_t e : ev_cx)
+            if (e) (void)hipEventDestroy(e);
+        if (cstream) (void)hipStreamDestroy(cstream);
         if (stream) (void)hipStreamDestroy(stream);
         if (pstream) (void)hipStreamDestroy(pstream);
         if (ustream) (void)hipStreamDestroy(ustream);
@@ -1661,11 +1709,53 @@ struct Plan : PlanBase {
         lrows(k, m, r0);
         return m > 0;
     }
+    // U(k,:) on my process column: its nonempty columns (the Schur update's
+    // columns, in order) and the panel's value offset where each group of
+    // csz of them starts (the U panel is the concatenation of the columns'
+    // segments, SRC/superlu_defs.h:152-198)
+    int ucols_runs(int k, int csz, std::array<i64, NCHM> *run) const {
+        if (run) run->fill(0);
+        if (!uidx[k]) return 0;
+        const int_t *ix = uidx[k];
+        const i64 klst = xsup[k + 1];
+        i64 p = SLU_BR_HEADER, r = 0;
+        int nc = 0;
+        for (i64 b = 0; b < ix[0]; ++b) {
+            const int jb = (int)ix[p];
+            for (int c = 0; c < W(jb); ++c) {
+                const i64 fst = ix[p + SLU_UB_DESCRIPTOR + c];
+                if (fst >= klst) continue;
+                if (run && csz > 0 && nc % csz == 0 && nc / csz < NCHM) (*run)[nc / csz] = r;
+                ++nc;
+                r += klst - fst;
+            }
+            p += SLU_UB_DESCRIPTOR + W(jb);
+        }
+        return nc;
+    }
     void layout_values() {
         pkg.assign(nsupers, -1);
         dscr.assign(nsupers, -1);
         lpos.assign(nsupers, -1);
         upos.assign(nsupers, -1);
+        if (xmode) {
+            std::array<i64, NCHM> none;
+            none.fill(-1);
+            lgsz.assign(nsupers, 0);
+            ucsz.assign(nsupers, 0);
+            ucols.assign(nsupers, 0);
+            lgpos.assign(nsupers, none);
+            ugpos.assign(nsupers, none);
+            ugrun.assign(nsupers, none);
+            for (int k = 0; k < nsupers; ++k) {
+                int m, r0;
+                lrows(k, m, r0);
+                lgsz[k] = group_size(m);
+                ucols[k] = ucols_runs(k, 0, nullptr);
+                ucsz[k] = group_size(ucols[k]);
+                ucols_runs(k, ucsz[k], &ugrun[k]);
+            }
+        }
         for (size_t L = 0; L < levels.size(); ++L) {
             LevelRange &R = levels[L];
             const vector<int> &ks = bylev[L];
@@ -1735,9 +1825,18 @@ struct Plan : PlanBase {
             //      U(k,:) along my process column (root = owning row).  The
             //      supernodes of a root are grouped by the set of ranks that
             //      need them (same order on every member), one section per
-            //      group, sent only to those ranks.
+            //      group and chunk, sent only to those ranks.  Chunk c of a
+            //      group holds row group c of its L panels (resp. column group
+            //      c of its U panels): the level's sections go out chunk by
+            //      chunk, the sender's TRSM of the next chunk beside the
+            //      current chunk's transfer, the receivers' Schur tiles of a
+            //      chunk as soon as it is in.
             R.ps_off = (int)psecs.size();
             R.pc_off = (int)pcopy.size();
+            const int nch = pchunks;
+            vector<vector<Sec>> csec(nch);
+            vector<vector<CopyItem<T>>> ccp(nch);
+            vector<vector<char>> ccp_src(nch);
             auto lay_panels = [&](int g, int root, vector<std::pair<uint32_t, int>> &km) {
                 std::sort(km.begin(), km.end());
                 const int me = g == G_ROW ? mycol : myrow;
@@ -1746,7 +1845,7 @@ struct Plan : PlanBase {
                     while (j < km.size() && km[j].first == km[i].first) ++j;
                     const uint32_t mask = km[i].first;
                     const bool rcv = me != root && (mask >> me & 1);
-                    if (mask) {
+                    for (int ch = 0; mask && ch < nch; ++ch) {
                         const i64 start = (me == root || rcv) ? pan_total : -1;
                         i64 cnt = 0;
                         for (size_t q = i; q < j; ++q) {
@@ -1755,27 +1854,37 @@ struct Plan : PlanBase {
                             if (g == G_ROW) {
                                 int m, r0;
                                 lrows(k, m, r0);
-                                len = (i64)m * W(k);
+                                const int gs = lgsz[k], a = ch * gs;
+                                if (a >= m) continue;
+                                const int rows = std::min(gs, m - a);
+                                len = (i64)rows * W(k);
                                 if (me == root) {
                                     const int ljb = k / Pc;
-                                    add_copy(pcopy, pcopy_src, /*src*/ 0, lval_off[ljb] + r0,
-                                             lval_ld[ljb], 1, pan_total, m, m, W(k));
+                                    add_copy(ccp[ch], ccp_src[ch], /*src*/ 0, lval_off[ljb] + r0 + a,
+                                             lval_ld[ljb], 1, pan_total, rows, rows, W(k));
                                 } else if (rcv) {
-                                    lpos[k] = pan_total;
+                                    lgpos[k][ch] = pan_total;
+                                    if (ch == 0) lpos[k] = pan_total;
                                 }
                             } else {
-                                len = uidx[k][1];
+                                const int nc = ucols[k], cs = ucsz[k];
+                                if (ch * cs >= nc) continue;
+                                const i64 r1 = (ch + 1) * cs < nc ? ugrun[k][ch + 1] : (i64)uidx[k][1];
+                                len = r1 - ugrun[k][ch];
+                                if (!len) continue;
                                 if (me == root) {
-                                    add_copy(pcopy, pcopy_src, /*src*/ 1, uval_off[k / Pr], len, 1,
+                                    add_copy(ccp[ch], ccp_src[ch], /*src*/ 1, uval_off[k / Pr] + ugrun[k][ch], len, 1,
                                              pan_total, len, len, 1);
                                 } else if (rcv) {
-                                    upos[k] = pan_total;
+                                    ugpos[k][ch] = pan_total;
+                                    if (ch == 0) upos[k] = pan_total;
                                 }
                             }
                             if (me == root || rcv) pan_total += len;
                             cnt += len;
                         }
-                        psecs.push_back({g, root, 1, start, cnt, mask});
+                        if (!cnt) continue;
+                        csec[ch].push_back({g, root, 1, start, cnt, mask});
                         if (me == root) comm_volume += cnt * __builtin_popcount(mask);
                         else if (rcv) comm_volume += cnt;
                     }
@@ -1796,6 +1905,15 @@ struct Plan : PlanBase {
                         if (k % Pr == r && uidx[k]) km.push_back({cmask(k) & ~(1u << r), k});
                     lay_panels(G_COL, r, km);
                 }
+            R.nch = nch;
+            R.ps_o[0] = R.pc_o[0] = 0;
+            for (int ch = 0; ch < nch; ++ch) {
+                psecs.insert(psecs.end(), csec[ch].begin(), csec[ch].end());
+                pcopy.insert(pcopy.end(), ccp[ch].begin(), ccp[ch].end());
+                pcopy_src.insert(pcopy_src.end(), ccp_src[ch].begin(), ccp_src[ch].end());
+                R.ps_o[ch + 1] = (int)psecs.size() - R.ps_off;
+                R.pc_o[ch + 1] = (int)pcopy.size() - R.pc_off;
+            }
             R.ps_n = (int)psecs.size() - R.ps_off;
             R.pc_n = (int)pcopy.size() - R.pc_off;
             pan_level.push_back(pan_total);
@@ -1810,6 +1928,10 @@ struct Plan : PlanBase {
             for (int k : bylev[L]) {
                 if (lpos[k] >= 0) lpos[k] += slot;
                 if (upos[k] >= 0) upos[k] += slot;
+                for (int ch = 0; ch < NCHM; ++ch) {
+                    if (lgpos[k][ch] >= 0) lgpos[k][ch] += slot;
+                    if (ugpos[k][ch] >= 0) ugpos[k][ch] += slot;
+                }
             }
             for (int i = R.ps_off; i < R.ps_off + R.ps_n; ++i)
                 if (psecs[i].off >= 0) psecs[i].off += slot;
@@ -1869,10 +1991,10 @@ struct Plan : PlanBase {
         vector<DiagItemF<T>> df_items;
         vector<TrsmLItem<T>> tl_items;
         vector<TrsmUItem<T>> tu_items;
-        vector<TrsmItemF<T>> lf_items, uf_items;
+        vector<TrsmItemF<T>> lf_c[NCHM], uf_c[NCHM]; // per exchange chunk
         vector<KInfo<T>> kinfos;
         vector<KInfoHost> khost;
-        vector<TileItem> big[2], small[2]; // [0] critical, [1] rest
+        vector<TileItem> big[2][NCHM], small[2][NCHM]; // [0] critical, [1] rest; per chunk
         vector<CopyItem<T>> dcopy;
         vector<char> dcopy_src;
         vector<int> h_rg, h_ra, h_cg, h_cb, h_pair, h_ct0;
@@ -1934,8 +2056,10 @@ struct Plan : PlanBase {
                 b[V_DF] += O.df_items.size();
                 b[V_TL] += O.tl_items.size();
                 b[V_TU] += O.tu_items.size();
-                b[V_LF] += O.lf_items.size();
-                b[V_UF] += O.uf_items.size();
+                for (int ch = 0; ch < NCHM; ++ch) {
+                    b[V_LF] += O.lf_c[ch].size();
+                    b[V_UF] += O.uf_c[ch].size();
+                }
                 b[V_K] += O.kinfos.size();
                 b[V_DC] += O.dcopy.size();
                 b[V_RG] += O.h_rg.size();
@@ -1962,6 +2086,31 @@ struct Plan : PlanBase {
             h_pair.resize_uninit(b[V_PAIR]);
         }
         t_resize += ms_since(tm0);
+        // the TRSM items of a level chunk by chunk (each chunk's items of all
+        // the level's supernode groups together), so that one launch covers
+        // a chunk
+        vector<std::array<i64, NCHM>> lfpos(NC), ufpos(NC);
+        for (int L = 0; L < NL; ++L) {
+            LevelRange &R = levels[L];
+            i64 pl = base[first[L]][V_LF], pu = base[first[L]][V_UF];
+            const i64 l0 = pl, u0 = pu;
+            R.lf_o[0] = R.uf_o[0] = 0;
+            for (int ch = 0; ch < NCHM; ++ch) {
+                for (int t = first[L]; t < first[L + 1]; ++t) {
+                    lfpos[t][ch] = pl;
+                    ufpos[t][ch] = pu;
+                    pl += outs[t].lf_c[ch].size();
+                    pu += outs[t].uf_c[ch].size();
+                }
+                if (ch < R.nch) {
+                    R.lf_o[ch + 1] = (int)(pl - l0);
+                    R.uf_o[ch + 1] = (int)(pu - u0);
+                } else {
+                    SLU_REQUIRE(pl - l0 == R.lf_o[R.nch] && pu - u0 == R.uf_o[R.nch],
+                                "level %d: TRSM items past the level's %d chunks", L, R.nch);
+                }
+            }
+        }
         const auto tp0 = std::chrono::steady_clock::now();
         parallel_for(NC, [&](int c) {
             SchedOut &O = outs[c];
@@ -1976,10 +2125,11 @@ struct Plan : PlanBase {
                 k.ra = shift(k.ra, br);
                 k.pair = shift(k.pair, bp);
             }
-            for (auto &t : O.uf_items) {
-                t.voff = shift(t.voff, bc);
-                t.t0 = shift(t.t0, bc);
-            }
+            for (auto &v : O.uf_c)
+                for (auto &t : v) {
+                    t.voff = shift(t.voff, bc);
+                    t.t0 = shift(t.t0, bc);
+                }
             for (auto &t : O.tu_items) {
                 t.voff = shift(t.voff, bc);
                 t.t0 = shift(t.t0, bc);
@@ -1991,8 +2141,10 @@ struct Plan : PlanBase {
             put(df_items, O.df_items, B[V_DF]);
             put(tl_items, O.tl_items, B[V_TL]);
             put(tu_items, O.tu_items, B[V_TU]);
-            put(lf_items, O.lf_items, B[V_LF]);
-            put(uf_items, O.uf_items, B[V_UF]);
+            for (int ch = 0; ch < NCHM; ++ch) {
+                put(lf_items, O.lf_c[ch], lfpos[c][ch]);
+                put(uf_items, O.uf_c[ch], ufpos[c][ch]);
+            }
             put(kinfos, O.kinfos, B[V_K]);
             for (size_t i = 0; i < O.khost.size(); ++i) khost[B[V_K] + i] = std::move(O.khost[i]);
             put(dcopy, O.dcopy, B[V_DC]);
@@ -2036,22 +2188,37 @@ struct Plan : PlanBase {
             }
             // critical tiles first: they are launched ahead of the rest so the
             // next level's panels can be factored while the rest runs
-            for (int cls = 0; cls < 2; ++cls)
-                for (int t = first[L]; t < first[L + 1]; ++t) {
-                    const int kb = (int)(base[t][V_K] - R.k_off);
-                    for (TileItem x : outs[t].big[cls]) {
-                        x.kslot += kb;
-                        tiles_big.push_back(x);
+            // (chunk by chunk within each class: prefix offsets bc_o / br_o,
+            // sc_o / sr_o relative to the class's first tile)
+            for (int cls = 0; cls < 2; ++cls) {
+                const int b0 = (int)tiles_big.size(), s0 = (int)tiles.size();
+                int *bo = cls ? R.br_o : R.bc_o, *so = cls ? R.sr_o : R.sc_o;
+                bo[0] = so[0] = 0;
+                for (int ch = 0; ch < NCHM; ++ch) {
+                    for (int t = first[L]; t < first[L + 1]; ++t) {
+                        const int kb = (int)(base[t][V_K] - R.k_off);
+                        for (TileItem x : outs[t].big[cls][ch]) {
+                            x.kslot += kb;
+                            tiles_big.push_back(x);
+                        }
+                        for (TileItem x : outs[t].small[cls][ch]) {
+                            x.kslot += kb;
+                            tiles.push_back(x);
+                        }
                     }
-                    for (TileItem x : outs[t].small[cls]) {
-                        x.kslot += kb;
-                        tiles.push_back(x);
-                    }
-                    if (cls == 0) {
-                        R.bigc_n += (int)outs[t].big[0].size();
-                        R.tilec_n += (int)outs[t].small[0].size();
+                    if (ch < R.nch) {
+                        bo[ch + 1] = (int)tiles_big.size() - b0;
+                        so[ch + 1] = (int)tiles.size() - s0;
+                    } else {
+                        SLU_REQUIRE((int)tiles_big.size() - b0 == bo[R.nch] && (int)tiles.size() - s0 == so[R.nch],
+                                    "level %d: Schur tiles past the level's %d chunks", L, R.nch);
                     }
                 }
+                if (cls == 0) {
+                    R.bigc_n = bo[R.nch];
+                    R.tilec_n = so[R.nch];
+                }
+            }
             R.big_n = (int)tiles_big.size() - R.big_off;
             R.df_n = (int)(B1[V_DF] - B0[V_DF]);
             for (int i = R.df_off; i < R.df_off + R.df_n; ++i) R.df_maxw = std::max(R.df_maxw, df_items[i].w);
@@ -2154,7 +2321,7 @@ struct Plan : PlanBase {
                     t.ldt = dld;
                     t.w = w;
                     t.nrows = std::min(RB, m - c0);
-                    O.lf_items.push_back(t);
+                    O.lf_c[xmode ? c0 / lgsz[k] : 0].push_back(t); // (RB divides the group size)
                     O.n_trsm_items++;
                 }
             } else {
@@ -2191,7 +2358,12 @@ struct Plan : PlanBase {
                     any = true;
                     O.h_cg.push_back((int)xsup[jb] + c);
                     O.h_cb.push_back(bidx);
-                    O.h_cvoff.push_back(base + run);
+                    if (xmode && !urow_here) { // received in column groups (layout_values)
+                        const int g = ncols / ucsz[k];
+                        O.h_cvoff.push_back(ugpos[k][g] + run - ugrun[k][g]);
+                    } else {
+                        O.h_cvoff.push_back(base + run);
+                    }
                     const int t0 = (int)(fst - xsup[k]);
                     O.h_ct0.push_back(t0);
                     kmin = std::min(kmin, t0);
@@ -2220,7 +2392,7 @@ struct Plan : PlanBase {
                 t.ldt = dld;
                 t.w = w;
                 t.nrows = std::min(RB, ncols - c0);
-                O.uf_items.push_back(t);
+                O.uf_c[xmode ? c0 / ucsz[k] : 0].push_back(t);
                 O.n_trsm_items++;
             }
             for (int c0 = 0; !fast && c0 < ncols; c0 += TRSM_THREADS) {
@@ -2242,17 +2414,9 @@ struct Plan : PlanBase {
         if (m == 0 || ncols == 0) return; // nothing to update from k here
         // ---- Schur update of k on this rank's destinations
         KInfo<T> ki{};
-        if (lcol_here) {
-            ki.a = d_L.p + lval_off[ljb] + r0;
-            ki.lda = lval_ld[ljb];
-        } else {
-            SLU_REQUIRE(lpos[k] >= 0, "L panel %d not received", k);
-            ki.a = d_pan.p + lpos[k];
-            ki.lda = m;
-        }
+        if (!lcol_here) SLU_REQUIRE(lpos[k] >= 0, "L panel %d not received", k);
         SLU_REQUIRE(urow_here || upos[k] >= 0, "U panel %d not received", k);
         ki.ubase = urow_here ? d_U.p : d_pan.p;
-        ki.m = m;
         ki.n = ncols;
         ki.kmin = kmin;
         ki.kw = w - kmin;
@@ -2279,8 +2443,6 @@ struct Plan : PlanBase {
                 p += SLU_LB_DESCRIPTOR + nr;
             }
         }
-        ki.rg = (const int *)(intptr_t)rows_off;
-        ki.ra = (const int *)(intptr_t)rows_off;
         const int pair_off = (int)O.h_pair.size();
         KInfoHost kh;
         for (int ib : lib_)
@@ -2305,34 +2467,61 @@ struct Plan : PlanBase {
         if (ksplit_tiles > 0 && big && bylev[level_of[k]].size() <= 2 && tm * tn < ksplit_tiles)
             nsplit = std::max(1, std::min({4, (w - kmin) / 64, ksplit_tiles / (tm * tn)}));
         const int kch = ((w - kmin + nsplit - 1) / nsplit + 15) / 16 * 16;
-        const int slot0 = (int)O.kinfos.size(); // relocated by the merge
-        for (int c = 0; c < nsplit; ++c) {
-            KInfo<T> kc = ki;
-            kc.kmin = kmin + c * kch;
-            kc.kw = std::min(kch, w - kc.kmin);
-            if (kc.kw <= 0) {
-                nsplit = c;
-                break;
-            }
-            O.kinfos.push_back(kc);
-            O.khost.push_back(kh);
-        }
         // A destination (ib,jb) belongs to the panel of supernode min(ib,jb);
         // it is critical when that panel is factored at the next level.  All
         // destinations in a row of L block ib (resp. a column of U block jb)
         // with level(ib) == level(k)+1 are critical, and no others.
         const int nl = level_of[k] + 1;
-        vector<char> crow(tm, 0), ccol(tn, 0);
-        for (int r = 0; r < m; ++r)
-            if (level_of[lib_[O.h_ra[rows_off + r]]] == nl) crow[r / BM] = 1;
+        vector<char> ccol(tn, 0);
         for (int c = 0; c < ncols; ++c)
             if (level_of[ujb[O.h_cb[cols_off + c]]] == nl) ccol[c / BN] = 1;
-        for (int c = 0; c < nsplit; ++c)
-            for (int i = 0; i < tm; ++i)
-                for (int j = 0; j < tn; ++j) {
-                    const int cls = (crow[i] || ccol[j]) ? 0 : 1;
-                    (big ? O.big[cls] : O.small[cls]).push_back(TileItem{slot0 + c, i, j});
+        // 2D grids: one KInfo per row group of the L panel (its own rows,
+        // base and leading dimension: a received group is column-major with
+        // ld = its rows), the tiles of a group in the exchange chunk of their
+        // rows and columns
+        const int gs = xmode ? lgsz[k] : m, ng = xmode ? ngroups(m, gs) : 1;
+        for (int g = 0; g < ng; ++g) {
+            const int ga = g * gs, rows = std::min(gs, m - ga);
+            KInfo<T> kg = ki;
+            if (lcol_here) {
+                kg.a = d_L.p + lval_off[ljb] + r0 + ga;
+                kg.lda = lval_ld[ljb];
+            } else if (xmode) {
+                SLU_REQUIRE(lgpos[k][g] >= 0, "L panel %d row group %d not received", k, g);
+                kg.a = d_pan.p + lgpos[k][g];
+                kg.lda = rows;
+            } else {
+                kg.a = d_pan.p + lpos[k];
+                kg.lda = m;
+            }
+            kg.m = rows;
+            kg.rg = (const int *)(intptr_t)(rows_off + ga);
+            kg.ra = (const int *)(intptr_t)(rows_off + ga);
+            const int tmg = (rows + BM - 1) / BM;
+            vector<char> crow(tmg, 0);
+            for (int r = 0; r < rows; ++r)
+                if (level_of[lib_[O.h_ra[rows_off + ga + r]]] == nl) crow[r / BM] = 1;
+            const int slot0 = (int)O.kinfos.size(); // relocated by the merge
+            int ns = nsplit;
+            for (int c = 0; c < ns; ++c) {
+                KInfo<T> kc = kg;
+                kc.kmin = kmin + c * kch;
+                kc.kw = std::min(kch, w - kc.kmin);
+                if (kc.kw <= 0) {
+                    ns = c;
+                    break;
                 }
+                O.kinfos.push_back(kc);
+                O.khost.push_back(kh);
+            }
+            for (int c = 0; c < ns; ++c)
+                for (int i = 0; i < tmg; ++i)
+                    for (int j = 0; j < tn; ++j) {
+                        const int cls = (crow[i] || ccol[j]) ? 0 : 1;
+                        const int ch = xmode ? std::max(g, j * BN / ucsz[k]) : 0;
+                        (big ? O.big[cls][ch] : O.small[cls][ch]).push_back(TileItem{slot0 + c, i, j});
+                    }
+        }
         // algorithmic work: exact unpadded flops and padded flops
         double fl = 0;
         for (int c = 0; c < ncols; ++c) fl += 2.0 * m * (w - O.h_ct0[cols_off + c]);
@@ -2448,6 +2637,11 @@ struct Plan : PlanBase {
         HIPCHK(hipEventCreateWithFlags(&ev_pend, hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&ev_tu0, hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&ev_tu1, hipEventDisableTiming));
+        if (xmode) {
+            HIPCHK(hipEventCreateWithFlags(&ev_pk, hipEventDisableTiming));
+            HIPCHK(hipEventCreateWithFlags(&ev_dx, hipEventDisableTiming));
+            for (hipEvent_t &e : ev_cx) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        }
         d_info.alloc(Pr * Pc);
         stats.lu_bytes = (double)(lval_total + uval_total) * sizeof(T);
         stats.index_bytes = (double)(d_lblk.bytes() + d_lmap.bytes() + d_ublk.bytes() +
@@ -2798,43 +2992,30 @@ struct Plan : PlanBase {
     // own beside the L panel's (both only wait for the diagonal block; near
     // the root each is a few slabs, latency-bound)
     int trsm_2stream = getenv("SLU_TRSM_2STREAM") ? atoi(getenv("SLU_TRSM_2STREAM")) : 1;
-    void launch_trsm_fast(const LevelRange &R, hipStream_t st) {
+    // the level's fast-path TRSM items, or (ch >= 0) those of exchange chunk ch
+    void launch_trsm_fast(const LevelRange &R, hipStream_t st, int ch = -1) {
+        const int lo = R.lf_off + (ch >= 0 ? R.lf_o[ch] : 0), ln = ch >= 0 ? R.lf_o[ch + 1] - R.lf_o[ch] : R.lf_n;
+        const int uo = R.uf_off + (ch >= 0 ? R.uf_o[ch] : 0), un = ch >= 0 ? R.uf_o[ch + 1] - R.uf_o[ch] : R.uf_n;
         // the U launch on ustream when both panels have slabs
-        const bool two = trsm_2stream && ustream && st == pstream && R.lf_n && R.uf_n;
+        const bool two = trsm_2stream && ustream && st == pstream && ln && un;
         hipStream_t su = two ? ustream : st;
         if (two) {
             HIPCHK(hipEventRecord(ev_tu0, st));
             HIPCHK(hipStreamWaitEvent(ustream, ev_tu0, 0));
         }
         if constexpr (cplx) {
-            if (R.lf_n)
-                hipLaunchKernelGGL((k_trsm_blk<T, 0>), dim3(R.lf_n), dim3(256), 0, st,
-                                   d_lf.p + R.lf_off);
-            if (R.uf_n)
-                hipLaunchKernelGGL((k_trsm_blk<T, 1>), dim3(R.uf_n), dim3(256), 0, su,
-                                   d_uf.p + R.uf_off);
+            if (ln) hipLaunchKernelGGL((k_trsm_blk<T, 0>), dim3(ln), dim3(256), 0, st, d_lf.p + lo);
+            if (un) hipLaunchKernelGGL((k_trsm_blk<T, 1>), dim3(un), dim3(256), 0, su, d_uf.p + uo);
         } else if (R.tf_maxw <= 64 && trsm_narrow) {
             // narrow levels: the 64-wide instantiation (several workgroups per CU)
-            if (R.lf_n)
-                hipLaunchKernelGGL((k_trsm_reg<T, 0, 64>), dim3(R.lf_n), dim3(64 * TR_WAVES), 0, st,
-                                   d_lf.p + R.lf_off);
-            if (R.uf_n)
-                hipLaunchKernelGGL((k_trsm_reg<T, 1, 64>), dim3(R.uf_n), dim3(64 * TR_WAVES), 0, su,
-                                   d_uf.p + R.uf_off);
+            if (ln) hipLaunchKernelGGL((k_trsm_reg<T, 0, 64>), dim3(ln), dim3(64 * TR_WAVES), 0, st, d_lf.p + lo);
+            if (un) hipLaunchKernelGGL((k_trsm_reg<T, 1, 64>), dim3(un), dim3(64 * TR_WAVES), 0, su, d_uf.p + uo);
         } else if (R.tf_maxw <= 128 && trsm_narrow >= 2) {
-            if (R.lf_n)
-                hipLaunchKernelGGL((k_trsm_reg<T, 0, 128>), dim3(R.lf_n), dim3(64 * TR_WAVES), 0, st,
-                                   d_lf.p + R.lf_off);
-            if (R.uf_n)
-                hipLaunchKernelGGL((k_trsm_reg<T, 1, 128>), dim3(R.uf_n), dim3(64 * TR_WAVES), 0, su,
-                                   d_uf.p + R.uf_off);
+            if (ln) hipLaunchKernelGGL((k_trsm_reg<T, 0, 128>), dim3(ln), dim3(64 * TR_WAVES), 0, st, d_lf.p + lo);
+            if (un) hipLaunchKernelGGL((k_trsm_reg<T, 1, 128>), dim3(un), dim3(64 * TR_WAVES), 0, su, d_uf.p + uo);
         } else {
-            if (R.lf_n)
-                hipLaunchKernelGGL((k_trsm_reg<T, 0>), dim3(R.lf_n), dim3(64 * TR_WAVES), 0, st,
-                                   d_lf.p + R.lf_off);
-            if (R.uf_n)
-                hipLaunchKernelGGL((k_trsm_reg<T, 1>), dim3(R.uf_n), dim3(64 * TR_WAVES), 0, su,
-                                   d_uf.p + R.uf_off);
+            if (ln) hipLaunchKernelGGL((k_trsm_reg<T, 0>), dim3(ln), dim3(64 * TR_WAVES), 0, st, d_lf.p + lo);
+            if (un) hipLaunchKernelGGL((k_trsm_reg<T, 1>), dim3(un), dim3(64 * TR_WAVES), 0, su, d_uf.p + uo);
         }
         if (two) {
             HIPCHK(hipEventRecord(ev_tu1, ustream));
@@ -3007,60 +3188,134 @@ struct Plan : PlanBase {
                                            d_df.p + R.df_off, thresh, opts.replace_tiny_pivot,
                                            d_counters.p, d_zpiv.p);
                 });
-            if (R.dc_n || R.ds_n)
-                span(4, P, [&] {
+            if (xmode && !opts.serial) {
+                // 2D grid: the exchanges on the comm stream C, the panels in
+                // R.nch chunks.  P: TRSM(c) -> pack(c) -> [C: send / receive
+                // chunk c] for every c, so chunk c + 1's TRSM runs beside
+                // chunk c's transfer; the critical tiles of chunk c (P) and
+                // its rest tiles (Schur stream) start when chunk c is in.
+                hipStream_t C = cstream;
+                auto exchange = [&](const vector<Sec> &secs, int off, int cnt, const char *what, hipEvent_t done) {
+                    HIPCHK(hipEventRecord(ev_pk, P));
+                    HIPCHK(hipStreamWaitEvent(C, ev_pk, 0));
+                    X.s = C;
+                    if (cnt) span(4, C, [&] { issue(secs, off, cnt, what, (int)L); });
+                    HIPCHK(hipEventRecord(done, C));
+                };
+                if (R.dc_n || R.ds_n) {
                     if (R.dc_n)
-                        hipLaunchKernelGGL(k_copy<T>, dim3(R.dc_n), dim3(256), 0, P,
-                                           d_dcopy.p + R.dc_off);
-                    issue(dsecs, R.ds_off, R.ds_n, "diagonal-package exchange", (int)L);
-                });
-            if (R.lf_n || R.uf_n) span(1, P, [&] { launch_trsm_fast(R, P); });
-            if (R.tl_n || R.tu_n)
-                span(1, P, [&] {
-                    if (R.tl_n)
-                        hipLaunchKernelGGL(k_trsm_l<T>, dim3(R.tl_n), dim3(TRSM_THREADS), 0, P,
-                                           d_tl.p + R.tl_off);
-                    if (R.tu_n)
-                        hipLaunchKernelGGL(k_trsm_u<T>, dim3(R.tu_n), dim3(TRSM_THREADS), 0, P,
-                                           d_tu.p + R.tu_off);
-                });
-            if (R.pc_n || R.ps_n)
-                span(4, P, [&] {
-                    if (R.pc_n)
-                        hipLaunchKernelGGL(k_copy<T>, dim3(R.pc_n), dim3(256), 0, P,
-                                           d_pcopy.p + R.pc_off);
-                    issue(psecs, R.ps_off, R.ps_n, "L/U panel exchange", (int)L);
-                });
-            HIPCHK(hipEventRecord(ev_pan[L], P));
-            // critical tiles of L on the panel stream, after the rest of L-1
-            if (L > 0) HIPCHK(hipStreamWaitEvent(P, ev_rest[L - 1], 0));
-            if (R.bigc_n) {
-                span(2, P, [&] { launch_big(R, R.big_off, R.bigc_n, P); });
-                stats.n_schur_launches++;
-                stats.n_schur_big_launches++;
-            }
-            if (R.tilec_n) {
-                span(3, P, [&] { launch_small(R, R.tile_off, R.tilec_n, P); });
-                stats.n_schur_launches++;
-            }
-            // the rest of L on the Schur stream, once the panels of L exist
-            HIPCHK(hipStreamWaitEvent(stream, ev_pan[L], 0));
-            if (R.big_n > R.bigc_n) {
-                // the first rest_split %% of the rest tiles as a launch of their own
-                const int nrest = R.big_n - R.bigc_n;
-                const int n1 = rest_split > 0 && !opts.serial ? (int)((i64)nrest * rest_split / 100) : 0;
-                span(2, stream, [&] {
-                    if (n1 > 0) launch_big(R, R.big_off + R.bigc_n, n1, stream);
-                    if (nrest > n1) launch_big(R, R.big_off + R.bigc_n + n1, nrest - n1, stream);
-                });
-                stats.n_schur_launches++;
-                stats.n_schur_big_launches++;
-            }
-            if (R.tile_n > R.tilec_n) {
-                span(3, stream, [&] {
-                    launch_small(R, R.tile_off + R.tilec_n, R.tile_n - R.tilec_n, stream);
-                });
-                stats.n_schur_launches++;
+                        span(4, P, [&] {
+                            hipLaunchKernelGGL(k_copy<T>, dim3(R.dc_n), dim3(256), 0, P, d_dcopy.p + R.dc_off);
+                        });
+                    exchange(dsecs, R.ds_off, R.ds_n, "diagonal-package exchange", ev_dx);
+                    HIPCHK(hipStreamWaitEvent(P, ev_dx, 0));
+                }
+                for (int ch = 0; ch < R.nch; ++ch) {
+                    if (R.lf_o[ch + 1] > R.lf_o[ch] || R.uf_o[ch + 1] > R.uf_o[ch])
+                        span(1, P, [&] { launch_trsm_fast(R, P, ch); });
+                    if (ch == 0 && (R.tl_n || R.tu_n)) // (wide supernodes' generic items: all in chunk 0)
+                        span(1, P, [&] {
+                            if (R.tl_n)
+                                hipLaunchKernelGGL(k_trsm_l<T>, dim3(R.tl_n), dim3(TRSM_THREADS), 0, P,
+                                                   d_tl.p + R.tl_off);
+                            if (R.tu_n)
+                                hipLaunchKernelGGL(k_trsm_u<T>, dim3(R.tu_n), dim3(TRSM_THREADS), 0, P,
+                                                   d_tu.p + R.tu_off);
+                        });
+                    const int pcn = R.pc_o[ch + 1] - R.pc_o[ch];
+                    if (pcn)
+                        span(4, P, [&] {
+                            hipLaunchKernelGGL(k_copy<T>, dim3(pcn), dim3(256), 0, P, d_pcopy.p + R.pc_off + R.pc_o[ch]);
+                        });
+                    exchange(psecs, R.ps_off + R.ps_o[ch], R.ps_o[ch + 1] - R.ps_o[ch], "L/U panel exchange",
+                             ev_cx[ch]);
+                }
+                // critical tiles of L on the panel stream, after the rest of L-1
+                if (L > 0) HIPCHK(hipStreamWaitEvent(P, ev_rest[L - 1], 0));
+                for (int ch = 0; ch < R.nch; ++ch) {
+                    HIPCHK(hipStreamWaitEvent(P, ev_cx[ch], 0));
+                    const int nb = R.bc_o[ch + 1] - R.bc_o[ch], nsm = R.sc_o[ch + 1] - R.sc_o[ch];
+                    if (nb) {
+                        span(2, P, [&] { launch_big(R, R.big_off + R.bc_o[ch], nb, P); });
+                        stats.n_schur_launches++;
+                        stats.n_schur_big_launches++;
+                    }
+                    if (nsm) {
+                        span(3, P, [&] { launch_small(R, R.tile_off + R.sc_o[ch], nsm, P); });
+                        stats.n_schur_launches++;
+                    }
+                }
+                HIPCHK(hipEventRecord(ev_pan[L], P));
+                // the rest of L on the Schur stream, chunk by chunk as they arrive
+                for (int ch = 0; ch < R.nch; ++ch) {
+                    HIPCHK(hipStreamWaitEvent(stream, ev_cx[ch], 0));
+                    const int nb = R.br_o[ch + 1] - R.br_o[ch], nsm = R.sr_o[ch + 1] - R.sr_o[ch];
+                    if (nb) {
+                        span(2, stream, [&] { launch_big(R, R.big_off + R.bigc_n + R.br_o[ch], nb, stream); });
+                        stats.n_schur_launches++;
+                        stats.n_schur_big_launches++;
+                    }
+                    if (nsm) {
+                        span(3, stream, [&] { launch_small(R, R.tile_off + R.tilec_n + R.sr_o[ch], nsm, stream); });
+                        stats.n_schur_launches++;
+                    }
+                }
+            } else {
+                if (R.dc_n || R.ds_n)
+                    span(4, P, [&] {
+                        if (R.dc_n)
+                            hipLaunchKernelGGL(k_copy<T>, dim3(R.dc_n), dim3(256), 0, P,
+                                               d_dcopy.p + R.dc_off);
+                        issue(dsecs, R.ds_off, R.ds_n, "diagonal-package exchange", (int)L);
+                    });
+                if (R.lf_n || R.uf_n) span(1, P, [&] { launch_trsm_fast(R, P); });
+                if (R.tl_n || R.tu_n)
+                    span(1, P, [&] {
+                        if (R.tl_n)
+                            hipLaunchKernelGGL(k_trsm_l<T>, dim3(R.tl_n), dim3(TRSM_THREADS), 0, P,
+                                               d_tl.p + R.tl_off);
+                        if (R.tu_n)
+                            hipLaunchKernelGGL(k_trsm_u<T>, dim3(R.tu_n), dim3(TRSM_THREADS), 0, P,
+                                               d_tu.p + R.tu_off);
+                    });
+                if (R.pc_n || R.ps_n)
+                    span(4, P, [&] {
+                        if (R.pc_n)
+                            hipLaunchKernelGGL(k_copy<T>, dim3(R.pc_n), dim3(256), 0, P,
+                                               d_pcopy.p + R.pc_off);
+                        issue(psecs, R.ps_off, R.ps_n, "L/U panel exchange", (int)L);
+                    });
+                HIPCHK(hipEventRecord(ev_pan[L], P));
+                // critical tiles of L on the panel stream, after the rest of L-1
+                if (L > 0) HIPCHK(hipStreamWaitEvent(P, ev_rest[L - 1], 0));
+                if (R.bigc_n) {
+                    span(2, P, [&] { launch_big(R, R.big_off, R.bigc_n, P); });
+                    stats.n_schur_launches++;
+                    stats.n_schur_big_launches++;
+                }
+                if (R.tilec_n) {
+                    span(3, P, [&] { launch_small(R, R.tile_off, R.tilec_n, P); });
+                    stats.n_schur_launches++;
+                }
+                // the rest of L on the Schur stream, once the panels of L exist
+                HIPCHK(hipStreamWaitEvent(stream, ev_pan[L], 0));
+                if (R.big_n > R.bigc_n) {
+                    // the first rest_split %% of the rest tiles as a launch of their own
+                    const int nrest = R.big_n - R.bigc_n;
+                    const int n1 = rest_split > 0 && !opts.serial ? (int)((i64)nrest * rest_split / 100) : 0;
+                    span(2, stream, [&] {
+                        if (n1 > 0) launch_big(R, R.big_off + R.bigc_n, n1, stream);
+                        if (nrest > n1) launch_big(R, R.big_off + R.bigc_n + n1, nrest - n1, stream);
+                    });
+                    stats.n_schur_launches++;
+                    stats.n_schur_big_launches++;
+                }
+                if (R.tile_n > R.tilec_n) {
+                    span(3, stream, [&] {
+                        launch_small(R, R.tile_off + R.tilec_n, R.tile_n - R.tilec_n, stream);
+                    });
+                    stats.n_schur_launches++;
+                }
             }
             HIPCHK(hipEventRecord(ev_rest[L], stream));
             if (opts.timing >= 2) lvl_end.push_back(mark_on(stream)); // level wall time
@@ -3081,6 +3336,11 @@ struct Plan : PlanBase {
             }
         }
         }
+        if (xmode && !opts.serial) { // the comm stream's last group before the end of the factorization
+            HIPCHK(hipEventRecord(ev_pend, cstream));
+            HIPCHK(hipStreamWaitEvent(stream, ev_pend, 0));
+        }
+        X.s = opts.serial ? stream : pstream;
         HIPCHK(hipEventRecord(ev_pend, pstream));
         HIPCHK(hipStreamWaitEvent(stream, ev_pend, 0));
         HIPCHK(hipGetLastError());

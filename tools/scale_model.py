@@ -126,14 +126,19 @@ def model(rows, vol, pr, pc, bw, lat, chunks=1, trsm_scale=1.0):
         recv = vol[L]
         ncoll = (pr > 1) + (pc > 1)  # one grouped diag broadcast + one grouped panel broadcast
         xfer = recv / bw / 1e6
-        # chunks > 1: the panel sections go out in `chunks` groups and the
-        # level's Schur tiles start with the first one (the rest of the
-        # transfer runs beside the level's own update)
+        trsm = trsm_scale * r["trsm"] / ((pr + pc) / 2)
+        # chunks > 1 (engine.hip, SLU_PANEL_CHUNKS): the panels go out in
+        # `chunks` groups on the comm stream -- TRSM of chunk c + 1 beside
+        # the transfer of chunk c -- and the level's Schur tiles of a chunk
+        # start when it is in, so the chain to the level's first tiles holds
+        # one chunk's TRSM and transfer, and the rest of both run beside the
+        # level's own update
         comm = (2 + chunks - 1) * ncoll * lat * 1e-3 + xfer / chunks
-        chain.append(r["diag"] + trsm_scale * r["trsm"] / ((pr + pc) / 2) + comm)
+        chain.append(r["diag"] + trsm / chunks + comm)
         tiles = r["big"] + r["small"]
         s1 = r["schur"] * waves(tiles / P) / waves(tiles)
-        schur.append(max(s1, xfer * (chunks - 1) / chunks + s1 / chunks) if chunks > 1 else s1)
+        tail = max(xfer, trsm) * (chunks - 1) / chunks
+        schur.append(max(s1, tail + s1 / chunks) if chunks > 1 else s1)
     if P == 1:
         return sum(r["wall"] for r in rows), chain, schur
     t = chain[0] + sum(max(schur[i], chain[i + 1] if i + 1 < len(rows) else 0.0)
