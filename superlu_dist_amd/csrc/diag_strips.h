@@ -207,21 +207,46 @@ k_diag_strips(const DiagItemF<T> *items, int nitems, unsigned *flags, unsigned e
             }
         }
     };
+    // trail() of rows [lo, hi) on waves w0.. (wn of them), each wave first
+    // loading the rows of L21 (sP rows 32 + ..) its fragments read, from
+    // the published strip r0 (wave-private rows: no barrier)
+    auto trail_rest = [&](int r0, int lo, int hi, int w0, int wn) {
+        const int nfr = hi > lo ? (hi - lo + 15) / 16 : 0;
+        for (int fr = wv - w0; fr < nfr; fr += wn) {
+            T v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int e = lane + 64 * u, r = lo + fr * 16 + (e & 15), k = e >> 4;
+                v[u] = keep_if(r < hi, ld_sc1(A + r0 + PW + min(r, hi - 1) + (int64_t)(r0 + k) * ld));
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int e = lane + 64 * u, r = lo + fr * 16 + (e & 15), k = e >> 4;
+                sP[PW + r][k] = v[u];
+            }
+        }
+        asm volatile("" ::: "memory"); // (one wave: its LDS accesses complete in order)
+        trail(r0, lo, hi, w0, wn);
+    };
     // ---- apply the panels of the strips to my left, in order
     for (int p = 0; p < q; ++p) {
         if (!ds_wait(fl + p, epoch, err, &s_ok)) return;
         const int r0 = p * PW, nr = w - r0;
         DS_PROBE(0);
-        // only L21_p (rows r0 + 32 ..): L_pp enters through its inverse
+        // only L21_p (rows r0 + 32 ..): L_pp enters through its inverse.  The
+        // last panel before my own LU: only its first 64 rows now (the rows
+        // my LU reads); waves 1-3 load the rest beside the LU, each the rows
+        // it updates (trail_rest below)
         const int nb21 = nr - PW, rb = r0 + PW;
-        if (nb21 > 0)
+        const int nst = p + 1 == q ? min(64, nb21) : nb21;
+        if (nst > 0)
             stage_loop<DS_THREADS, DS_TU, T>(
-                tid, nb21 * PW,
+                tid, nst * PW,
                 [&](int e, bool ok) {
-                    const int ee = min(e, nb21 * PW - 1);
-                    return keep_if(ok, ld_sc1(A + rb + ee % nb21 + (int64_t)(r0 + ee / nb21) * ld));
+                    const int ee = min(e, nst * PW - 1);
+                    return keep_if(ok, ld_sc1(A + rb + ee % nst + (int64_t)(r0 + ee / nst) * ld));
                 },
-                [&](int e, T v) { sP[PW + e % nb21][e / nb21] = v; });
+                [&](int e, T v) { sP[PW + e % nst][e / nst] = v; });
         stage_loop<DS_THREADS, 4, T>( // dinvLT: [b][a] = Linv[a][b]
             tid, PW * PW, [&](int e, bool ok) { return keep_if(ok, ld_sc1(dinvLT + (int64_t)p * PW * PW + min(e, PW * PW - 1))); },
             [&](int e, T v) { sLi[e % PW][e / PW] = v; });
@@ -315,7 +340,7 @@ k_diag_strips(const DiagItemF<T> *items, int nitems, unsigned *flags, unsigned e
             s_zp[lane] = 0;
         }
     } else if (q > 0) {
-        trail(c0 - PW, 64, nrow, 1, 3); // the last panel's update of rows c0 + 64 ..
+        trail_rest(c0 - PW, 64, nrow, 1, 3); // the last panel's update of rows c0 + 64 ..
     }
     __syncthreads();
     DS_PROBE(3);

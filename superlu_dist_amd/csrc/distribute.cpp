@@ -38,6 +38,7 @@
 #include <atomic>
 #include <cstdlib>
 #include <chrono>
+#include <sys/mman.h>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -54,6 +55,18 @@ namespace {
 using i64 = int64_t;
 
 template <typename T> inline T zero_of() { return T{}; }
+
+// calloc (free()-able: the reference's Destroy_LU frees the *_dat arrays)
+// with the 2 MB-aligned interior advised as transparent huge pages: the
+// value arrays' first touch (A's entries here, the refill's zeroing, the
+// factor download) then faults once per 2 MB instead of once per 4 KB
+inline void *calloc_huge(size_t n, size_t sz) {
+    void *p = calloc(n, sz);
+    constexpr uintptr_t HP = uintptr_t(2) << 20;
+    const uintptr_t a = ((uintptr_t)p + HP - 1) & ~(HP - 1), e = ((uintptr_t)p + n * sz) & ~(HP - 1);
+    if (p && e > a) madvise((void *)a, e - a, MADV_HUGEPAGE);
+    return p;
+}
 
 // Per-thread scratch of -1s, reset when a new call (generation) first uses
 // it on a thread: parallel_for's workers are fresh threads, but the calling
@@ -286,7 +299,7 @@ void *distribute_glu_t(i64 n, const int_t *xsup_in, const int_t *supno_in, const
     // value arrays zeroed by calloc: fresh zero pages from the kernel for
     // these sizes, so only the pages A's entries land on are ever touched
     // here (the factorization writes the rest; 16.8 GB at 100^3)
-    Llu->Lnzval_bc_dat = a ? (T *)calloc((size_t)(lv + 1), sizeof(T)) : nullptr;
+    Llu->Lnzval_bc_dat = a ? (T *)calloc_huge((size_t)(lv + 1), sizeof(T)) : nullptr;
     SLU_REQUIRE(Llu->Lrowind_bc_dat && (Llu->Lnzval_bc_dat || !a), "distribute: out of host memory (L)");
     Llu->Lrowind_bc_dat[li] = 0;
     if (a) Llu->Lnzval_bc_dat[lv] = zero_of<T>();
@@ -308,7 +321,7 @@ void *distribute_glu_t(i64 n, const int_t *xsup_in, const int_t *supno_in, const
     Llu->Ufstnz_br_cnt = ui + 1;
     Llu->Unzval_br_cnt = uv + 1;
     Llu->Ufstnz_br_dat = (int_t *)malloc((ui + 1) * sizeof(int_t));
-    Llu->Unzval_br_dat = a ? (T *)calloc((size_t)(uv + 1), sizeof(T)) : nullptr;
+    Llu->Unzval_br_dat = a ? (T *)calloc_huge((size_t)(uv + 1), sizeof(T)) : nullptr;
     SLU_REQUIRE(Llu->Ufstnz_br_dat && (Llu->Unzval_br_dat || !a), "distribute: out of host memory (U)");
     Llu->Ufstnz_br_dat[ui] = 0;
     if (a) Llu->Unzval_br_dat[uv] = zero_of<T>();

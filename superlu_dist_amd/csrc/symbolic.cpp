@@ -193,6 +193,12 @@ struct Result {
 // Pivots are diagonal (pivotL, SRC/symbfact.c:729-731), so the reference's
 // perm_r is the identity on the columns done so far: "row r pivoted" is
 // r < j while column j is searched, r <= j while it prunes.
+#ifdef SLU_SYMB_COUNT
+static long long g_cnt[8];
+#define SYMB_CNT(i, v) (g_cnt[i] += (v))
+#else
+#define SYMB_CNT(i, v) ((void)0)
+#endif
 template <class T>
 struct Walker {
     // input: A Pc' with rows relabelled by perm_c (NCP)
@@ -374,6 +380,7 @@ struct Walker {
             if (repfnz[rep] == (T)NONE || supno[rep] == js) continue;
             if (xprune[rep] < xlsub[rep + 1]) continue; // pruned before
             I lo = xlsub[rep], hi = xlsub[rep + 1] - 1;
+            SYMB_CNT(1, hi - lo + 1);
             bool hit = false;
             for (I q = lo; q <= hi; ++q)
                 if (lsub[q] == tj) {
@@ -477,6 +484,7 @@ struct Walker {
     // and rows marked `mark`; returns the count written
     I l_write(I at, T below, T mark) {
         I o = at;
+        SYMB_CNT(2, last_len);
         for (T c = lhead; c != (T)NONE; c = lnx[c])
             if (c >= below && marker[c] != mark) lsub[o++] = c;
         return o - at;
@@ -530,6 +538,7 @@ struct Walker {
                 x = xe = 0;
             }
             for (;;) {
+                SYMB_CNT(0, xe - x);
                 while (x < xe) {
                     const T c = L[x++], cm = mk[c];
                     if (cm == tj) continue;
@@ -579,6 +588,7 @@ struct Walker {
             if (js) {
                 // L(:, j) = P ++ (L(:, j-1) minus j-1 minus P): P to the front
                 if (split >= 0) {
+                    SYMB_CNT(4, nexp);
                     for (I i = start + nexp - 1; i >= start; --i) {
                         l_unlink(L[i]);
                         l_push_front(L[i]);
@@ -587,6 +597,7 @@ struct Walker {
                         l_unlink(vrep);
                     } else {
                         for (T c = lhead; c != (T)NONE;) {
+                            SYMB_CNT(3, 1);
                             const T nx = lnx[c];
                             if (c < tj) l_unlink(c);
                             c = nx;
@@ -811,6 +822,10 @@ static Result symbfact_t(I m, I n, const I *cb, const I *ce, const I *ri64, cons
         fprintf(stderr, "symbfact: search %.3f s, total %.3f s\n",
                 std::chrono::duration<double>(t1 - t0).count(),
                 std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
+#ifdef SLU_SYMB_COUNT
+    fprintf(stderr, "symbfact counts: dfs %lld prune-scan %lld list-write %lld unlink-scan %lld p-front %lld\n",
+            g_cnt[0], g_cnt[1], g_cnt[2], g_cnt[3], g_cnt[4]);
+#endif
     return R;
 }
 

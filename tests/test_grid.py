@@ -117,6 +117,12 @@ def test_rccl_call_sequence_is_the_tested_one_cpu(case, pr, pc, tmp_path, monkey
         assert sends[key] == recvs[key], key
     nlev = {lv for r in range(P) for _, lv, _ in host[r] if lv >= 0}
     assert len(nlev) > 3                     # the per-level exchanges are in it
+    # the chunked panel exchange (SLU_PANEL_CHUNKS, default 4): on the
+    # stencil some level's panels go out in more than one group
+    from collections import Counter
+    per = Counter((r, lv) for r in range(P) for ph, lv, _ in host[r] if ph.startswith("L/U panel"))
+    if case == "stencil":
+        assert max(per.values()) > 1, per
 
 
 @pytest.mark.gpu
