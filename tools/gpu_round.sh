@@ -1,17 +1,17 @@
 #!/bin/bash
-# Round 4 end-of-round GPU session: the whole GPU suite, the bench line,
+# End-of-round GPU session: the whole GPU suite, the bench line,
 # rocprofv3 kernel statistics, the HBM-traffic and MFMA-busy PMC passes of the
 # dominant kernel, and their summaries into profiles/ (TAG prefix).  Every GPU
 # step has its own time limit and the steps are chained with &&.
-# usage: bash tools/gpu_round_r04.sh TAG [bench args...]
+# usage: [SKIP_TESTS=1] bash tools/gpu_round.sh TAG [bench args...]
 set -o pipefail
-TAG=${1:-r04z}; shift
+TAG=${1:-r06z}; shift
 OUT=gpurun_out/$TAG
 rm -rf $OUT; mkdir -p $OUT
 export TMPDIR=/tmp
-echo "== pytest -m gpu" && \
-timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
-    > $OUT/pytest_gpu.log 2>&1 && tail -3 $OUT/pytest_gpu.log && \
+{ [ "$SKIP_TESTS" = 1 ] || { echo "== pytest -m gpu" && \
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+    > $OUT/pytest_gpu.log 2>&1 && tail -3 $OUT/pytest_gpu.log; }; } && \
 echo "== bench" && \
 timeout -k 10 600 python -u bench.py "$@" > $OUT/bench.json 2> $OUT/bench.err && cat $OUT/bench.json && \
 echo "== rocprofv3 kernel stats" && \

@@ -65,10 +65,10 @@ template <typename T> int run(int w, int nb, int reps) {
     CK(hipMalloc(&cnt, 16));
     CK(hipMalloc(&zp, nb * 4));
     CK(hipMalloc(&err, 4));
-    CK(hipMalloc(&flags, nb * DS_MAXS * 4));
+    CK(hipMalloc(&flags, nb * DS_NFLAGS * 4));
     CK(hipMemset(zp, 0, nb * 4));
     CK(hipMemset(err, 0, 4));
-    CK(hipMemset(flags, 0, nb * DS_MAXS * 4));
+    CK(hipMemset(flags, 0, nb * DS_NFLAGS * 4));
     unsigned epoch = 0;
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
