@@ -133,11 +133,12 @@ def model(rows, vol, pr, pc, bw, lat, chunks=1, trsm_scale=1.0):
         # start when it is in, so the chain to the level's first tiles holds
         # one chunk's TRSM and transfer, and the rest of both run beside the
         # level's own update
-        comm = (2 + chunks - 1) * ncoll * lat * 1e-3 + xfer / chunks
+        # (the latency of the later chunks' groups runs beside the update too)
+        comm = 2 * ncoll * lat * 1e-3 + xfer / chunks
         chain.append(r["diag"] + trsm / chunks + comm)
         tiles = r["big"] + r["small"]
         s1 = r["schur"] * waves(tiles / P) / waves(tiles)
-        tail = max(xfer, trsm) * (chunks - 1) / chunks
+        tail = max(xfer + ncoll * lat * 1e-3 * chunks, trsm) * (chunks - 1) / chunks
         schur.append(max(s1, tail + s1 / chunks) if chunks > 1 else s1)
     if P == 1:
         return sum(r["wall"] for r in rows), chain, schur
