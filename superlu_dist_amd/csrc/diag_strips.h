@@ -118,6 +118,21 @@ __device__ __forceinline__ bool ds_wait(const unsigned *f, unsigned epoch, int *
     return *s_ok != 0;
 }
 
+// one wave waits for *f >= epoch (every lane loads the same word: a
+// uniform loop); false (and *err set) on timeout
+__device__ __forceinline__ bool ds_wait_wave(const unsigned *f, unsigned epoch, int *err) {
+    unsigned n = 0;
+    while (__hip_atomic_load((const __attribute__((address_space(1))) unsigned *)f, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT) < epoch) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++n > (1u << 23)) { // ~1 s
+            if ((threadIdx.x & 63) == 0) atomicExch(err, 1);
+            return false;
+        }
+    }
+    return true;
+}
+
 // publish: every wave's stores have completed, then one lane sets the flag
 __device__ __forceinline__ void ds_publish(unsigned *f, unsigned epoch) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -126,6 +141,13 @@ __device__ __forceinline__ void ds_publish(unsigned *f, unsigned epoch) {
         __hip_atomic_store((__attribute__((address_space(1))) unsigned *)f, epoch, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
 }
+
+// Two flags per strip (the item's flags are 2 DS_MAXS words: A then B).
+// A: the first 64 rows of L21_q and (L_qq^{-1})^T are published -- what the
+// next strip's own LU needs; B: all of L21_q.  The strip right of q waits
+// for A before its LU and its waves 1-3 for B beside the LU; the strips
+// further right wait for B.
+constexpr int DS_NFLAGS = 2 * DS_MAXS;
 
 // Block -> (item, strip) of the XCD-grouped layout above; grid = 64 *
 // ceil(nitems / 8).
@@ -147,7 +169,7 @@ k_diag_strips(const DiagItemF<T> *items, int nitems, unsigned *flags, unsigned e
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int ld = it.ld, c0 = q * PW, pw = min(PW, w - c0);
     T *A = it.a;
-    unsigned *fl = flags + (size_t)item * DS_MAXS;
+    unsigned *fl = flags + (size_t)item * DS_NFLAGS, *flB = fl + DS_MAXS;
     const int nb = ns;
     T *dinvU = it.dinv, *dinvLT = it.dinv + (int64_t)nb * PW * PW;
 
@@ -212,6 +234,10 @@ k_diag_strips(const DiagItemF<T> *items, int nitems, unsigned *flags, unsigned e
     // the published strip r0 (wave-private rows: no barrier)
     auto trail_rest = [&](int r0, int lo, int hi, int w0, int wn) {
         const int nfr = hi > lo ? (hi - lo + 15) / 16 : 0;
+        // (rows past the first 64 of L21: published with the strip's flag B;
+        // on a timeout the error is set and the rows are garbage -- the
+        // engine then fails the factorization)
+        if (wv - w0 < nfr) (void)ds_wait_wave(flB + r0 / PW, epoch, err);
         for (int fr = wv - w0; fr < nfr; fr += wn) {
             T v[8];
 #pragma unroll
@@ -230,7 +256,7 @@ k_diag_strips(const DiagItemF<T> *items, int nitems, unsigned *flags, unsigned e
     };
     // ---- apply the panels of the strips to my left, in order
     for (int p = 0; p < q; ++p) {
-        if (!ds_wait(fl + p, epoch, err, &s_ok)) return;
+        if (!ds_wait((p + 1 == q ? fl : flB) + p, epoch, err, &s_ok)) return;
         const int r0 = p * PW, nr = w - r0;
         DS_PROBE(0);
         // only L21_p (rows r0 + 32 ..): L_pp enters through its inverse.  The
@@ -421,76 +447,99 @@ k_diag_strips(const DiagItemF<T> *items, int nitems, unsigned *flags, unsigned e
         }
     }
     __syncthreads();
-    if (!anyz) {
-        // (III) rows 64 .. nrow - 1: 16 x 16 fragments, all reads before the
-        // barrier, the writes after it
-        const int nb = nrow - 64, nfr = nb > 0 ? (nb + 15) / 16 : 0, nf = 2 * nfr;
-        constexpr int FMAX = (MW - 64) / 16 * 2 / 4; // fragments per wave
-        typename M::acc_t acc[FMAX];
-#pragma unroll
-        for (int u = 0; u < FMAX; ++u) {
-            acc[u] = M::zero();
-            const int f = wv + 4 * u;
-            if (f < nf) {
-                const int fr = f >> 1, fc = f & 1, r = fr * 16 + (lane & 15);
-#pragma unroll
-                for (int ks = 0; ks < PW; ks += M::KSTEP) {
-                    const int k = ks + (lane >> 4);
-                    M::step(acc[u], keep_if(r < nb, sS[c0 + 64 + min(r, nb - 1)][k]), sUi[k][fc * 16 + (lane & 15)]);
-                }
-            }
-        }
-        __syncthreads();
-#pragma unroll
-        for (int u = 0; u < FMAX; ++u) {
-            const int f = wv + 4 * u;
-            if (f < nf) {
-                const int fr = f >> 1, fc = f & 1;
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int r = fr * 16 + M::row(lane, i);
-                    if (r < nb) sS[c0 + 64 + r][fc * 16 + (lane & 15)] = M::get(acc[u], i);
-                }
-            }
-        }
-    } else if (wv > 0) { // rows 64.., thread per row
-        const int i = tid;
-        if (i < nrow) {
-            T x[PW];
-#pragma unroll
-            for (int c = 0; c < PW; ++c) x[c] = sS[c0 + i][c];
-#pragma unroll
-            for (int j = 0; j < PW; ++j) {
-                if (j < pw) {
-                    const T l = s_zp[j] ? x[j] : Sx::mul(x[j], s_rp[j]);
-                    x[j] = l;
-#pragma unroll
-                    for (int c = j + 1; c < PW; ++c) x[c] = Sx::fms(x[c], l, sS[c0 + j][c]);
-                }
-            }
-#pragma unroll
-            for (int c = 0; c < PW; ++c) sS[c0 + i][c] = x[c];
-        }
-    }
-    __syncthreads();
-
-    DS_PROBE(4);
-    // ---- publish what the strips to the right read: L21_q (rows c0 + 32 ..)
-    // and (L_qq^{-1})^T (row-major), then the flag; then the rest of the
-    // strip (rows < c0 + 32) and U_qq^{-1} (row-major), which only the
-    // TRSMs after this kernel read
-    {
-        const int r1 = c0 + PW, n21 = w - r1;
-        for (int e = tid; e < n21 * pw; e += DS_THREADS) {
-            const int r = r1 + e % n21, c = e / n21;
+    // ---- (III) rows 64 .. nrow - 1 and the publication of L21_q: first
+    // rows 64-95 (the first fragment of every wave) and L21_q's first 64 rows
+    // with (L_qq^{-1})^T under flag A, then the rest under flag B.  (16 x 16
+    // fragments, all reads of a part before a barrier, its writes after it:
+    // a row block's two column halves are on two waves.)
+    const int r1 = c0 + PW, n21 = w - r1;
+    auto store21 = [&](int a, int b) { // L21_q rows [a, b) (rows of L21, from r1)
+        const int nn = b - a;
+        for (int e = tid; e < nn * pw; e += DS_THREADS) {
+            const int r = r1 + a + e % nn, c = e / nn;
             st_sc1(A + r + (int64_t)(c0 + c) * ld, sS[r][c]);
         }
+    };
+    const int nA = min(64, max(n21, 0)); // L21 rows under flag A
+    if (!anyz) {
+        const int nb = nrow - 64, nfr = nb > 0 ? (nb + 15) / 16 : 0, nf = 2 * nfr;
+        constexpr int FMAX = (MW - 64) / 16 * 2 / 4; // fragments per wave
+        auto part = [&](int u0, int u1) {
+            typename M::acc_t acc[FMAX];
+#pragma unroll
+            for (int u = 0; u < FMAX; ++u) {
+                acc[u] = M::zero();
+                const int f = wv + 4 * u;
+                if (u >= u0 && u < u1 && f < nf) {
+                    const int fr = f >> 1, fc = f & 1, r = fr * 16 + (lane & 15);
+#pragma unroll
+                    for (int ks = 0; ks < PW; ks += M::KSTEP) {
+                        const int k = ks + (lane >> 4);
+                        M::step(acc[u], keep_if(r < nb, sS[c0 + 64 + min(r, nb - 1)][k]),
+                                sUi[k][fc * 16 + (lane & 15)]);
+                    }
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int u = 0; u < FMAX; ++u) {
+                const int f = wv + 4 * u;
+                if (u >= u0 && u < u1 && f < nf) {
+                    const int fr = f >> 1, fc = f & 1;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int r = fr * 16 + M::row(lane, i);
+                        if (r < nb) sS[c0 + 64 + r][fc * 16 + (lane & 15)] = M::get(acc[u], i);
+                    }
+                }
+            }
+            __syncthreads();
+        };
+        part(0, 1); // rows 64 .. 95
+        DS_PROBE(4);
+        store21(0, nA);
         for (int e = tid; e < PW * PW; e += DS_THREADS) {
             const int i = e / PW, jj = e % PW;
             st_sc1(dinvLT + (int64_t)q * PW * PW + e, sLi[jj][i]);
         }
         ds_publish(fl + q, epoch);
-        DS_PROBE(5);
+        part(1, FMAX); // rows 96 ..
+        store21(nA, n21);
+        ds_publish(flB + q, epoch);
+    } else {
+        if (wv > 0) { // rows 64.., thread per row
+            const int i = tid;
+            if (i < nrow) {
+                T x[PW];
+#pragma unroll
+                for (int c = 0; c < PW; ++c) x[c] = sS[c0 + i][c];
+#pragma unroll
+                for (int j = 0; j < PW; ++j) {
+                    if (j < pw) {
+                        const T l = s_zp[j] ? x[j] : Sx::mul(x[j], s_rp[j]);
+                        x[j] = l;
+#pragma unroll
+                        for (int c = j + 1; c < PW; ++c) x[c] = Sx::fms(x[c], l, sS[c0 + j][c]);
+                    }
+                }
+#pragma unroll
+                for (int c = 0; c < PW; ++c) sS[c0 + i][c] = x[c];
+            }
+        }
+        __syncthreads();
+        DS_PROBE(4);
+        store21(0, max(n21, 0));
+        for (int e = tid; e < PW * PW; e += DS_THREADS) {
+            const int i = e / PW, jj = e % PW;
+            st_sc1(dinvLT + (int64_t)q * PW * PW + e, sLi[jj][i]);
+        }
+        ds_publish(fl + q, epoch);
+        ds_publish(flB + q, epoch);
+    }
+    DS_PROBE(5);
+    // ---- then the rest of the strip (rows < c0 + 32) and U_qq^{-1}
+    // (row-major), which only the TRSMs after this kernel read
+    {
         const int r1c = min(r1, w);
         for (int e = tid; e < r1c * pw; e += DS_THREADS) {
             const int r = e % r1c, c = e / r1c;

@@ -725,7 +725,7 @@ struct Plan : PlanBase {
     DevBuf<DRec> d_prec;
     DevBuf<i64> d_cvoff;
     DevBuf<int> d_counters; // [0] tiny pivots, [1] k_diag_strips hand-off timeout
-    DevBuf<unsigned> d_dsflags; // k_diag_strips: per fast diag item, DS_MAXS strip flags
+    DevBuf<unsigned> d_dsflags; // k_diag_strips: per fast diag item, DS_NFLAGS strip flags (A, B)
     unsigned ds_epoch = 0;      // ... set to the factorization's epoch when a strip is published
     DevBuf<int> d_zpiv;     // per supernode: max zero-pivot column + 1
     DevBuf<i64> d_info;     // 2D grids: all-gather of the per-rank info
@@ -2625,7 +2625,7 @@ struct Plan : PlanBase {
         sub("blocks", (d_lblk.bytes() + d_lmap.bytes() + d_ublk.bytes() + d_ucol_voff.bytes() + d_ucol_fst.bytes()) / 1e6);
         d_counters.alloc(4);
         d_zpiv.alloc(nsupers);
-        d_dsflags.alloc(std::max<size_t>(df_items.size(), 1) * DS_MAXS);
+        d_dsflags.alloc(std::max<size_t>(df_items.size(), 1) * DS_NFLAGS);
         HIPCHK(hipMemset(d_dsflags.p, 0, d_dsflags.bytes()));
         ev_pan.resize(levels.size());
         ev_rest.resize(levels.size());
@@ -3061,7 +3061,7 @@ struct Plan : PlanBase {
     void launch_strips(const LevelRange &R, double thresh, hipStream_t st) {
         if constexpr (!cplx)
             hipLaunchKernelGGL(k_diag_strips<T>, dim3(ds_grid(R.df_n)), dim3(DS_THREADS), 0, st, d_df.p + R.df_off,
-                               R.df_n, d_dsflags.p + (size_t)R.df_off * DS_MAXS, ds_epoch, d_counters.p + 1, thresh,
+                               R.df_n, d_dsflags.p + (size_t)R.df_off * DS_NFLAGS, ds_epoch, d_counters.p + 1, thresh,
                                opts.replace_tiny_pivot, d_counters.p, d_zpiv.p);
     }
     void launch_big(const LevelRange &R, int off, int cnt, hipStream_t st) {
