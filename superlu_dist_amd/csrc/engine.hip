@@ -2992,6 +2992,9 @@ struct Plan : PlanBase {
     // own beside the L panel's (both only wait for the diagonal block; near
     // the root each is a few slabs, latency-bound)
     int trsm_2stream = getenv("SLU_TRSM_2STREAM") ? atoi(getenv("SLU_TRSM_2STREAM")) : 1;
+    // SLU_TRSM_PF=1 (default): k_trsm_reg's latency form (next block's T and
+    // Dinv loaded during the current block, columns stored when final)
+    int trsm_pf = getenv("SLU_TRSM_PF") ? atoi(getenv("SLU_TRSM_PF")) : 1;
     // the level's fast-path TRSM items, or (ch >= 0) those of exchange chunk ch
     void launch_trsm_fast(const LevelRange &R, hipStream_t st, int ch = -1) {
         const int lo = R.lf_off + (ch >= 0 ? R.lf_o[ch] : 0), ln = ch >= 0 ? R.lf_o[ch + 1] - R.lf_o[ch] : R.lf_n;
@@ -3003,19 +3006,26 @@ struct Plan : PlanBase {
             HIPCHK(hipEventRecord(ev_tu0, st));
             HIPCHK(hipStreamWaitEvent(ustream, ev_tu0, 0));
         }
+        auto go = [&](auto maxw, auto pf) {
+            constexpr int MW = decltype(maxw)::value;
+            constexpr bool P = decltype(pf)::value;
+            if (ln) hipLaunchKernelGGL((k_trsm_reg<T, 0, MW, P>), dim3(ln), dim3(64 * TR_WAVES), 0, st, d_lf.p + lo);
+            if (un) hipLaunchKernelGGL((k_trsm_reg<T, 1, MW, P>), dim3(un), dim3(64 * TR_WAVES), 0, su, d_uf.p + uo);
+        };
+        auto go_pf = [&](auto maxw) {
+            if (trsm_pf) go(maxw, std::true_type{});
+            else go(maxw, std::false_type{});
+        };
         if constexpr (cplx) {
             if (ln) hipLaunchKernelGGL((k_trsm_blk<T, 0>), dim3(ln), dim3(256), 0, st, d_lf.p + lo);
             if (un) hipLaunchKernelGGL((k_trsm_blk<T, 1>), dim3(un), dim3(256), 0, su, d_uf.p + uo);
         } else if (R.tf_maxw <= 64 && trsm_narrow) {
             // narrow levels: the 64-wide instantiation (several workgroups per CU)
-            if (ln) hipLaunchKernelGGL((k_trsm_reg<T, 0, 64>), dim3(ln), dim3(64 * TR_WAVES), 0, st, d_lf.p + lo);
-            if (un) hipLaunchKernelGGL((k_trsm_reg<T, 1, 64>), dim3(un), dim3(64 * TR_WAVES), 0, su, d_uf.p + uo);
+            go_pf(std::integral_constant<int, 64>{});
         } else if (R.tf_maxw <= 128 && trsm_narrow >= 2) {
-            if (ln) hipLaunchKernelGGL((k_trsm_reg<T, 0, 128>), dim3(ln), dim3(64 * TR_WAVES), 0, st, d_lf.p + lo);
-            if (un) hipLaunchKernelGGL((k_trsm_reg<T, 1, 128>), dim3(un), dim3(64 * TR_WAVES), 0, su, d_uf.p + uo);
+            go_pf(std::integral_constant<int, 128>{});
         } else {
-            if (ln) hipLaunchKernelGGL((k_trsm_reg<T, 0>), dim3(ln), dim3(64 * TR_WAVES), 0, st, d_lf.p + lo);
-            if (un) hipLaunchKernelGGL((k_trsm_reg<T, 1>), dim3(un), dim3(64 * TR_WAVES), 0, su, d_uf.p + uo);
+            go_pf(std::integral_constant<int, FAST_MAXW>{});
         }
         if (two) {
             HIPCHK(hipEventRecord(ev_tu1, ustream));

@@ -1629,21 +1629,60 @@ k_schur_big(const TileItem *tiles, const KInfo<T> *kinfo, T *Lval, T *Uval,
 // LDS), Z = X_b - acc, X_b = Z Dinv_b; results return to A layout through a
 // per-wave LDS tile.  Same MODE convention as k_trsm_blk.
 constexpr int TR_WAVES = 4;
-// T staged 8 elements per thread in flight (16: slower, profiles/r05tu/).  A
-// next-block register prefetch of Dinv / T was measured and dropped: faster
-// serialized near the root, but beside the Schur tiles the extra registers
-// cost more than it saved (100^3 289 -> 297 ms, profiles/r05tpf/).
+// T staged 8 elements per thread in flight (16: slower, profiles/r05tu/) --
+// the non-PF form.  Round 6's phase probes (profiles/r06j/trsm_micro.txt) put
+// 40% of a lone 256-wide slab's 59 us in that staging (one global round trip
+// per 8 elements, 1 wave per SIMD, nothing to hide it) and 13% in the final
+// store; the PF form below (next block's T / Dinv in registers, loads that
+// land untouched until used, stores per block) takes it to 39 us, and
+// serialized 100^3 TRSM from 29.0 to 23.1 ms with the pipelined factor
+// unchanged (profiles/r06j/).  (Round 5's register prefetch masked the
+// loaded values, which made the compiler wait for each load at once.)
 constexpr int TR_TU = 8;
+// B operands read from LDS this many k-steps ahead of their MFMAs (k_trsm_reg)
+#ifndef TR_PFD
+#define TR_PFD 4
+#endif
+// LDS written by a wave, then read by other lanes of the same wave
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_s_waitcnt(0xc07f); // lgkmcnt(0)
+    __builtin_amdgcn_wave_barrier();
+}
+#ifdef SLU_TR_PROBE
+// Diagnostics build only (tools/micro/trsm_micro.hip): k_trsm_reg cycles per
+// phase summed over workgroups (thread 0's view): 0 X load, 1 Dinv/T staging,
+// 2 X_{<b} T_{<b,b} MFMAs, 3 Z Dinv_b with its layout changes, 4 X store.
+__device__ long long slu_tr_tp[8];
+#define TR_PROBE_START() long long tr_t0 = clock64()
+#define TR_PROBE(i)                                                                          \
+    do {                                                                                     \
+        if (threadIdx.x == 0) {                                                              \
+            const long long t = clock64();                                                   \
+            atomicAdd((unsigned long long *)&slu_tr_tp[i], (unsigned long long)(t - tr_t0)); \
+            tr_t0 = t;                                                                       \
+        }                                                                                    \
+    } while (0)
+#else
+#define TR_PROBE_START()
+#define TR_PROBE(i)
+#endif
 // MAXW: the widest supernode of the launch's items.  The narrow levels
 // (MAXW 64: 16 row registers, 17 KB of LDS) run several workgroups per CU
 // where the 256-wide form (64 registers, 68 KB) runs one.
-template <typename T, int MODE, int MAXW = FAST_MAXW>
+// PF (the latency form, for launches of few slabs, where each workgroup's
+// chain of global round trips is the launch time): Dinv_{b+1} and
+// T_{<b+1,b+1} are loaded into registers while block b computes, and the
+// columns of block b are stored as soon as they are final.
+template <typename T, int MODE, int MAXW = FAST_MAXW, bool PF = false>
 __global__ void __launch_bounds__(64 * TR_WAVES, MAXW <= 64 ? 4 : MAXW <= 128 ? 2 : 1)
+__attribute__((amdgpu_waves_per_eu(MAXW <= 64 ? 4 : MAXW <= 128 ? 2 : 1, MAXW <= 64 ? 4 : MAXW <= 128 ? 2 : 1)))
 k_trsm_reg(const TrsmItemF<T> *items) {
     constexpr int PW = 32, NKS = MAXW / 4, NBMAX = MAXW / PW;
     constexpr int TROWS = MAXW - PW > TR_WAVES * 16 ? MAXW - PW : TR_WAVES * 16; // sT rows
     using Sx = S<T>;
     using M = Mma<T>;
+    TR_PROBE_START();
     const TrsmItemF<T> it = items[blockIdx.x];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int w = it.w, nb = (w + PW - 1) / PW;
@@ -1664,6 +1703,38 @@ k_trsm_reg(const TrsmItemF<T> *items) {
         t0 = it.t0[myr];
         rbase = it.voff[myr] - t0;
     }
+    constexpr int NT = 64 * TR_WAVES, DPT = PW * PW / NT; // Dinv elements per thread
+    static_assert(PW * PW % NT == 0, "TR_WAVES");
+    T pd[DPT], pt[PF ? DPT * (NBMAX - 1) : 1]; // PF: the next block's Dinv / T
+    // T_{<b,b} element e (b * PW * PW of them, DPT * b per thread); the
+    // columns past w are masked when stored, not when loaded, so that the
+    // loads can land in registers untouched until then
+    auto t_src = [&](int b, int e) {
+        const int kr = b * PW;
+        const int i = MODE == 0 ? e % kr : e / PW, j = MODE == 0 ? e / kr : e % PW;
+        const int col = min(b * PW + j, w - 1);
+        return gld(MODE == 0 ? it.t + i + (int64_t)col * it.ldt : it.t + col + (int64_t)i * it.ldt);
+    };
+    auto t_put = [&](int b, int e, T v) {
+        const int kr = b * PW;
+        const int j = MODE == 0 ? e / kr : e % PW;
+        v = keep_if(b * PW + j < w, v);
+        if (MODE == 0) sT[e % kr][e / kr] = v;
+        else sT[e / PW][e % PW] = v;
+    };
+    // (PF: Dinv_0, Dinv_1 and T_{<1,1} requested ahead of X, so that their
+    // round trip overlaps X's)
+    T pd0[DPT];
+    if (PF) {
+#pragma unroll
+        for (int u = 0; u < DPT; ++u) pd0[u] = gld(it.dinv + tid + u * NT);
+        if (nb > 1) {
+#pragma unroll
+            for (int u = 0; u < DPT; ++u) pd[u] = gld(it.dinv + PW * PW + tid + u * NT);
+#pragma unroll
+            for (int u = 0; u < DPT; ++u) pt[u] = t_src(1, tid + u * NT);
+        }
+    }
     T xa[NKS];
 #pragma unroll
     for (int s = 0; s < NKS; ++s) {
@@ -1675,16 +1746,27 @@ k_trsm_reg(const TrsmItemF<T> *items) {
         }
         xa[s] = v;
     }
+#ifdef SLU_TR_PROBE
+    if (tid == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+    TR_PROBE(0);
 #pragma unroll
     for (int b = 0; b < NBMAX; ++b) {
         if (b >= nb) break;
         __syncthreads();
-        stage_loop<64 * TR_WAVES, 4, T>(
-            tid, PW * PW,
-            [&](int e, bool ok) { return keep_if(ok, gld(it.dinv + (int64_t)b * PW * PW + min(e, PW * PW - 1))); },
-            [&](int e, T v) { sD[e / PW][e % PW] = v; });
         const int kr = b * PW;
-        if (kr > 0)
+        if (PF) {
+#pragma unroll
+            for (int u = 0; u < DPT; ++u) sD[(tid + u * NT) / PW][(tid + u * NT) % PW] = b == 0 ? pd0[u] : pd[u];
+#pragma unroll
+            for (int u = 0; u < DPT * b; ++u) t_put(b, tid + u * NT, pt[u]);
+        } else {
+            stage_loop<64 * TR_WAVES, 4, T>(
+                tid, PW * PW,
+                [&](int e, bool ok) { return keep_if(ok, gld(it.dinv + (int64_t)b * PW * PW + min(e, PW * PW - 1))); },
+                [&](int e, T v) { sD[e / PW][e % PW] = v; });
+        }
+        if (!PF && kr > 0)
             stage_loop<64 * TR_WAVES, TR_TU, T>(
                 tid, kr * PW,
                 [&](int e, bool ok) {
@@ -1699,48 +1781,100 @@ k_trsm_reg(const TrsmItemF<T> *items) {
                     else sT[e / PW][e % PW] = v;
                 });
         __syncthreads();
-        typename M::acc_t a0 = M::zero(), a1 = M::zero();
+        if (PF && b > 0 && b + 1 < nb) {
 #pragma unroll
-        for (int s = 0; s < 8 * b; ++s) {
-            T b0 = sT[4 * s + kq][rl], b1 = sT[4 * s + kq][16 + rl];
-            M::step(a0, xa[s], b0);
-            M::step(a1, xa[s], b1);
+            for (int u = 0; u < DPT; ++u) pd[u] = gld(it.dinv + (int64_t)(b + 1) * PW * PW + tid + u * NT);
+#pragma unroll
+            for (int u = 0; u < DPT * (b + 1); ++u) pt[u] = t_src(b + 1, tid + u * NT);
+        }
+        TR_PROBE(1);
+        typename M::acc_t a0 = M::zero(), a1 = M::zero();
+        {
+            // the B operands read from LDS TR_PFD k-steps ahead of their
+            // MFMAs: one wave per SIMD has no other wave to hide an LDS read
+            // behind, and with the read right before its MFMA every pair of
+            // MFMAs waited for one (lgkmcnt(0)) -- the compiler, short of
+            // registers, did not pipeline them itself
+            T q0[TR_PFD], q1[TR_PFD];
+            const int ns = 8 * b;
+#pragma unroll
+            for (int s = 0; s < TR_PFD; ++s)
+                if (s < ns) {
+                    q0[s] = sT[4 * s + kq][rl];
+                    q1[s] = sT[4 * s + kq][16 + rl];
+                }
+#pragma unroll
+            for (int s = 0; s < 8 * b; ++s) {
+                const T b0 = q0[s % TR_PFD], b1 = q1[s % TR_PFD];
+                if (s + TR_PFD < ns) {
+                    q0[s % TR_PFD] = sT[4 * (s + TR_PFD) + kq][rl];
+                    q1[s % TR_PFD] = sT[4 * (s + TR_PFD) + kq][16 + rl];
+                }
+                // (the scheduler would sink the reads back to their uses)
+                __builtin_amdgcn_sched_barrier(0);
+                M::step(a0, xa[s], b0);
+                M::step(a1, xa[s], b1);
+                __builtin_amdgcn_sched_barrier(0);
+            }
         }
         __syncthreads(); // every wave is done with sT before W (= its first rows) is written
+        TR_PROBE(2);
         // Z = X_b - acc: acc (C layout) -> LDS, read back in A layout
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             W[M::row(lane, i)][rl] = M::get(a0, i);
             W[M::row(lane, i)][16 + rl] = M::get(a1, i);
         }
-        __syncthreads();
-        T za[8];
+        // W is the wave's own: its layout changes need the wave's LDS writes
+        // done, not the workgroup (the first __syncthreads above covers sT)
+        wave_lds_sync();
+        T za[8], d0[8], d1[8];
+#pragma unroll
+        for (int s = 0; s < 8; ++s) { // (Dinv_b's B operands read with Z: one wait for both)
+            d0[s] = sD[4 * s + kq][rl];
+            d1[s] = sD[4 * s + kq][16 + rl];
+        }
 #pragma unroll
         for (int s = 0; s < 8; ++s) za[s] = Sx::fms(xa[8 * b + s], W[rl][4 * s + kq], one_of(xa[0]));
         typename M::acc_t c0 = M::zero(), c1 = M::zero();
 #pragma unroll
         for (int s = 0; s < 8; ++s) {
-            M::step(c0, za[s], sD[4 * s + kq][rl]);
-            M::step(c1, za[s], sD[4 * s + kq][16 + rl]);
+            M::step(c0, za[s], d0[s]);
+            M::step(c1, za[s], d1[s]);
         }
-        __syncthreads();
+        wave_lds_sync();
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             W[M::row(lane, i)][rl] = M::get(c0, i);
             W[M::row(lane, i)][16 + rl] = M::get(c1, i);
         }
-        __syncthreads();
+        wave_lds_sync();
 #pragma unroll
         for (int s = 0; s < 8; ++s) xa[8 * b + s] = W[rl][4 * s + kq];
+        if (PF) {
+#pragma unroll
+            for (int s = 8 * b; s < 8 * b + 8; ++s) {
+                const int k = 4 * s + kq;
+                if (rv && k < w) {
+                    if (MODE == 0) it.x[myr + (int64_t)k * it.ldx] = xa[s];
+                    else if (k >= t0) it.x[rbase + k] = xa[s];
+                }
+            }
+        }
+        TR_PROBE(3);
     }
 #pragma unroll
-    for (int s = 0; s < NKS; ++s) {
+    for (int s = 0; s < (PF ? 0 : NKS); ++s) {
         const int k = 4 * s + kq;
         if (rv && k < w) {
             if (MODE == 0) it.x[myr + (int64_t)k * it.ldx] = xa[s];
             else if (k >= t0) it.x[rbase + k] = xa[s];
         }
     }
+#ifdef SLU_TR_PROBE
+    if (tid == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+    TR_PROBE(4);
 }
 
 } // namespace slu
