@@ -29,6 +29,7 @@
 #include <map>
 #include <future>
 #include <mutex>
+#include <set>
 #include <thread>
 #include <vector>
 
@@ -361,6 +362,10 @@ struct DevA {
 DevA g_deva;
 std::mutex g_deva_mu;
 uint64_t g_deva_gen = 0;
+// LocalLU_t of the LUstructs whose pddistribute left A's values out of the
+// host arrays (SUPERLU_MI355X_DEFER_A, default on for fp64 unless
+// SUPERLU_MI355X_HOST_FACTORS=1): their pdgstrf needs g_deva to hold their A
+std::set<const void *> g_host_a_deferred;
 
 inline uint64_t mix(uint64_t h, uint64_t v) {
     h ^= v + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2);
@@ -562,6 +567,13 @@ int_t pxgstrf(int dtype, const char *name, superlu_dist_options_t *options, int 
             if (g_deva.lu == LUstruct && g_deva.llu == LUstruct->Llu &&
                 g_deva.lrow == LUstruct->Llu->Lrowind_bc_ptr && g_deva.dtype == dtype && g_deva.n == n)
                 da = &g_deva;
+        }
+        if (!da) {
+            std::lock_guard<std::mutex> lk(g_deva_mu);
+            if (g_host_a_deferred.count(LUstruct->Llu))
+                throw slu::Error("this LUstruct was distributed with A's values kept for the device fill "
+                                 "(not placed in the host arrays), and another pddistribute has replaced "
+                                 "that A since: call pddistribute again, or set SUPERLU_MI355X_DEFER_A=0");
         }
         const char *hf = getenv("SUPERLU_MI355X_HOST_FACTORS");
         const bool keep_on_device = one && da && cache && !(hf && atoi(hf) == 1);
@@ -984,6 +996,11 @@ void pxgstrs(int dtype, const char *name, int_t n, LUS *LU, xScalePermstruct_t *
     }
 }
 
+extern "C" void *slu_distribute_glu_deferred(int64_t n, const int_t *xsup, const int_t *supno,
+                                             const int_t *xlsub, const int_t *lsub, const int_t *xusub,
+                                             const int_t *usub, const int64_t *xa, const int64_t *asub,
+                                             const double *a, int nprow, int npcol, int myrow, int mycol);
+
 // ------------------------------------------------------------------ distribute
 // pddistribute (SRC/pddistribute.c:327-2398) for callers that also take
 // pdgstrs from this library (libslu_mi355x_solve.so).  The LU storage is the
@@ -1008,6 +1025,15 @@ float pxdistribute(int dtype, const char *name, superlu_dist_options_t *options,
         const int_t *pr = sp->perm_r, *pc = sp->perm_c;
         const int Pr = (int)grid->nprow, Pc = (int)grid->npcol, P = Pr * Pc;
         const int myrow = grid->iam / Pc, mycol = grid->iam % Pc;
+        // SLU_DIST_TIME=1: phase times on stderr (diagnostics)
+        const bool dtime = getenv("SLU_DIST_TIME") != nullptr;
+        auto dt0 = std::chrono::steady_clock::now();
+        auto dtick = [&](const char *what) {
+            if (!dtime) return;
+            const auto t = std::chrono::steady_clock::now();
+            fprintf(stderr, "[pxdistribute] %-26s %8.1f ms\n", what, std::chrono::duration<double, std::milli>(t - dt0).count());
+            dt0 = t;
+        };
         // ---- A in the LUstruct's coordinates, as CSC (every rank: all of it)
         const i64 nl = As->rowptr[As->m_loc] - As->rowptr[0];
         std::vector<int64_t> ri, ci;
@@ -1016,13 +1042,20 @@ float pxdistribute(int dtype, const char *name, superlu_dist_options_t *options,
             std::vector<int64_t> r((size_t)nl), c((size_t)nl);
             std::vector<T> v((size_t)nl);
             const T *av = (const T *)As->nzval;
-            i64 e = 0;
-            for (i64 i = 0; i < As->m_loc; ++i)
-                for (i64 p = As->rowptr[i]; p < As->rowptr[i + 1]; ++p, ++e) {
-                    r[e] = pc[pr[i + As->fst_row]];
-                    c[e] = As->colind[p];
-                    v[e] = av[p];
+            // (rows in blocks on the host threads: entry e of row i is at
+            // rowptr[i] - rowptr[0] + its position in the row)
+            const i64 m_loc = As->m_loc, p0 = As->rowptr[0];
+            const int nrb = (int)((m_loc + 16383) / 16384);
+            slu::parallel_for(nrb, [&](int t) {
+                for (i64 i = (i64)t * 16384; i < std::min<i64>(m_loc, (i64)(t + 1) * 16384); ++i) {
+                    const int64_t gi = pc[pr[i + As->fst_row]];
+                    for (i64 p = As->rowptr[i]; p < As->rowptr[i + 1]; ++p) {
+                        r[p - p0] = gi;
+                        c[p - p0] = As->colind[p];
+                        v[p - p0] = av[p];
+                    }
                 }
+            }, 1);
             if (P == 1) {
                 ri.swap(r);
                 ci.swap(c);
@@ -1054,11 +1087,52 @@ float pxdistribute(int dtype, const char *name, superlu_dist_options_t *options,
                 gather(v.data(), vv.data(), (int)sizeof(T));
             }
         }
+        dtick("A coordinates");
         std::vector<int64_t> xa(n + 1, 0), asub(ri.size());
         std::vector<T> aval(ri.size());
-        for (int64_t c : ci) xa[c + 1]++;
-        for (i64 j = 0; j < n; ++j) xa[j + 1] += xa[j];
-        {
+        const i64 ne = (i64)ri.size();
+        // CSC by a counting sort; each column's entries in entry order (the
+        // stash below compares the pattern with the previous call's).  On
+        // the host threads: per (entry chunk, column) counts, then each chunk
+        // fills its slice of every column
+        const int NCH = std::max(1, std::min(slu::plan_threads(), (int)std::min<i64>(16, ne / 65536 + 1)));
+        if (NCH > 1 && ne < INT32_MAX && (i64)NCH * n <= (1ll << 27)) {
+            std::vector<int32_t> cc((size_t)NCH * n, 0); // counts, then fill cursors
+            auto eb = [&](int c) { return ne * c / NCH; };
+            slu::parallel_for(NCH, [&](int c) {
+                int32_t *cnt = cc.data() + (size_t)c * n;
+                for (i64 e = eb(c); e < eb(c + 1); ++e) cnt[ci[e]]++;
+            }, 1);
+            const int NB = (int)((n + 65535) / 65536);
+            slu::parallel_for(NB, [&](int t) {
+                for (i64 j = (i64)t * 65536; j < std::min<i64>(n, (i64)(t + 1) * 65536); ++j) {
+                    i64 tot = 0;
+                    for (int c = 0; c < NCH; ++c) tot += cc[(size_t)c * n + j];
+                    xa[j + 1] = tot;
+                }
+            }, 1);
+            for (i64 j = 0; j < n; ++j) xa[j + 1] += xa[j];
+            slu::parallel_for(NB, [&](int t) {
+                for (i64 j = (i64)t * 65536; j < std::min<i64>(n, (i64)(t + 1) * 65536); ++j) {
+                    i64 pos = xa[j];
+                    for (int c = 0; c < NCH; ++c) {
+                        const int32_t k = cc[(size_t)c * n + j];
+                        cc[(size_t)c * n + j] = (int32_t)pos;
+                        pos += k;
+                    }
+                }
+            }, 1);
+            slu::parallel_for(NCH, [&](int c) {
+                int32_t *f = cc.data() + (size_t)c * n;
+                for (i64 e = eb(c); e < eb(c + 1); ++e) {
+                    const i64 q = f[ci[e]]++;
+                    asub[q] = ri[e];
+                    aval[q] = vv[e];
+                }
+            }, 1);
+        } else {
+            for (int64_t c : ci) xa[c + 1]++;
+            for (i64 j = 0; j < n; ++j) xa[j + 1] += xa[j];
             std::vector<int64_t> f(xa.begin(), xa.end() - 1);
             for (size_t e = 0; e < ri.size(); ++e) {
                 const i64 q = f[ci[e]]++;
@@ -1066,6 +1140,15 @@ float pxdistribute(int dtype, const char *name, superlu_dist_options_t *options,
                 aval[q] = vv[e];
             }
         }
+        dtick("A as CSC");
+        // A's values go only to the stash (the device fill's source), not
+        // into the host L / U arrays: their first touch is the 16.8 GB of
+        // page zeroing that dominated pddistribute at 100^3, and nothing of
+        // this library reads them before pdgstrf overwrites them (INTEGRATION
+        // §1).  SUPERLU_MI355X_DEFER_A=0 or HOST_FACTORS=1: placed as the
+        // reference does.
+        const char *hfe = getenv("SUPERLU_MI355X_HOST_FACTORS"), *dfe = getenv("SUPERLU_MI355X_DEFER_A");
+        const bool defer = dtype == SLU_D && !(hfe && atoi(hfe) == 1) && !(dfe && atoi(dfe) == 0);
         auto stash = [&](bool first_time) { // A for the device fill of the following pdgstrf
             std::lock_guard<std::mutex> lk(g_deva_mu);
             const bool same = g_deva.lu == LU && g_deva.llu == LU->Llu &&
@@ -1084,20 +1167,28 @@ float pxdistribute(int dtype, const char *name, superlu_dist_options_t *options,
             g_deva.asub = std::move(asub);
             g_deva.a.assign((const char *)aval.data(), (const char *)(aval.data() + aval.size()));
             g_deva.gen = ++g_deva_gen;
+            if (defer) g_host_a_deferred.insert(LU->Llu);
+            else g_host_a_deferred.erase(LU->Llu);
         };
         if (options->Fact == 2 /* SamePattern_SameRowPerm */) {
-            if (slu_refill_values(dtype, LU, n, xa.data(), asub.data(), aval.data(), Pr, Pc, myrow,
-                                  mycol))
+            if (!defer && slu_refill_values(dtype, LU, n, xa.data(), asub.data(), aval.data(), Pr, Pc, myrow,
+                                            mycol))
                 throw slu::Error(slu_last_error());
+            dtick("refill");
             stash(false);
+            dtick("stash");
             return 0.0f;
         }
         // ---- first-time branch: the restated structural distribute
         const Glu_persist_t *gp = LU->Glu_persist;
-        LUS *tmp = (LUS *)slu_distribute_glu(dtype, n, gp->xsup, gp->supno, glu->xlsub, glu->lsub,
-                                             glu->xusub, glu->usub, xa.data(), asub.data(),
-                                             aval.data(), Pr, Pc, myrow, mycol);
+        LUS *tmp = defer ? (LUS *)slu_distribute_glu_deferred(n, gp->xsup, gp->supno, glu->xlsub, glu->lsub,
+                                                              glu->xusub, glu->usub, xa.data(), asub.data(),
+                                                              (const double *)aval.data(), Pr, Pc, myrow, mycol)
+                         : (LUS *)slu_distribute_glu(dtype, n, gp->xsup, gp->supno, glu->xlsub, glu->lsub,
+                                                     glu->xusub, glu->usub, xa.data(), asub.data(),
+                                                     aval.data(), Pr, Pc, myrow, mycol);
         if (!tmp) throw slu::Error(slu_last_error());
+        dtick("structural distribute");
         *LU->Llu = *tmp->Llu; // the arrays move over (malloc'ed: SUPERLU_FREE frees them)
         free(tmp->Glu_persist->xsup);
         free(tmp->Glu_persist->supno);
@@ -1185,7 +1276,9 @@ float pxdistribute(int dtype, const char *name, superlu_dist_options_t *options,
             std::lock_guard<std::mutex> lk(g_cache_mu);
             unmark_evicted(lu_key(LU)); // new storage: A's values, no factors yet
         }
+        dtick("placeholders");
         stash(true);
+        dtick("stash");
         return (float)((double)Llu->Lnzval_bc_cnt * sizeof(T) + (double)Llu->Unzval_br_cnt * sizeof(T) +
                        (double)(Llu->Lrowind_bc_cnt + Llu->Ufstnz_br_cnt) * sizeof(int_t));
     } catch (const std::exception &e) {

@@ -68,6 +68,19 @@ inline void *calloc_huge(size_t n, size_t sz) {
     return p;
 }
 
+// the same for storage every element of which is written here (index
+// arrays, the U segment list), first touched on the worker threads
+inline void *malloc_huge(size_t bytes) {
+    void *p = malloc(bytes);
+    constexpr uintptr_t HP = uintptr_t(2) << 20;
+    const uintptr_t a = ((uintptr_t)p + HP - 1) & ~(HP - 1), e = ((uintptr_t)p + bytes) & ~(HP - 1);
+    if (p && e > a) madvise((void *)a, e - a, MADV_HUGEPAGE);
+    return p;
+}
+struct FreeDeleter {
+    void operator()(void *p) const { free(p); }
+};
+
 // Per-thread scratch of -1s, reset when a new call (generation) first uses
 // it on a thread: parallel_for's workers are fresh threads, but the calling
 // thread keeps its thread_locals from one call to the next.
@@ -87,7 +100,8 @@ inline i64 next_generation() {
 template <typename T, typename LocalLU, typename LUstruct>
 void *distribute_glu_t(i64 n, const int_t *xsup_in, const int_t *supno_in, const int_t *xlsub,
                        const int_t *lsub, const int_t *xusub, const int_t *usub, const i64 *xa,
-                       const i64 *asub, const T *a, int Pr, int Pc, int myrow, int mycol) {
+                       const i64 *asub, const T *a, int Pr, int Pc, int myrow, int mycol,
+                       bool place_a = true) {
     SLU_REQUIRE(n > 0 && Pr > 0 && Pc > 0 && myrow >= 0 && myrow < Pr && mycol >= 0 && mycol < Pc,
                 "distribute: bad arguments (n %lld, grid %dx%d, rank (%d,%d))", (long long)n, Pr,
                 Pc, myrow, mycol);
@@ -115,7 +129,7 @@ void *distribute_glu_t(i64 n, const int_t *xsup_in, const int_t *supno_in, const
     // (uninitialised storage: the fill below touches every entry on the
     // threads, where a vector's value-initialisation wrote GBs serially)
     // (int32 pairs: n < 2^31 is checked below; half the bytes to write)
-    std::unique_ptr<std::pair<int32_t, int32_t>[]> useg;
+    std::unique_ptr<std::pair<int32_t, int32_t>[], FreeDeleter> useg;
     {
         const int NCH = std::max(1, std::min(4 * slu::plan_threads(), (int)std::min<i64>(n, 64)));
         vector<i64> cb(NCH + 1, 0); // chunk c: columns [cb[c], cb[c + 1])
@@ -159,7 +173,8 @@ void *distribute_glu_t(i64 n, const int_t *xsup_in, const int_t *supno_in, const
         }, 1);
         SLU_REQUIRE(n < INT32_MAX, "distribute: n = %lld too large", (long long)n);
         dtick("U segments: offsets");
-        useg.reset(new std::pair<int32_t, int32_t>[(size_t)ucnt[ns]]);
+        useg.reset((std::pair<int32_t, int32_t> *)malloc_huge((size_t)ucnt[ns] * sizeof(std::pair<int32_t, int32_t>)));
+        SLU_REQUIRE(useg || !ucnt[ns], "distribute: out of host memory (U segments)");
         slu::parallel_for(NCH, [&](int c) {
             i64 *fill = cc.data() + (size_t)c * ns;
             for (i64 j = cb[c]; j < cb[c + 1]; ++j)
@@ -293,7 +308,7 @@ void *distribute_glu_t(i64 n, const int_t *xsup_in, const int_t *supno_in, const
     }
     Llu->Lrowind_bc_cnt = li + 1;
     Llu->Lnzval_bc_cnt = lv + 1;
-    Llu->Lrowind_bc_dat = (int_t *)malloc((li + 1) * sizeof(int_t));
+    Llu->Lrowind_bc_dat = (int_t *)malloc_huge((li + 1) * sizeof(int_t));
     // a == nullptr: index arrays only (no value storage; the coarse symbolic
     // of frontend.cpp reads the structure of the 1x1 layout)
     // value arrays zeroed by calloc: fresh zero pages from the kernel for
@@ -320,7 +335,7 @@ void *distribute_glu_t(i64 n, const int_t *xsup_in, const int_t *supno_in, const
     }
     Llu->Ufstnz_br_cnt = ui + 1;
     Llu->Unzval_br_cnt = uv + 1;
-    Llu->Ufstnz_br_dat = (int_t *)malloc((ui + 1) * sizeof(int_t));
+    Llu->Ufstnz_br_dat = (int_t *)malloc_huge((ui + 1) * sizeof(int_t));
     Llu->Unzval_br_dat = a ? (T *)calloc_huge((size_t)(uv + 1), sizeof(T)) : nullptr;
     SLU_REQUIRE(Llu->Ufstnz_br_dat && (Llu->Unzval_br_dat || !a), "distribute: out of host memory (U)");
     Llu->Ufstnz_br_dat[ui] = 0;
@@ -333,6 +348,7 @@ void *distribute_glu_t(i64 n, const int_t *xsup_in, const int_t *supno_in, const
         const i64 gb = (i64)lb * Pr + myrow, klst = xsup[gb + 1];
         int_t *index = Llu->Ufstnz_br_dat + Llu->Ufstnz_br_offset[lb];
         T *uval = a ? Llu->Unzval_br_dat + Llu->Unzval_br_offset[lb] : nullptr;
+        const bool put = a && place_a;
         Llu->Ufstnz_br_ptr[lb] = index;
         Llu->Unzval_br_ptr[lb] = uval;
         const i64 len1 = u_len1[lb];
@@ -355,7 +371,7 @@ void *distribute_glu_t(i64 n, const int_t *xsup_in, const int_t *supno_in, const
             index[desc + SLU_UB_DESCRIPTOR + (j - xsup[jb])] = irow;
             const i64 k = klst - irow;
             index[desc + 1] += k;
-            if (a) {
+            if (put) {
                 T *seg = uval + vo; // (zero from calloc)
                 for (i64 p = xa[j]; p < xa[j + 1]; ++p) {
                     const i64 r = asub[p];
@@ -427,7 +443,7 @@ void *distribute_glu_t(i64 n, const int_t *xsup_in, const int_t *supno_in, const
             pos[row] = cnt[s]++;
         }
         // (lusup is zero from calloc)
-        for (i64 c = 0; a && c < w; ++c) {
+        for (i64 c = 0; a && place_a && c < w; ++c) {
             const i64 j = f + c;
             for (i64 p = xa[j]; p < xa[j + 1]; ++p) {
                 const i64 row = asub[p];
@@ -557,6 +573,23 @@ void *slu_distribute_glu(int dtype, int64_t n, const int_t *xsup, const int_t *s
                 nprow, npcol, myrow, mycol);
         }
         throw slu::Error(slu::fmt("distribute: bad dtype %d", dtype));
+    } catch (const std::exception &e) {
+        slu::set_last_error(e.what());
+        return nullptr;
+    }
+}
+
+// pddistribute of the device-resident library (abi.cpp): the value arrays
+// allocated (zero) but A's entries not placed -- its pdgstrf fills the
+// device storage from the A it keeps (real fp64 only)
+void *slu_distribute_glu_deferred(int64_t n, const int_t *xsup, const int_t *supno,
+                                  const int_t *xlsub, const int_t *lsub, const int_t *xusub,
+                                  const int_t *usub, const int64_t *xa, const int64_t *asub,
+                                  const double *a, int nprow, int npcol, int myrow, int mycol) {
+    try {
+        return distribute_glu_t<double, dLocalLU_t, dLUstruct_t>(n, xsup, supno, xlsub, lsub, xusub, usub,
+                                                                 xa, asub, a, nprow, npcol, myrow, mycol,
+                                                                 false);
     } catch (const std::exception &e) {
         slu::set_last_error(e.what());
         return nullptr;

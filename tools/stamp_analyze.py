@@ -68,6 +68,63 @@ def main():
             ov.append(c)
     ov = np.array(ov)
     print("tiles overlapping on the same CU:", {int(v): int((ov == v).sum()) for v in np.unique(ov)})
+    # phase alignment: per CU, the time with >= 1 tile resident, with >= 1 /
+    # 2 tiles in their K loop (K-loop intervals placed by the cycle counts)
+    cpt = np.median(tot[sel] / d["dur"][sel])  # cycles per 100 MHz tick
+    res = k1 = k2 = 0.0
+    for cu, idx in by.items():
+        ev_r, ev_k = [], []
+        for i in idx:
+            s0 = float(d["rt0"][i])
+            ev_r += [(s0, 1), (s0 + d["dur"][i], -1)]
+            ks = s0 + d["pro"][i] / cpt
+            ev_k += [(ks, 1), (ks + d["kl"][i] / cpt, -1)]
+        for ev, acc in ((ev_r, "r"), (ev_k, "k")):
+            ev.sort()
+            c, last = 0, None
+            for t, dv in ev:
+                if last is not None and c > 0:
+                    if acc == "r":
+                        res += t - last
+                    else:
+                        k1 += t - last
+                        if c > 1:
+                            k2 += t - last
+                last = t
+                c += dv
+    print(f"per CU, of the time with a tile resident: >=1 tile in its K loop {k1 / res:.1%}, "
+          f">=2 tiles in their K loops {k2 / res:.1%}")
+    # what a full kw-256 tile's K loop overlapped on its CU: the other tiles'
+    # prologue / K loop / epilogue time over its K interval, and its cycles
+    # per stage binned by the dominant one
+    bins = defaultdict(list)
+    for cu, idx in by.items():
+        idx = sorted(idx, key=lambda i: d["rt0"][i])
+        ph = []
+        for i in idx:
+            s0 = float(d["rt0"][i])
+            a = s0 + d["pro"][i] / cpt
+            b = a + d["kl"][i] / cpt
+            ph.append((s0, a, b, b + d["epi"][i] / cpt))
+        for j, i in enumerate(idx):
+            if not (full[i] and d["kw"][i] == 256):
+                continue
+            ks, ke = ph[j][1], ph[j][2]
+            ov = [0.0, 0.0, 0.0]
+            for q in range(max(0, j - 8), min(len(idx), j + 8)):
+                if q == j:
+                    continue
+                p0, p1, p2, p3 = ph[q]
+                for t, (lo, hi) in enumerate(((p0, p1), (p1, p2), (p2, p3))):
+                    ov[t] += max(0.0, min(hi, ke) - max(lo, ks))
+            L = max(ke - ks, 1e-9)
+            f = [x / L for x in ov]
+            key = "alone" if sum(f) < 0.3 else ("pro", "K", "epi")[int(np.argmax(f))]
+            bins[key].append(d["kl"][i] / 16)
+    for key in ("alone", "pro", "K", "epi"):
+        v = np.array(bins.get(key, [0]))
+        print(f"full kw-256 tiles whose K loop mostly overlapped {key:5s}: {len(bins.get(key, [])):7d} tiles, "
+              f"cycles per stage mean {v.mean():7.0f} median {np.median(v):7.0f}")
 
 
 if __name__ == "__main__":
