@@ -1288,15 +1288,6 @@ k_schur_big(const TileItem *tiles, const KInfo<T> *kinfo, T *Lval, T *Uval,
     enum { c0_, c1_, c2_, c3_, rt_ };
     if (threadIdx.x == 0) s_stamp_[rt_] = wall_clock64();
 #endif
-#ifdef SB_DEPHASE
-    // (A/B build) the first launch round's second workgroup per CU starts
-    // SB_DEPHASE cycles late, so that the two residents' K loops and
-    // prologue/epilogue alternate instead of running in step
-    if (blockIdx.x >= 256 && blockIdx.x < 512 && gridDim.x >= 1024) {
-        const long long t = clock64();
-        while (clock64() - t < SB_DEPHASE) __builtin_amdgcn_s_sleep(16);
-    }
-#endif
     SB_STAMP(c0_);
     const TileItem ti = tiles[blockIdx.x];
     const KInfo<T> ki = kinfo[ti.kslot];
