@@ -4014,6 +4014,13 @@ struct Plan : PlanBase {
         SLU_REQUIRE(xa[0] == 0 && xa[n] >= 0, "A: bad column pointers");
         const int_t *supno = LU->Glu_persist->supno;
         const i64 nnz = xa[n];
+        const bool aprof = getenv("SLU_PROFILE_PLAN") != nullptr;
+        auto ta = std::chrono::steady_clock::now();
+        auto atick = [&](const char *what) { // SLU_PROFILE_PLAN: phase times on stderr
+            if (!aprof) return;
+            fprintf(stderr, "[slu plan %d] a_pattern %-16s %7.1f ms\n", iam, what, ms_since(ta));
+            ta = std::chrono::steady_clock::now();
+        };
         vector<i64> map((size_t)nnz, -1);
         // columns on the host threads: each nonzero belongs to one column, so
         // the writes to map are disjoint
@@ -4053,8 +4060,10 @@ struct Plan : PlanBase {
                 if (i + 1 == col.size() || col[i + 1].first != col[i].first)
                     map[col[i].second] = col[i].first;
         }, 512);
+        atick("map");
         d_amap.upload(map.empty() ? vector<i64>(1, -1) : map);
         d_aval.alloc(std::max<i64>(nnz, 1));
+        atick("map upload");
         a_nnz = nnz;
         d_acur = a_fact = snap_acur = nullptr; // the previous pattern's values are gone
         {   // rows of A for the refinement's residual (k_resid): all of A on a
@@ -4062,24 +4071,62 @@ struct Plan : PlanBase {
             auto mine = [&](i64 e, int j) {
                 return !xmode || ((int)supno[j] % Pc == mycol && (int)supno[asub[e]] % Pr == myrow);
             };
+            // a counting sort by row on the host threads: the columns in NCH
+            // chunks of about equal nnz, per (chunk, row) counts, then each
+            // chunk fills its slice of every row (chunk order = column order,
+            // so each row's entries come in column order, as serially)
+            const int NCH = std::max(1, std::min(plan_threads(), (int)std::min<i64>(16, nnz / 65536 + 1)));
+            SLU_REQUIRE(nnz < INT32_MAX, "A: %lld nonzeros", (long long)nnz);
+            vector<int> cb(NCH + 1, 0);
+            for (int c = 1; c < NCH; ++c)
+                cb[c] = std::max(cb[c - 1], (int)(std::lower_bound(xa, xa + n + 1, nnz * c / NCH) - xa));
+            cb[NCH] = n;
+            vector<int32_t> cc((size_t)NCH * n, 0); // [chunk][row] counts, then fill cursors
+            parallel_for(NCH, [&](int c) {
+                int32_t *cnt = cc.data() + (size_t)c * n;
+                for (int j = cb[c]; j < cb[c + 1]; ++j)
+                    for (i64 e = xa[j]; e < xa[j + 1]; ++e)
+                        if (mine(e, j)) ++cnt[asub[e]];
+            }, 1);
             vector<i64> rp(n + 1, 0);
-            for (int j = 0; j < n; ++j)
-                for (i64 e = xa[j]; e < xa[j + 1]; ++e)
-                    if (mine(e, j)) ++rp[asub[e] + 1];
-            for (int i = 0; i < n; ++i) rp[i + 1] += rp[i];
-            vector<i64> re((size_t)rp[n]), nx(rp.begin(), rp.end() - 1);
-            vector<int> rc((size_t)rp[n]);
-            for (int j = 0; j < n; ++j)
-                for (i64 e = xa[j]; e < xa[j + 1]; ++e) {
-                    if (!mine(e, j)) continue;
-                    const i64 q = nx[asub[e]]++;
-                    rc[q] = j;
-                    re[q] = e;
+            const int NB = (n + 65535) / 65536;
+            parallel_for(NB, [&](int t) {
+                for (int i = t * 65536; i < std::min(n, (t + 1) * 65536); ++i) {
+                    i64 tot = 0;
+                    for (int c = 0; c < NCH; ++c) tot += cc[(size_t)c * n + i];
+                    rp[i + 1] = tot;
                 }
+            }, 1);
+            for (int i = 0; i < n; ++i) rp[i + 1] += rp[i];
+            parallel_for(NB, [&](int t) {
+                for (int i = t * 65536; i < std::min(n, (t + 1) * 65536); ++i) {
+                    i64 pos = rp[i];
+                    for (int c = 0; c < NCH; ++c) {
+                        const int32_t k = cc[(size_t)c * n + i];
+                        cc[(size_t)c * n + i] = (int32_t)pos;
+                        pos += k;
+                    }
+                }
+            }, 1);
+            vector<i64> re((size_t)rp[n]);
+            vector<int> rc((size_t)rp[n]);
+            parallel_for(NCH, [&](int c) {
+                int32_t *nx = cc.data() + (size_t)c * n;
+                for (int j = cb[c]; j < cb[c + 1]; ++j)
+                    for (i64 e = xa[j]; e < xa[j + 1]; ++e) {
+                        if (!mine(e, j)) continue;
+                        const i64 q = nx[asub[e]]++;
+                        rc[q] = j;
+                        re[q] = e;
+                    }
+            }, 1);
+            atick("rows");
             d_rp.upload(rp);
             d_rc.upload(rc.empty() ? vector<int>(1, 0) : rc);
             d_re.upload(re.empty() ? vector<i64>(1, 0) : re);
+            atick("rows upload");
             HIPCHK(hipDeviceSynchronize());
+            atick("device sync");
         }
     }
 
