@@ -27,12 +27,13 @@
 #include <vector>
 
 #include "common.h"
+#include "noinit_vec.h"
 #include "slu_abi.h"
 
 // csrc/symbolic_dev.hip (the full library links both)
 bool slu_symb_epilogue_dev(int64_t n, int64_t nsup, const int32_t *raw, int64_t raw_len, const int64_t *xlsub_raw,
                            const int32_t *xsup, const int32_t *supno, const int32_t *usub, int64_t nu,
-                           std::vector<int64_t> &lsub, std::vector<int64_t> &xlsub, int64_t *nnzL, int64_t *nnzU,
+                           slu::i64_vec &lsub, std::vector<int64_t> &xlsub, int64_t *nnzL, int64_t *nnzU,
                            std::string &err);
 bool slu_symb_have_device();
 
@@ -44,19 +45,21 @@ using I = int64_t;
 // where the last symbfact ran its epilogue (countnz + fixupL): 0 host, 1 device
 static int g_last_epilogue = 0;
 
-// SLU_SYMB_DEVICE=1: the epilogue on the GPU (an error without one), =0: on
-// the host; unset: the caller's default -- the engine API (slu_symbfact, one
-// process per GPU) on the GPU for square problems with >= 20 000 supernodes
-// when a GPU is visible; the drop-in `symbfact`, which pdgssvx calls on every
-// rank of an MPI job, on the host (the search stays on the host either way)
+// SLU_SYMB_DEVICE=1: the epilogue on the GPU (an error without one); else on
+// the host threads, for every caller.  (Round 6: the host epilogue on the
+// host threads with uninitialised index storage takes 0.34 s at 100^3 in the
+// build container, 1.8 s before; the device one cost 0.67 s on the box, most
+// of it initialising HIP from inside the symbolic phase.)  The search stays
+// on the host either way.
 static bool use_device_epilogue(I m, I n, I nsup, bool dev_default) {
+    (void)nsup;
+    (void)dev_default;
     const char *e = getenv("SLU_SYMB_DEVICE");
-    if (e) {
-        if (atoi(e) == 0) return false;
+    if (e && atoi(e) != 0) {
         if (!slu_symb_have_device()) throw Error("symbfact: SLU_SYMB_DEVICE=1 but no GPU is visible");
         return m == n;
     }
-    return dev_default && m == n && nsup >= 20000 && slu_symb_have_device();
+    return false;
 }
 using std::vector;
 constexpr I NONE = -1;
@@ -182,7 +185,8 @@ static vector<I> relaxed_ends(I n, const I *et, I relax) {
 
 struct Result {
     I n = 0;
-    vector<I> xsup, supno, xlsub, lsub, xusub, usub;
+    vector<I> xsup, supno, xlsub, xusub;
+    i64_vec lsub, usub; // (filled on the host threads or by the device epilogue's copy)
     I nnzL = 0, nnzU = 0, nnzLU = 0, lsub_size = 0;
 };
 
@@ -776,45 +780,82 @@ static Result symbfact_t(I m, I n, const I *cb, const I *ce, const I *ri64, cons
             return R;
         }
     }
+    auto te = std::chrono::steady_clock::now();
+    auto etick = [&](const char *what) {
+        if (!getenv("SLU_SYMB_TIME")) return;
+        fprintf(stderr, "symbfact epilogue: %-10s %.3f s\n", what,
+                std::chrono::duration<double>(std::chrono::steady_clock::now() - te).count());
+        te = std::chrono::steady_clock::now();
+    };
     R.xsup.assign(w.xsup.begin(), w.xsup.end());
     R.supno.assign(w.supno.begin(), w.supno.end());
     R.xlsub = std::move(w.xlsub);
     R.xusub = std::move(w.xusub);
-    R.usub.assign(w.usub.begin(), w.usub.begin() + R.xusub[mn]);
+    {
+        const I nu = R.xusub[mn];
+        R.usub.resize(nu);
+        parallel_for((int)((nu + (1 << 20) - 1) >> 20), [&](int t) {
+            for (I p = (I)t << 20; p < std::min<I>(nu, (I)(t + 1) << 20); ++p) R.usub[p] = w.usub[p];
+        }, 1);
+    }
+    etick("copies");
 
     // ---- counts (SRC/util.c:95-152) and the final L subscripts: the first
-    // column's list of each supernode, in supernode order (SRC/util.c:163-199)
+    // column's list of each supernode, in supernode order (SRC/util.c:163-199).
+    // On the host threads: blocks of supernodes / columns, partial sums added
+    // in block order (integers: the same totals as serially)
     const I nsup = R.supno[n];
-    for (I s = 0; s <= nsup; ++s) {
-        const I f = R.xsup[s];
-        I len = R.xlsub[f + 1] - R.xlsub[f];
-        for (I c = f; c < R.xsup[s + 1]; ++c) {
-            R.nnzL += len;
-            R.nnzU += c - f + 1;
-            --len;
+    constexpr I SB = 4096;
+    const int nsb = (int)((nsup + 1 + SB - 1) / SB), ncb = (int)((n + SB - 1) / SB);
+    vector<I> pl(nsb, 0), pu(nsb, 0), pc(ncb, 0), flen(nsup + 1), fsrc(nsup + 1);
+    parallel_for(nsb, [&](int t) {
+        I a = 0, u = 0;
+        for (I s = (I)t * SB; s < std::min<I>(nsup + 1, (I)(t + 1) * SB); ++s) {
+            const I f = R.xsup[s];
+            fsrc[s] = R.xlsub[f];
+            flen[s] = R.xlsub[f + 1] - R.xlsub[f];
+            I len = flen[s];
+            for (I c = f; c < R.xsup[s + 1]; ++c) {
+                a += len;
+                u += c - f + 1;
+                --len;
+            }
         }
-    }
-    for (I c = 0; c < n; ++c)
-        for (I p = R.xusub[c]; p < R.xusub[c + 1]; ++p) {
-            const I f = R.usub[p];
-            R.nnzU += R.xsup[R.supno[f] + 1] - f;
-        }
+        pl[t] = a;
+        pu[t] = u;
+    }, 1);
+    parallel_for(ncb, [&](int t) {
+        I u = 0;
+        for (I c = (I)t * SB; c < std::min<I>(n, (I)(t + 1) * SB); ++c)
+            for (I p = R.xusub[c]; p < R.xusub[c + 1]; ++p) {
+                const I f = R.usub[p];
+                u += R.xsup[R.supno[f] + 1] - f;
+            }
+        pc[t] = u;
+    }, 1);
+    etick("counts");
+    for (I v : pl) R.nnzL += v;
+    for (I v : pu) R.nnzU += v;
+    for (I v : pc) R.nnzU += v;
     R.nnzLU = R.nnzL + R.nnzU - mn;
     if (n > 1) {
         R.lsub_size = R.xlsub[n];
-        I out = 0;
-        I total = 0;
-        for (I s = 0; s <= nsup; ++s) total += R.xlsub[R.xsup[s] + 1] - R.xlsub[R.xsup[s]];
-        R.lsub.resize(total);
-        for (I s = 0; s <= nsup; ++s) {
-            const I f = R.xsup[s], a = R.xlsub[f], b = R.xlsub[f + 1];
-            R.xlsub[f] = out;
-            // the reference applies perm_r here: the identity on pivoted
-            // rows, EMPTY on rows past min(m, n)
-            for (I p = a; p < b; ++p) R.lsub[out++] = (I)w.lsub[p] < mn ? (I)w.lsub[p] : NONE;
-            for (I c = f + 1; c < R.xsup[s + 1]; ++c) R.xlsub[c] = out;
-        }
-        R.xlsub[n] = out;
+        vector<I> out(nsup + 2, 0);
+        for (I s = 0; s <= nsup; ++s) out[s + 1] = out[s] + flen[s];
+        R.lsub.resize(out[nsup + 1]);
+        etick("lsub alloc");
+        parallel_for(nsb, [&](int t) {
+            for (I s = (I)t * SB; s < std::min<I>(nsup + 1, (I)(t + 1) * SB); ++s) {
+                const I f = R.xsup[s], a = fsrc[s], o = out[s];
+                // the reference applies perm_r here: the identity on pivoted
+                // rows, EMPTY on rows past min(m, n)
+                for (I q = 0; q < flen[s]; ++q) R.lsub[o + q] = (I)w.lsub[a + q] < mn ? (I)w.lsub[a + q] : NONE;
+                R.xlsub[f] = o;
+                for (I c = f + 1; c < R.xsup[s + 1]; ++c) R.xlsub[c] = o + flen[s];
+            }
+        }, 1);
+        R.xlsub[n] = out[nsup + 1];
+        etick("lsub");
     } else {
         R.lsub.assign(w.lsub.begin(), w.lsub.begin() + R.xlsub[n]);
     }
@@ -852,8 +893,8 @@ static I relax_of(const superlu_dist_options_t *o) {
     return std::min(env_or("SUPERLU_RELAX", "NREL", o->superlu_relax, false), maxsup_of(o));
 }
 
-template <class T>
-static T *copy_out(const vector<I> &v, size_t n) {
+template <class T, class V>
+static T *copy_out(const V &v, size_t n) {
     T *p = (T *)malloc(std::max<size_t>(n, 1) * sizeof(T));
     if (!p) throw Error("symbfact: out of host memory");
     if (n) memcpy(p, v.data(), n * sizeof(T));

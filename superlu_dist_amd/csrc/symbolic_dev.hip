@@ -21,6 +21,8 @@
 #include <string>
 #include <vector>
 
+#include "noinit_vec.h"
+
 namespace slu {
 namespace symbdev {
 
@@ -87,7 +89,7 @@ template <class T> struct Dev {
 // supernode, xlsub_raw positions), xsup / supno / usub int32.  Fills lsub
 // (compact, the final size known from the lists), xlsub[0..n], nnzL / nnzU.
 bool epilogue(I n, I nsup, const int32_t *raw, I raw_len, const I *xlsub_raw, const int32_t *xsup,
-              const int32_t *supno, const int32_t *usub, I nu, std::vector<I> &lsub, std::vector<I> &xlsub,
+              const int32_t *supno, const int32_t *usub, I nu, i64_vec &lsub, std::vector<I> &xlsub,
               I *nnzL, I *nnzU, std::string &err) {
     // per supernode: source position and compact offset (host: O(nsup))
     std::vector<I> src(nsup), off(nsup + 1);
@@ -155,7 +157,7 @@ bool epilogue(I n, I nsup, const int32_t *raw, I raw_len, const I *xlsub_raw, co
 // C++ entry for csrc/symbolic.cpp (the full library links both)
 bool slu_symb_epilogue_dev(int64_t n, int64_t nsup, const int32_t *raw, int64_t raw_len, const int64_t *xlsub_raw,
                            const int32_t *xsup, const int32_t *supno, const int32_t *usub, int64_t nu,
-                           std::vector<int64_t> &lsub, std::vector<int64_t> &xlsub, int64_t *nnzL, int64_t *nnzU,
+                           slu::i64_vec &lsub, std::vector<int64_t> &xlsub, int64_t *nnzL, int64_t *nnzU,
                            std::string &err) {
     return slu::symbdev::epilogue(n, nsup, raw, raw_len, xlsub_raw, xsup, supno, usub, nu, lsub, xlsub, nnzL, nnzU,
                                   err);
