@@ -392,3 +392,41 @@ def test_second_system_on_the_same_grid():
     summary = "\n".join(" ".join(r) for r in res)
     assert len(res) == 4 and all(int(i) == 0 and float(e) < 1e-10 and rs == "same"
                                  for _, _, i, e, rs in res), summary
+
+
+_DEFER_CHILD = r"""
+import numpy as np
+from superlu_dist_amd import capi
+from superlu_dist_amd import symbolic as SY
+from superlu_dist_amd.frontend import STENCIL_3D7, Csc, nd_order
+nx = 8
+def system():
+    A = Csc.stencil(STENCIL_3D7, nx, nx, nx)
+    n = A.n
+    cp, ri, v = A.arrays()
+    co = SY.sp_colorder(n, n, cp, ri, nd_order(nx, nx, nx), SY.MY_PERMC)
+    sb = SY.symbfact(n, n, co.colbeg, co.colend, SY.relabel_rows(ri, co.perm_c), co.etree, 60, 256)
+    return capi.DeviceResidentSystem(n, cp, co.perm_c[ri], v, co.perm_c, co.etree, sb.xsup, sb.supno,
+                                     sb.xlsub, sb.lsub, sb.xusub, sb.usub, 12.0)
+s1, s2 = system(), system()
+s1.distribute(0)
+s2.distribute(0)  # replaces the A kept for s1's device fill
+print("factoring s1", flush=True)
+s1.factor()
+print("s1 factored", flush=True)
+"""
+
+
+@pytest.mark.gpu
+def test_deferred_a_replaced_fails_loudly():
+    """libslu_mi355x_solve.so's pddistribute keeps A for the device fill
+    instead of placing it into the host value arrays: a
+    pdgstrf on an LUstruct whose kept A another pddistribute has replaced
+    stops with a message instead of factoring the zero host arrays."""
+    import subprocess
+    import sys
+    r = subprocess.run([sys.executable, "-c", _DEFER_CHILD], capture_output=True, text=True, timeout=240,
+                       cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert "factoring s1" in r.stdout, r.stdout + r.stderr
+    assert "s1 factored" not in r.stdout and r.returncode != 0
+    assert "another pddistribute has replaced" in r.stderr, r.stderr[-2000:]
