@@ -3,7 +3,11 @@
 // arrays are filled on the host threads or by a device copy right after, and
 // the serial zeroing a plain vector does first cost as much as the fill.
 #pragma once
+#include <sys/mman.h>
+
 #include <cstdint>
+#include <cstdlib>
+#include <new>
 #include <memory>
 #include <utility>
 #include <vector>
@@ -15,6 +19,21 @@ template <class T> struct NoInit : std::allocator<T> {
     template <class U> struct rebind {
         using other = NoInit<U>;
     };
+    // arrays of 64 MB and more on 2 MB-aligned storage advised as huge pages:
+    // their first touch (from the host threads) faults once per 2 MB
+    T *allocate(size_t n) {
+        const size_t bytes = n * sizeof(T);
+        if (bytes < (size_t(64) << 20)) return std::allocator<T>::allocate(n);
+        constexpr size_t HP = size_t(2) << 20;
+        void *p = std::aligned_alloc(HP, (bytes + HP - 1) / HP * HP);
+        if (!p) throw std::bad_alloc();
+        madvise(p, (bytes + HP - 1) / HP * HP, MADV_HUGEPAGE);
+        return (T *)p;
+    }
+    void deallocate(T *p, size_t n) {
+        if (n * sizeof(T) < (size_t(64) << 20)) std::allocator<T>::deallocate(p, n);
+        else std::free(p);
+    }
     template <class U, class... A> void construct(U *p, A &&...a) {
         if constexpr (sizeof...(A) == 0) ::new ((void *)p) U;
         else ::new ((void *)p) U(std::forward<A>(a)...);

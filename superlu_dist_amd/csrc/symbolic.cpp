@@ -16,6 +16,8 @@
 // order decides the order of each supernode's L subscripts, and pddistribute
 // lays the factor blocks out in that order.
 #include <algorithm>
+#include <atomic>
+#include <memory>
 #include <chrono>
 #include <cstdio>
 #include <cstdint>
@@ -209,7 +211,8 @@ struct Walker {
     const I *cb, *ce;
     const T *ri;
     I maxsuper;
-    vector<T> xsup, supno, marker, repfnz, parent, segrep, lsub, usub;
+    vector<T> xsup, supno, marker, repfnz, parent, segrep;
+    std::vector<T, NoInit<T>> lsub, usub; // (grown without zeroing: written before read)
     vector<I> xlsub, xusub, xprune, xplore;
     I nextu = 0;
 
@@ -431,6 +434,9 @@ struct Walker {
     I cur_fs = 0, last_len = 0, tail_sum = 0;          // tail_sum: classic sizes past the first list
     I lbelow = 0; // rows of the list below the next column (1; a relaxed copy: its width)
     T lmin = 0;   // smallest row of the list (the representative's first nonzero row bound)
+    // no current supernode: the one before column j was closed by close_at(j)
+    // (a subtree task's first column, or the column after an imported task)
+    bool closed = false;
 
     void vinit() {
         cur.assign(m, (T)-3);
@@ -475,6 +481,7 @@ struct Walker {
         }
         cur_s = s;
         cur_fs = fs;
+        closed = false;
         last_len = b - a;
         tail_sum = rep > fs ? b - a : 0;
         lbelow = 0;
@@ -497,7 +504,7 @@ struct Walker {
     I column_v(I j) {
         const T tj = (T)j;
         I ns = supno[j];
-        const bool prev = j > 0; // a current supernode (columns cur_fs .. j-1) exists
+        const bool prev = j > 0 && !closed; // a current supernode (columns cur_fs .. j-1) exists
         const T sc = prev ? cur_s : (T)-2;
         const I start = !prev ? xlsub[j] : (j - 1 > cur_fs ? xlsub[cur_fs + 1] + last_len : xlsub[cur_fs + 1]);
         I nextl = start, nseg = 0, split = -1, p_in = 0;
@@ -622,13 +629,15 @@ struct Walker {
             }
             // the current supernode ends at j - 1: its last list where the
             // classic compaction leaves it
-            if (j - 1 > cur_fs) {
-                const I to = xlsub[cur_fs + 1];
-                l_write(to, (T)0, (T)-4); // (every row: no mark equals -4)
-                xlsub[j - 1] = to;
-                xprune[j - 1] = to + last_len;
+            if (!closed) {
+                if (j - 1 > cur_fs) {
+                    const I to = xlsub[cur_fs + 1];
+                    l_write(to, (T)0, (T)-4); // (every row: no mark equals -4)
+                    xlsub[j - 1] = to;
+                    xprune[j - 1] = to + last_len;
+                }
+                set_rep(cur_fs, j - 1);
             }
-            set_rep(cur_fs, j - 1);
             // L(:, j) in full: P, the virtual part, then Q
             if (split >= 0) {
                 const I nq = nexp - split;
@@ -686,9 +695,18 @@ struct Walker {
         }
         vinit();
         for (I j = a; j < b;) {
+            if (sub_i < subs.size() && subs[sub_i].first == j) { // a subtree searched by its own Walker
+                close_at(j, rend);
+                const auto ti0 = std::chrono::steady_clock::now();
+                j = import_task(*subs[sub_i].second);
+                subs[sub_i].second->free();
+                ++sub_i;
+                t_import += std::chrono::duration<double>(std::chrono::steady_clock::now() - ti0).count();
+                continue;
+            }
             if (rend[j] != NONE) {
                 const I k = rend[j];
-                if (j > 0) finish_current(j);
+                if (j > 0 && !closed) finish_current(j);
                 relaxed(j, k);
                 for (I i = j; i <= k; ++i) pivot(i);
                 start_supernode(j, k);
@@ -705,7 +723,111 @@ struct Walker {
                 ++j;
             }
         }
-        if (b > a) finish_current(b);
+        if (b > a) close_at(b, rend);
+    }
+
+    // Closes the current supernode as column j's processing would in the
+    // sequential search, j being a column that cannot extend it (the first
+    // column of a subtree that is not the one ending at j - 1's parent, or
+    // the end): before a relaxed supernode or at the end finish_current,
+    // else what column_v does for a column that does not join.  Leaves
+    // xlsub[j] at where column j's list starts.
+    void close_at(I j, const I *rend) {
+        if (closed || j == 0) return;
+        if (j >= mn_ || rend[j] != NONE) {
+            finish_current(j);
+        } else {
+            if (j - 1 > cur_fs) {
+                const I to = xlsub[cur_fs + 1];
+                reserve(to, last_len);
+                l_write(to, (T)0, (T)-4);
+                xlsub[j - 1] = to;
+                xprune[j - 1] = to + last_len;
+                xlsub[j] = to + last_len;
+            } else {
+                xlsub[j] = xlsub[cur_fs + 1];
+            }
+            set_rep(cur_fs, j - 1);
+        }
+        cur_s = (T)-2;
+        closed = true;
+    }
+
+    // ---- subtree tasks: a subtree [lo, hi] of the postordered etree whose
+    // root's next column is not its parent searched by its own Walker (the
+    // search of a column only reaches its descendants), then its arrays
+    // imported here at the positions and supernode numbers the sequential
+    // search would have given them (tests/test_symbolic.py: identical arrays)
+    struct TaskOut {
+        I lo = 0, hi = -1, nsup = 0, nl = 0, nu = 0;
+        vector<T> supno, xsup, repc, lsub, usub; // supno: lo..hi+1; xsup: 0..nsup
+        vector<I> xlsub, xprune, xusub;          // lo..hi+1 (xusub: lo+1..hi+1)
+        void free() {
+            *this = TaskOut();
+        }
+    };
+    // the subtrees inside this Walker's range searched before it (first
+    // column, result), in column order
+    vector<std::pair<I, TaskOut *>> subs;
+    size_t sub_i = 0;
+    double t_import = 0;
+    I mn_ = 0;
+
+    // this Walker as a task over [lo, hi] (fresh): local supernode numbers
+    // from 0, positions from 0
+    std::unique_ptr<TaskOut> run_task(I lo, I hi, const I *rend) {
+        supno[lo] = (T)NONE;
+        xsup[0] = (T)lo;
+        xlsub[lo] = 0;
+        xusub[lo] = 0;
+        nextu = 0;
+        closed = true;
+        run(lo, hi + 1, rend);
+        auto o = std::make_unique<TaskOut>();
+        o->lo = lo;
+        o->hi = hi;
+        o->nsup = (I)supno[hi + 1] + 1;
+        o->nl = xlsub[hi + 1];
+        o->nu = nextu;
+        o->supno.assign(supno.begin() + lo, supno.begin() + hi + 2);
+        o->xsup.assign(xsup.begin(), xsup.begin() + o->nsup + 1);
+        o->repc.assign(repc.begin() + lo, repc.begin() + hi + 1);
+        o->lsub.assign(lsub.begin(), lsub.begin() + o->nl);
+        o->usub.assign(usub.begin(), usub.begin() + o->nu);
+        o->xlsub.assign(xlsub.begin() + lo, xlsub.begin() + hi + 2);
+        o->xprune.assign(xprune.begin() + lo, xprune.begin() + hi + 1);
+        o->xusub.assign(xusub.begin() + lo, xusub.begin() + hi + 2);
+        return o;
+    }
+
+    // a finished task's arrays into this (closed) Walker; returns hi + 1
+    I import_task(const TaskOut &o) {
+        const I lo = o.lo, hi = o.hi, off = xlsub[lo], uoff = nextu;
+        const T soff = (T)(supno[lo] + 1); // (supno[0] = NONE: the first supernode is 0)
+        reserve(off, o.nl);
+        parallel_for((int)((o.nl + (1 << 22) - 1) >> 22), [&](int t) {
+            const I a = (I)t << 22, b = std::min<I>(o.nl, (I)(t + 1) << 22);
+            std::copy(o.lsub.begin() + a, o.lsub.begin() + b, lsub.begin() + off + a);
+        }, 1);
+        if (uoff + o.nu > (I)usub.size()) usub.resize(std::max<I>(2 * usub.size(), uoff + o.nu + 1024));
+        parallel_for((int)((o.nu + (1 << 22) - 1) >> 22), [&](int t) {
+            const I a = (I)t << 22, b = std::min<I>(o.nu, (I)(t + 1) << 22);
+            std::copy(o.usub.begin() + a, o.usub.begin() + b, usub.begin() + uoff + a);
+        }, 1);
+        nextu = uoff + o.nu;
+        for (I c = lo; c <= hi; ++c) {
+            supno[c] = o.supno[c - lo] + soff;
+            xlsub[c] = o.xlsub[c - lo] + off;
+            xprune[c] = o.xprune[c - lo] + off;
+            repc[c] = o.repc[c - lo];
+            xusub[c + 1] = o.xusub[c + 1 - lo] + uoff;
+        }
+        supno[hi + 1] = o.supno[hi + 1 - lo] + soff;
+        xlsub[hi + 1] = o.xlsub[hi + 1 - lo] + off;
+        for (I sn = 0; sn <= o.nsup; ++sn) xsup[soff + sn] = o.xsup[sn];
+        cur_s = (T)-2;
+        closed = true;
+        return hi + 1;
     }
 
     // before a relaxed supernode at column j (or at the end, j = b): the
@@ -728,6 +850,81 @@ struct Walker {
     }
 };
 
+// Subtree tasks for the host threads.  The search of a column only reaches
+// its descendants when every entry A(r, j), r < j, has r in j's subtree
+// (checked here; if not, no tasks).  A task is a subtree of between tmin and
+// tmax columns whose root is not its parent's last child -- so the column
+// after it is not the root's parent and cannot extend the subtree's last
+// supernode -- and that does not start inside a relaxed supernode; the
+// search in column order imports its arrays when it gets there.  (Tasks
+// inside tasks, to take the upper separators' siblings off the ordered
+// search too, measured slower: every level waits for its slowest subtree
+// and the nested imports copy the lists again, 11.2 -> 12.4 s at 100^3 in
+// the build container.)  SLU_SYMB_TASKS=0: none; SLU_SYMB_TASK_MIN / _MAX:
+// the bounds (default 1024 and max(4096, n / (4 threads))).
+struct SymbTask {
+    I lo, hi;
+    int depth;
+    vector<int> subs; // direct subtasks, in column order (none: the tasks are flat)
+};
+static void plan_tasks(I n, const I *parent, const I *cb, const I *ce, const I *ri, const I *rend,
+                       vector<SymbTask> &tasks, vector<int> &top) {
+    tasks.clear();
+    top.clear();
+    auto env = [](const char *k, I d) {
+        const char *e = getenv(k);
+        return e ? (I)atoll(e) : d;
+    };
+    if (env("SLU_SYMB_TASKS", 1) == 0) return;
+    if (const char *cl = getenv("SLU_SYMB_CLASSIC"); cl && atoi(cl) == 1) return;
+    const I tmin = std::max<I>(2, env("SLU_SYMB_TASK_MIN", 1024));
+    const I tmax = std::max<I>(tmin, env("SLU_SYMB_TASK_MAX", std::max<I>(4096, n / (4 * plan_threads()))));
+    if (n < 2 * tmin) return;
+    vector<I> desc(n + 1, 0);
+    for (I j = 0; j < n; ++j) {
+        if (parent[j] <= j || parent[j] > n) return; // not a postordered forest
+        desc[parent[j]] += desc[j] + 1;
+    }
+    std::atomic<bool> ok(true);
+    parallel_for((int)((n + 4095) / 4096), [&](int t) {
+        for (I j = (I)t * 4096; j < std::min<I>(n, (I)(t + 1) * 4096); ++j)
+            for (I p = cb[j]; p < ce[j]; ++p)
+                if (ri[p] < j && ri[p] < j - desc[j]) ok = false;
+    }, 1);
+    if (!ok) return;
+    // the last column of the relaxed supernode each column lies in (NONE: none)
+    vector<I> inrel(n, NONE);
+    for (I f = 0; f < n; ++f)
+        if (rend[f] != NONE)
+            for (I c = f; c <= rend[f]; ++c) inrel[c] = rend[f];
+    vector<I> head(n + 1, NONE), next(n, NONE); // children in increasing order
+    for (I v = n - 1; v >= 0; --v) {
+        next[v] = head[parent[v]];
+        head[parent[v]] = v;
+    }
+    vector<I> stack;
+    for (I c = head[n]; c != NONE; c = next[c]) stack.push_back(c);
+    while (!stack.empty()) {
+        const I v = stack.back();
+        stack.pop_back();
+        const I size = desc[v] + 1;
+        if (size < tmin) continue;                      // small: searched in column order
+        if (inrel[v] != NONE && inrel[v] != v) continue; // inside a relaxed supernode: likewise
+        const bool closable = parent[v] == n || v + 1 != parent[v];
+        if (size <= tmax && closable) {
+            tasks.push_back({v - desc[v], v, 1, {}});
+            continue;
+        }
+        for (I c = head[v]; c != NONE; c = next[c]) stack.push_back(c);
+    }
+    if (tasks.size() < 2) {
+        tasks.clear();
+        return;
+    }
+    std::sort(tasks.begin(), tasks.end(), [](const SymbTask &x, const SymbTask &y) { return x.lo < y.lo; });
+    for (int i = 0; i < (int)tasks.size(); ++i) top.push_back(i);
+}
+
 // symbfact (SRC/symbfact.c:81-215).  m x n matrix, columns [cb[j], ce[j])
 // of ri (A Pc', rows relabelled by perm_c); etree postordered.
 template <class T>
@@ -747,14 +944,62 @@ static Result symbfact_t(I m, I n, const I *cb, const I *ce, const I *ri64, cons
     const vector<I> rend = relaxed_ends(n, etree, relax);
 
     const auto t0 = std::chrono::steady_clock::now();
+    auto setup = [&](Walker<T> &w) {
+        w.m = m;
+        w.cb = cb;
+        w.ce = ce;
+        w.ri = ri.data();
+        w.maxsuper = maxsuper;
+        w.mn_ = mn;
+    };
+    // subtree tasks on the host threads, deepest first; each Walker imports
+    // its direct subtasks' arrays (identical arrays; SLU_SYMB_TASKS=0: one
+    // search in column order)
+    vector<SymbTask> tasks;
+    vector<int> top_tasks;
+    if (m == n) plan_tasks(n, etree, cb, ce, ri64, rend.data(), tasks, top_tasks);
     Walker<T> w(m, n, std::max<I>(4 * annz, 1024));
-    w.m = m;
-    w.cb = cb;
-    w.ce = ce;
-    w.ri = ri.data();
-    w.maxsuper = maxsuper;
+    setup(w);
+    using Out = typename Walker<T>::TaskOut;
+    vector<std::unique_ptr<Out>> outs(tasks.size());
+    bool seq = tasks.empty();
+    if (!seq) {
+        try {
+            int dmax = 0;
+            for (auto &t : tasks) dmax = std::max(dmax, t.depth);
+            for (int d = dmax; d >= 1; --d) {
+                vector<int> lv;
+                for (int i = 0; i < (int)tasks.size(); ++i)
+                    if (tasks[i].depth == d) lv.push_back(i);
+                parallel_for((int)lv.size(), [&](int q) {
+                    const SymbTask &t = tasks[lv[q]];
+                    I nz = 0;
+                    for (I c = t.lo; c <= t.hi; ++c) nz += ce[c] - cb[c];
+                    Walker<T> tw(m, n, std::max<I>(4 * nz, 1024));
+                    setup(tw);
+                    for (int si : t.subs) tw.subs.push_back({tasks[si].lo, outs[si].get()});
+                    outs[lv[q]] = tw.run_task(t.lo, t.hi, rend.data());
+                }, 1);
+            }
+            for (int si : top_tasks) w.subs.push_back({tasks[si].lo, outs[si].get()});
+            I total = 0, totu = 0; // the imported lists at once, not by doublings
+            for (int si : top_tasks) {
+                total += outs[si]->nl;
+                totu += outs[si]->nu;
+            }
+            if ((I)w.lsub.size() < total + 4 * annz) w.lsub.resize(total + 4 * annz);
+            if ((I)w.usub.size() < totu + 2 * annz) w.usub.resize(totu + 2 * annz);
+        } catch (const std::exception &) {
+            seq = true; // (the search in column order reports the first failing column)
+            w.subs.clear();
+        }
+    }
+    if (getenv("SLU_SYMB_TIME") && !seq)
+        fprintf(stderr, "symbfact: %zu subtree tasks (%zu at the top) %.3f s\n", tasks.size(), top_tasks.size(),
+                std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
     w.run(0, mn, rend.data());
     const auto t1 = std::chrono::steady_clock::now();
+    if (getenv("SLU_SYMB_TIME") && !seq) fprintf(stderr, "symbfact: imports %.3f s\n", w.t_import);
 
     g_last_epilogue = 0;
     if constexpr (std::is_same<T, int32_t>::value) {

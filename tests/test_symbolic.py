@@ -201,6 +201,68 @@ def test_symbfact_virtual_last_list_3d_stencil(monkeypatch):
         assert s.nsupers < n
 
 
+def _tasks_vs_ordered(n, cb, ce, ri, etree, relax, maxsup, monkeypatch, tmin, tmax):
+    monkeypatch.setenv("SLU_SYMB_TASKS", "0")
+    a = S.symbfact(n, n, cb, ce, ri, etree, relax, maxsup)
+    monkeypatch.setenv("SLU_SYMB_TASKS", "1")
+    monkeypatch.setenv("SLU_SYMB_TASK_MIN", str(tmin))
+    monkeypatch.setenv("SLU_SYMB_TASK_MAX", str(tmax))
+    b = S.symbfact(n, n, cb, ce, ri, etree, relax, maxsup)
+    for f in ("xsup", "supno", "xlsub", "lsub", "xusub", "usub"):
+        np.testing.assert_array_equal(getattr(a, f), getattr(b, f), err_msg=f)
+    assert (a.ret, a.nnzL, a.nnzU, a.nnzLU) == (b.ret, b.nnzL, b.nnzU, b.nnzLU)
+    return b
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_symbfact_subtree_tasks_match_reference(name, monkeypatch):
+    """Subtree tasks forced down to a few columns (csrc/symbolic.cpp,
+    plan_tasks / import_task): every array still the REFERENCE's."""
+    monkeypatch.setenv("SLU_SYMB_TASK_MIN", "2")
+    g = _load(name)
+    n = int(g["meta"][0])
+    monkeypatch.setenv("SLU_SYMB_TASK_MAX", str(max(2, n // 16)))
+    test_symbfact_matches_reference(name)
+
+
+@pytest.mark.parametrize("relax,maxsup", [(60, 256), (4, 16), (1, 1), (8, 20)])
+@pytest.mark.parametrize("tmin,tmax", [(2, 40), (8, 300), (64, 2000)])
+def test_symbfact_subtree_tasks_equal_column_order(relax, maxsup, tmin, tmax, monkeypatch):
+    """A 20^3 nested-dissection Laplacian and a 12^3 27-point one: the
+    search with subtree tasks gives the same arrays as the one in column
+    order, for several relax / maxsup and task sizes."""
+    from superlu_dist_amd.frontend import STENCIL_3D7, STENCIL_3D27, Csc, nd_order
+    for st, k in ((STENCIL_3D7, 20), (STENCIL_3D27, 12)):
+        A = Csc.stencil(st, k, k, k)
+        cp, ri, _ = A.arrays()
+        co = S.sp_colorder(A.n, A.n, cp, ri, nd_order(k, k, k), S.MY_PERMC)
+        rr = S.relabel_rows(ri, co.perm_c)
+        _tasks_vs_ordered(A.n, co.colbeg, co.colend, rr, co.etree, relax, maxsup, monkeypatch, tmin, tmax)
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_symbfact_subtree_tasks_unsymmetric(seed, monkeypatch):
+    """Random unsymmetric patterns (the A'+A and A'A etrees): tasks where
+    the pattern allows them, the same arrays either way."""
+    rng = np.random.default_rng(100 + seed)
+    n = int(rng.integers(300, 900))
+    cols = []
+    for c in range(n):
+        rows = set(rng.integers(0, n, int(rng.integers(1, 5))).tolist()) | {c}
+        if c > 0 and rng.random() < 0.7:
+            rows.add(c - 1)
+        cols.append(list(rows))
+    colptr = np.zeros(n + 1, np.int64)
+    colptr[1:] = np.cumsum([len(c) for c in cols])
+    rowind = np.array([r for c in cols for r in c], np.int64)
+    perm = rng.permutation(n).astype(np.int64)
+    for colperm in (S.MMD_AT_PLUS_A, S.MMD_ATA):
+        co = S.sp_colorder(n, n, colptr, rowind, perm, colperm)
+        rr = S.relabel_rows(rowind, co.perm_c)
+        for relax, maxsup in ((1, 3), (4, 10)):
+            _tasks_vs_ordered(n, co.colbeg, co.colend, rr, co.etree, relax, maxsup, monkeypatch, 2, 30)
+
+
 def _epilogue_device():
     from superlu_dist_amd.lib import lib
     return int(lib().slu_symbfact_last_epilogue_device())
