@@ -1707,6 +1707,10 @@ k_trsm_reg(const TrsmItemF<T> *items) {
     __shared__ T sD[PW][PW + 1];
     const int rl = lane & 15, kq = lane >> 4;
     const int myr = wid * 16 + rl;
+    // fp64: the block products computed transposed (their C layout is then
+    // the A layout X lives in); fp32's C layout differs, so it goes through
+    // the per-wave LDS tile
+    constexpr bool TRANSPOSED = std::is_same<T, double>::value;
     const bool rv = myr < it.nrows;
     int64_t rbase = 0;
     int t0 = 0;
@@ -1823,11 +1827,39 @@ k_trsm_reg(const TrsmItemF<T> *items) {
                 }
                 // (the scheduler would sink the reads back to their uses)
                 __builtin_amdgcn_sched_barrier(0);
-                M::step(a0, xa[s], b0);
-                M::step(a1, xa[s], b1);
+                if constexpr (TRANSPOSED) { // (X T)^T = T^T X^T
+                    M::step(a0, b0, xa[s]);
+                    M::step(a1, b1, xa[s]);
+                } else {
+                    M::step(a0, xa[s], b0);
+                    M::step(a1, xa[s], b1);
+                }
                 __builtin_amdgcn_sched_barrier(0);
             }
         }
+        if constexpr (TRANSPOSED) {
+            // the products' transposes in C layout are X_b's own A layout
+            // (fp64: lane l holds rows l & 15, columns (l >> 4) + 4 i): Z and
+            // Z Dinv_b need no trip through LDS
+            TR_PROBE(2);
+            T za[8];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                za[i] = Sx::sub(xa[8 * b + i], M::get(a0, i));
+                za[4 + i] = Sx::sub(xa[8 * b + 4 + i], M::get(a1, i));
+            }
+            typename M::acc_t c0 = M::zero(), c1 = M::zero();
+#pragma unroll
+            for (int s = 0; s < 8; ++s) {
+                M::step(c0, sD[4 * s + kq][rl], za[s]);
+                M::step(c1, sD[4 * s + kq][16 + rl], za[s]);
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                xa[8 * b + i] = M::get(c0, i);
+                xa[8 * b + 4 + i] = M::get(c1, i);
+            }
+        } else {
         __syncthreads(); // every wave is done with sT before W (= its first rows) is written
         TR_PROBE(2);
         // Z = X_b - acc: acc (C layout) -> LDS, read back in A layout
@@ -1862,6 +1894,7 @@ k_trsm_reg(const TrsmItemF<T> *items) {
         wave_lds_sync();
 #pragma unroll
         for (int s = 0; s < 8; ++s) xa[8 * b + s] = W[rl][4 * s + kq];
+        }
         if (PF) {
 #pragma unroll
             for (int s = 8 * b; s < 8 * b + 8; ++s) {
