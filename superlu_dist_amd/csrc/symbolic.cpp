@@ -863,14 +863,11 @@ struct Walker {
 // the build container.)  SLU_SYMB_TASKS=0: none; SLU_SYMB_TASK_MIN / _MAX:
 // the bounds (default 1024 and max(4096, n / 8)).
 struct SymbTask {
-    I lo, hi;
-    int depth;
-    vector<int> subs; // direct subtasks, in column order (none: the tasks are flat)
+    I lo, hi; // the subtree's columns
 };
 static void plan_tasks(I n, const I *parent, const I *cb, const I *ce, const I *ri, const I *rend,
-                       vector<SymbTask> &tasks, vector<int> &top) {
+                       vector<SymbTask> &tasks) {
     tasks.clear();
-    top.clear();
     auto env = [](const char *k, I d) {
         const char *e = getenv(k);
         return e ? (I)atoll(e) : d;
@@ -915,7 +912,7 @@ static void plan_tasks(I n, const I *parent, const I *cb, const I *ce, const I *
         if (inrel[v] != NONE && inrel[v] != v) continue; // inside a relaxed supernode: likewise
         const bool closable = parent[v] == n || v + 1 != parent[v];
         if (size <= tmax && closable) {
-            tasks.push_back({v - desc[v], v, 1, {}});
+            tasks.push_back({v - desc[v], v});
             continue;
         }
         for (I c = head[v]; c != NONE; c = next[c]) stack.push_back(c);
@@ -925,7 +922,6 @@ static void plan_tasks(I n, const I *parent, const I *cb, const I *ce, const I *
         return;
     }
     std::sort(tasks.begin(), tasks.end(), [](const SymbTask &x, const SymbTask &y) { return x.lo < y.lo; });
-    for (int i = 0; i < (int)tasks.size(); ++i) top.push_back(i);
 }
 
 // symbfact (SRC/symbfact.c:81-215).  m x n matrix, columns [cb[j], ce[j])
@@ -955,12 +951,10 @@ static Result symbfact_t(I m, I n, const I *cb, const I *ce, const I *ri64, cons
         w.maxsuper = maxsuper;
         w.mn_ = mn;
     };
-    // subtree tasks on the host threads, deepest first; each Walker imports
-    // its direct subtasks' arrays (identical arrays; SLU_SYMB_TASKS=0: one
-    // search in column order)
+    // the subtree tasks on the host threads, then the search in column order
+    // importing their arrays (identical arrays; SLU_SYMB_TASKS=0: no tasks)
     vector<SymbTask> tasks;
-    vector<int> top_tasks;
-    if (m == n) plan_tasks(n, etree, cb, ce, ri64, rend.data(), tasks, top_tasks);
+    if (m == n) plan_tasks(n, etree, cb, ce, ri64, rend.data(), tasks);
     Walker<T> w(m, n, std::max<I>(4 * annz, 1024));
     setup(w);
     using Out = typename Walker<T>::TaskOut;
@@ -968,27 +962,19 @@ static Result symbfact_t(I m, I n, const I *cb, const I *ce, const I *ri64, cons
     bool seq = tasks.empty();
     if (!seq) {
         try {
-            int dmax = 0;
-            for (auto &t : tasks) dmax = std::max(dmax, t.depth);
-            for (int d = dmax; d >= 1; --d) {
-                vector<int> lv;
-                for (int i = 0; i < (int)tasks.size(); ++i)
-                    if (tasks[i].depth == d) lv.push_back(i);
-                parallel_for((int)lv.size(), [&](int q) {
-                    const SymbTask &t = tasks[lv[q]];
-                    I nz = 0;
-                    for (I c = t.lo; c <= t.hi; ++c) nz += ce[c] - cb[c];
-                    Walker<T> tw(m, n, std::max<I>(4 * nz, 1024));
-                    setup(tw);
-                    for (int si : t.subs) tw.subs.push_back({tasks[si].lo, outs[si].get()});
-                    outs[lv[q]] = tw.run_task(t.lo, t.hi, rend.data());
-                }, 1);
-            }
-            for (int si : top_tasks) w.subs.push_back({tasks[si].lo, outs[si].get()});
-            I total = 0, totu = 0; // the imported lists at once, not by doublings
-            for (int si : top_tasks) {
-                total += outs[si]->nl;
-                totu += outs[si]->nu;
+            parallel_for((int)tasks.size(), [&](int q) {
+                const SymbTask &t = tasks[q];
+                I nz = 0;
+                for (I c = t.lo; c <= t.hi; ++c) nz += ce[c] - cb[c];
+                Walker<T> tw(m, n, std::max<I>(4 * nz, 1024));
+                setup(tw);
+                outs[q] = tw.run_task(t.lo, t.hi, rend.data());
+            }, 1);
+            I total = 0, totu = 0; // room for the imported lists at once, not by doublings
+            for (size_t q = 0; q < tasks.size(); ++q) {
+                w.subs.push_back({tasks[q].lo, outs[q].get()});
+                total += outs[q]->nl;
+                totu += outs[q]->nu;
             }
             if ((I)w.lsub.size() < total + 4 * annz) w.lsub.resize(total + 4 * annz);
             if ((I)w.usub.size() < totu + 2 * annz) w.usub.resize(totu + 2 * annz);
@@ -998,7 +984,7 @@ static Result symbfact_t(I m, I n, const I *cb, const I *ce, const I *ri64, cons
         }
     }
     if (getenv("SLU_SYMB_TIME") && !seq)
-        fprintf(stderr, "symbfact: %zu subtree tasks (%zu at the top) %.3f s\n", tasks.size(), top_tasks.size(),
+        fprintf(stderr, "symbfact: %zu subtree tasks %.3f s\n", tasks.size(),
                 std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
     w.run(0, mn, rend.data());
     const auto t1 = std::chrono::steady_clock::now();
