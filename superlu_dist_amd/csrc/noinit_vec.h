@@ -21,11 +21,16 @@ template <class T> struct NoInit : std::allocator<T> {
     };
     // arrays of 64 MB and more on 2 MB-aligned storage advised as huge pages:
     // their first touch (from the host threads) faults once per 2 MB, and the
-    // symbolic search's random reads of the lists miss the TLB less (1.77 ->
-    // 1.36 s of symbolic phase at 100^3 on the box)
+    // symbolic search's random reads of the lists miss the TLB less (1.76 ->
+    // 1.37-1.44 s of symbolic phase at 100^3 on the box, the following first
+    // pdgstrf 816-840 -> 846-916 ms: profiles/r06thp/; SLU_NOINIT_THP=0 off)
     T *allocate(size_t n) {
         const size_t bytes = n * sizeof(T);
-        if (bytes < (size_t(64) << 20)) return std::allocator<T>::allocate(n);
+        static const bool thp = [] {
+            const char *e = std::getenv("SLU_NOINIT_THP"); // (=0: plain allocation, A/B)
+            return !(e && e[0] == '0');
+        }();
+        if (!thp || bytes < (size_t(64) << 20)) return std::allocator<T>::allocate(n);
         constexpr size_t HP = size_t(2) << 20;
         void *p = std::aligned_alloc(HP, (bytes + HP - 1) / HP * HP);
         if (!p) throw std::bad_alloc();
@@ -33,7 +38,11 @@ template <class T> struct NoInit : std::allocator<T> {
         return (T *)p;
     }
     void deallocate(T *p, size_t n) {
-        if (n * sizeof(T) < (size_t(64) << 20)) std::allocator<T>::deallocate(p, n);
+        static const bool thp = [] {
+            const char *e = std::getenv("SLU_NOINIT_THP");
+            return !(e && e[0] == '0');
+        }();
+        if (!thp || n * sizeof(T) < (size_t(64) << 20)) std::allocator<T>::deallocate(p, n);
         else std::free(p);
     }
     template <class U, class... A> void construct(U *p, A &&...a) {
