@@ -480,6 +480,12 @@ bool Amalg::build(int64_t n_, int ns, const int_t *xsup, const int_t *const *lid
     return true;
 }
 
+void Amalg::set_index(const int_t *const *lidx, const int_t *const *uidx) {
+    SLU_REQUIRE(work, "amalgamation: no deferred programs to build");
+    work->lidx = lidx;
+    work->uidx = uidx;
+}
+
 Amalg::Amalg() = default;
 Amalg::~Amalg() = default;
 

@@ -153,6 +153,9 @@ struct Amalg {
                const int_t *const *uidx, double zero_frac, int maxw);
     bool defer_programs = false;
     void build_programs();
+    // the LUstruct's index arrays for a deferred build_programs(): the
+    // pointer tables build() was given need not outlive it
+    void set_index(const int_t *const *lidx, const int_t *const *uidx);
     Amalg();
     ~Amalg();
     Amalg(const Amalg &) = delete;

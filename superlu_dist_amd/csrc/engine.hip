@@ -4348,13 +4348,22 @@ struct AmalgPlan : PlanBase {
             P->t_amalg = ms_since(ta);
             tick("analysis");
             // the relayout programs (host pass 4; beside the coarse plan's
-            // build it only slowed both down on the box's 16 cores)
-            P->A.build_programs();
-            tick("programs (host)");
+            // build it only slowed both down on the box's 16 cores).  Only an
+            // upload or a download of the caller-layout values runs them: a
+            // plan fed by fill_a whose factors stay in HBM (the device-
+            // resident drop-in) builds them when one first happens
+            const bool progs_now = P->opts.overlap_upload || P->opts.overlap_download;
+            if (progs_now) {
+                P->A.build_programs();
+                tick("programs (host)");
+            }
             P->build_inner();
             tick("coarse plan");
-            P->build_programs();
-            tick("relayout programs");
+            if (progs_now) {
+                P->build_programs();
+                P->progs = true;
+                tick("relayout programs");
+            }
             if (P->opts.overlap_download) P->build_d2h();
             tick("d2h programs");
         } catch (...) {
@@ -4397,6 +4406,19 @@ struct AmalgPlan : PlanBase {
     // level as soon as its panels are done): lx / ublks items of the groups
     // of level L at [lx_lev[L], lx_lev[L+1]) / [ub_lev[L], ub_lev[L+1]).
     vector<int> lx_lev, ub_lev; // (ub_lev: U chunks)
+    bool progs = false;         // the relayout programs are built
+    void ensure_programs() {
+        if (progs) return;
+        // (the index pointer tables of the LUstruct as it is now: those
+        // make() had are gone; the structure is the plan's by the cache key)
+        LocalLU *L = LU->Llu;
+        const vector<const int_t *> li(L->Lrowind_bc_ptr, L->Lrowind_bc_ptr + ns),
+            ui(L->Ufstnz_br_ptr, L->Ufstnz_br_ptr + ns);
+        A.set_index(li.data(), ui.data());
+        A.build_programs();
+        build_programs();
+        progs = true;
+    }
     void build_programs() {
         const int nl = (int)in->levels.size();
         auto lev = [&](int s) { return in->level_of[A.grp[s]]; };
@@ -4484,6 +4506,7 @@ struct AmalgPlan : PlanBase {
 
     // levels [L0, L1) of the relayout on stream st
     void relayout_levels(int dir, int L0, int L1, hipStream_t st) {
+        ensure_programs();
         programs_ready();
         const int a = lx_lev[L0], b = lx_lev[L1];
         if (b > a)
