@@ -525,14 +525,6 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    # the device-resident leg models a fresh process's first drop-in call:
-    # its child runs before this process holds the headline's LUstruct and
-    # HBM plan (beside them its plan build took 420 instead of 330 ms)
-    devres = None
-    if (world == 1 and not args.no_abi and not args.roofline_only and args.workload == "lap3d"
-            and args.ordering == "grid" and not args.no_device_resident):
-        log("device-resident drop-in leg (libslu_mi355x_solve.so, child process)")
-        devres = device_resident_leg(args.nx)
     t0 = time.time()
     gname = f"{pr}x{pc}" + (f"x{pz}" if pz > 1 else "")
     log(f"front-end {args.workload} nx={args.nx} grid {gname}")
@@ -621,8 +613,12 @@ def main():
         log("drop-in pdgstrf leg (utime[FACT])")
         abi, gpu_sums = abi_leg(lu, anorm, t_step_local,
                                 fingerprint=gpu_fingerprints if want_cpu else None)
-        if devres is not None:
-            abi["device_resident"] = devres
+        # (a fresh process's first drop-in call, after the headline: on a box
+        # whose HBM no process has mapped yet, the first 16.8 GB allocation
+        # alone takes ~0.5 s instead of ~0.06 s -- DESIGN section 16)
+        if args.workload == "lap3d" and args.ordering == "grid" and not args.no_device_resident:
+            log("device-resident drop-in leg (libslu_mi355x_solve.so, child process)")
+            abi["device_resident"] = device_resident_leg(args.nx)
             abi["device_resident"]["refactor_vs_ms_per_step"] = (
                 round(abi["device_resident"]["utime_fact_ms_refactor"] / t_step_local, 3)
                 if "utime_fact_ms_refactor" in abi["device_resident"] else None)

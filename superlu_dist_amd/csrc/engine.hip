@@ -799,16 +799,39 @@ struct Plan : PlanBase {
         // the panel stream carries the critical path (critical Schur tiles,
         // next level's diag LU / TRSM / exchanges): higher priority, so its
         // workgroups are dispatched ahead of the bulk Schur update's
-        int prio_lo = 0, prio_hi = 0;
-        const auto ts0 = std::chrono::steady_clock::now();
-        HIPCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
-        HIPCHK(hipStreamCreateWithPriority(&stream, hipStreamNonBlocking, prio_lo));
-        HIPCHK(hipStreamCreateWithPriority(&pstream, hipStreamNonBlocking, prio_hi));
-        HIPCHK(hipStreamCreateWithPriority(&ustream, hipStreamNonBlocking, prio_hi));
-        if (xmode) HIPCHK(hipStreamCreateWithPriority(&cstream, hipStreamNonBlocking, prio_hi));
-        if (getenv("SLU_PROFILE_PLAN"))
-            fprintf(stderr, "[slu plan %d] streams               %6.1f ms\n", iam, ms_since(ts0));
-        X.s = pstream;
+        // (created on a helper thread beside the host-side plan build --
+        // the first streams of a process take ~35 ms -- and joined before
+        // their first use)
+        std::string stream_err;
+        std::thread stream_thread([this, &stream_err] {
+            try {
+                if (comm) HIPCHK(hipSetDevice(comm->device));
+                int prio_lo = 0, prio_hi = 0;
+                const auto ts0 = std::chrono::steady_clock::now();
+                HIPCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+                HIPCHK(hipStreamCreateWithPriority(&stream, hipStreamNonBlocking, prio_lo));
+                HIPCHK(hipStreamCreateWithPriority(&pstream, hipStreamNonBlocking, prio_hi));
+                HIPCHK(hipStreamCreateWithPriority(&ustream, hipStreamNonBlocking, prio_hi));
+                if (xmode) HIPCHK(hipStreamCreateWithPriority(&cstream, hipStreamNonBlocking, prio_hi));
+                if (getenv("SLU_PROFILE_PLAN"))
+                    fprintf(stderr, "[slu plan %d] streams               %6.1f ms (helper thread)\n", iam,
+                            ms_since(ts0));
+            } catch (const std::exception &e) {
+                stream_err = e.what();
+            }
+        });
+        struct Joiner { // (an exception before the join must not leave it joinable)
+            std::thread &t;
+            ~Joiner() {
+                if (t.joinable()) t.join();
+            }
+        } stream_joiner{stream_thread};
+        auto join_streams = [&] {
+            if (!stream_thread.joinable()) return;
+            stream_thread.join();
+            SLU_REQUIRE(stream_err.empty(), "%s", stream_err.c_str());
+            X.s = pstream;
+        };
         int_t *hx = LU->Glu_persist->xsup;
         nsupers = (int)(LU->Glu_persist->supno[n - 1] + 1);
         xsup.assign(hx, hx + nsupers + 1);
@@ -832,6 +855,7 @@ struct Plan : PlanBase {
             d_U.alloc_guarded(std::max<i64>(uval_total, 1), SB_UGUARD);
         }
         tick("layout + alloc");
+        if (opts.overlap_upload || xmode || zmode) join_streams();
         if (opts.overlap_upload) {
             // the H2D copy of the values runs beside the rest of the plan
             // build (index exchange, levels, schedule, device tables)
@@ -880,11 +904,13 @@ struct Plan : PlanBase {
                                 "resize %.1f, copy %.1f, tiles %.1f)\n",
                         iam, t_addsn, t_merge, t_resize, t_put, t_tiles);
             tick("build_schedule");
+            join_streams();
             build_device();
             tick("build_device");
             build_d2h();
             tick("build_d2h");
         } catch (...) {
+            if (stream_thread.joinable()) stream_thread.join();
             if (up_thread.joinable()) up_thread.join();
             if (pin_thread.joinable()) pin_thread.join();
             throw;
